@@ -1,0 +1,176 @@
+/*
+ * rlks.h — C ABI of librlks.so, the MI355X (gfx950) rollout-and-training engine for the
+ * rl_scheduler multi-cloud pod scheduler.
+ *
+ * Drop-in boundary.  The reference's hot path sits behind the gymnasium Env API
+ * (K8sMultiCloudEnv, /root/reference/rl_scheduler/env/k8s_multi_cloud_env.py:36-157) and behind
+ * RLlib's PPO Algorithm surface (train(), compute_single_action(), save()/from_checkpoint(),
+ * /root/reference/rl_scheduler/agent/train_ppo.py:9-31, eval_ppo.py:17-27,
+ * final_evaluation.py:32-48).  The Python host package (rl-k8s-scheduler_amd/rlks) keeps that
+ * surface and binds the entry points below with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Every function returns 0 (RLKS_OK) or a negative RLKS_ERR_* code; rlks_last_error() gives
+ *    the message (thread-local).
+ *  - Pointers named *_dev are device (HBM) pointers owned by the caller (torch tensors);
+ *    *_host pointers are host memory.  `stream` is a hipStream_t (NULL = legacy default stream).
+ *  - All device work is enqueued asynchronously on `stream`; no function synchronises the
+ *    device except rlks_env_create/destroy, so every call can be captured in a hipGraph.
+ *  - Handles are not re-entrant: one handle per GPU per host thread.
+ */
+#ifndef RLKS_H
+#define RLKS_H
+
+#include <stdint.h>
+
+#include "rlks_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RLKS_OK 0
+#define RLKS_ERR_ARG (-1)
+#define RLKS_ERR_HIP (-2)
+#define RLKS_ERR_UNSUPPORTED (-3)
+#define RLKS_ERR_STATE (-4)
+
+const char* rlks_last_error(void);
+const char* rlks_version(void);
+
+/* ============================================================== environment (K1 + K2) ==== */
+typedef struct rlks_env rlks_env;
+
+/* K8sMultiCloudEnv.__init__ (:46-66): tables are [n_rows][n_clouds] float64 host arrays with the
+ * exact bits pandas parsed from data/processed/normalized_rl_data.csv (:58).  Allocates the SoA
+ * lane state (step, episode, optional MT19937 state) in HBM.  Synchronises. */
+int rlks_env_create(const rlks_env_cfg* cfg, const double* cost_host, const double* lat_host,
+                    rlks_env** out);
+int rlks_env_destroy(rlks_env* env);
+int rlks_env_config(const rlks_env* env, rlks_env_cfg* out);
+
+/* random.seed(seed) (:109-110) for the lanes in mask (NULL = all), MT19937 mode only:
+ * keys_dev[lane * key_stride + j] are the 32-bit words of abs(seed), little-endian (CPython
+ * random_seed); keylen_dev[lane] is the word count (>= 1). */
+int rlks_env_seed(rlks_env* env, const uint8_t* mask_dev, const uint32_t* keys_dev,
+                  const int32_t* keylen_dev, int key_stride, void* stream);
+
+/* reset() (:106-112) for the lanes in mask (NULL = all): current_step = 0, obs of row 0. */
+int rlks_env_reset(rlks_env* env, const uint8_t* mask_dev, float* obs_dev, void* stream);
+
+/* step(action) (:115-144) for all lanes.  status_dev[0] = invalid actions (when > 0 NO lane
+ * steps: the reference asserts before any change, :116); status_dev[1] = lanes that ran past the
+ * last table row (the reference's IndexError, :91).  reward64 is bit-exact f64 (no FMA);
+ * reward32/truncated/step_out/final_obs may be NULL. */
+int rlks_env_step(rlks_env* env, const int32_t* actions_dev, float* obs_dev, double* reward64_dev,
+                  float* reward32_dev, uint8_t* terminated_dev, uint8_t* truncated_dev,
+                  int32_t* step_out_dev, float* final_obs_dev, int32_t* status_dev, void* stream);
+
+/* Fused action sampling + step for the rollout (RLlib sampler + TorchCategorical): action =
+ * Categorical(logits) via Philox (explore != 0) or argmax (explore == 0, compute_single_action
+ * explore=False); logp of the chosen action; env step; auto-reset; episode-return tracking. */
+int rlks_env_sample_step(rlks_env* env, const float* logits_dev, int explore, int32_t* actions_dev,
+                         float* logp_dev, float* obs_next_dev, float* reward_dev, uint8_t* done_dev,
+                         void* stream);
+
+/* Sum of completed-episode returns and their count over all lanes (double[2]); clear != 0
+ * zeroes the accumulators (PPO result "episode_reward_mean", train_ppo.py:29-30). */
+int rlks_env_episode_stats(rlks_env* env, double* out_dev, int clear, void* stream);
+
+/* copy lane counters (current_step, episode index) into caller buffers (either may be NULL) */
+int rlks_env_lane_state(rlks_env* env, int32_t* steps_dev, int32_t* episodes_dev, void* stream);
+
+/* ============================================================== RNG test surface ========= */
+/* Philox4x32-10 of n counters ctr_dev[n][4] under key_dev[2] -> out_dev[n][4] */
+int rlks_philox4x32_10(const uint32_t* ctr_dev, const uint32_t* key_dev, uint32_t* out_dev, int n,
+                       void* stream);
+/* n draws of CPython random.random() after random.seed(key words) -> out_dev[n] (one lane) */
+int rlks_mt_random(const uint32_t* key_dev, int keylen, double* out_dev, int n, void* stream);
+
+/* ============================================================== advantages (K3) ========== */
+/* RLlib compute_advantages (use_gae=True) over a time-major [T][N] rollout:
+ *   delta_t = r_t + gamma * V_{t+1} * (1 - done_t) - V_t,  A_t = delta_t + gamma*lam*(1-done_t)*A_{t+1}
+ *   vtarg_t = A_t + V_t;  values_dev is [T+1][N] (row T = bootstrap V(s_T)).
+ * partials_dev (may be NULL) receives per-block [sum A, sum A^2] for standardisation. */
+int rlks_gae(const float* rewards_dev, const float* values_dev, const uint8_t* dones_dev, float gamma,
+             float lam, int T, int N, float* adv_dev, float* vtarg_dev, double* partials_dev,
+             void* stream);
+int rlks_gae_partials_count(int N);
+/* sums_dev[3] = {sum A, sum A^2, count} from the partials (deterministic order) */
+int rlks_adv_stats(const double* partials_dev, int n_partials, double count, double* sums_dev,
+                   void* stream);
+/* dyn_dev[ADV_MEAN], dyn_dev[ADV_INVSTD] from (possibly all-reduced) sums (numpy std, ddof=0) */
+int rlks_adv_finalize(const double* sums_dev, float* dyn_dev, void* stream);
+
+/* ============================================================== policy / value MLP (K4) == */
+/* Flat parameter buffer layout (fp32, torch [out][in] weights, each tensor 64-float aligned):
+ *   0 pi.w1 [H][D]  1 pi.b1 [H]  2 pi.w2 [H][H]  3 pi.b2 [H]  4 pi.w3 [A][H]  5 pi.b3 [A]
+ *   6 vf.w1 [H][D]  7 vf.b1 [H]  8 vf.w2 [H][H]  9 vf.b2 [H] 10 vf.w3 [1][H] 11 vf.b3 [1]
+ * (RLlib FCNet with vf_share_layers=False: _hidden_layers/_logits/_value_branch_separate/
+ *  _value_branch.) */
+#define RLKS_N_TENSORS 12
+int rlks_mlp_layout(const rlks_mlp_desc* desc, int64_t* offsets12, int64_t* padded_count,
+                    int64_t* real_count);
+
+/* logits_dev[n][A], values_dev[n] = FCNet forward of obs_dev[n][D] (either output may be NULL) */
+int rlks_policy_forward(const rlks_mlp_desc* desc, const float* params_dev, const float* obs_dev,
+                        int n, float* logits_dev, float* values_dev, void* stream);
+
+/* Rollout buffers, time-major, device pointers */
+typedef struct rlks_rollout_bufs {
+  float* obs;       /* [T+1][N][D] */
+  float* logits;    /* [T][N][A] */
+  float* values;    /* [T+1][N] */
+  int32_t* actions; /* [T][N] */
+  float* logp;      /* [T][N] */
+  float* rewards;   /* [T][N] */
+  uint8_t* dones;   /* [T][N] */
+  float* adv;       /* [T][N] */
+  float* vtarg;     /* [T][N] */
+  int32_t T;
+  int32_t N;
+} rlks_rollout_bufs;
+
+/* T steps of (policy forward -> sample -> env step) into bufs, then the bootstrap values
+ * V(obs[T]).  obs[0] must hold the current observations. */
+int rlks_rollout(rlks_env* env, const rlks_mlp_desc* desc, const float* params_dev,
+                 const rlks_rollout_bufs* bufs, int explore, void* stream);
+
+/* Minibatch rows per packed record: [obs D | logits_old A | adv | vtarg | logp_old | action] */
+int rlks_minibatch_stride(const rlks_mlp_desc* desc);
+/* Gather minibatch rows [row0, row0+rows) of epoch `epoch`'s permutation of the T*N samples
+ * (Philox-keyed Feistel bijection, no sort) into mb_dev; advantages standardised with dyn. */
+int rlks_ppo_gather(const rlks_mlp_desc* desc, const rlks_rollout_bufs* bufs, uint64_t perm_seed,
+                    int epoch, int64_t row0, int rows, const float* dyn_dev, float* mb_dev,
+                    void* stream);
+
+/* Gradient of the RLlib PPO loss (mean over `rows`*world rows via dyn[INV_COUNT]) w.r.t. the
+ * flat parameters -> grad_dev (padded_count floats).  stats_dev (double[RLKS_STAT_SIZE]) gets
+ * the sums for reporting and the KL update.  workspace from rlks_ppo_workspace_bytes. */
+int rlks_ppo_workspace_bytes(const rlks_mlp_desc* desc, int rows, int64_t* bytes);
+int rlks_ppo_grad(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
+                  const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev,
+                  double* stats_dev, void* workspace_dev, int64_t workspace_bytes, void* stream);
+
+/* Same, launching only the phases in `phases` (profiling / benchmarking: each phase reads what the
+ * previous phases left in the workspace). */
+#define RLKS_PHASE_FWD 1    /* F1: forward + head + loss + dZ2 */
+#define RLKS_PHASE_DW2 2    /* F2: dW2 = dZ2^T H1 (split over rows) */
+#define RLKS_PHASE_DH1 4    /* F3: dH1 = dZ2 W2 -> dZ1 -> dW1, db1 partials */
+#define RLKS_PHASE_REDUCE 8 /* fixed-order reduction of all partials (+ stats) */
+#define RLKS_PHASE_ALL 15
+int rlks_ppo_grad_phases(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
+                         const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
+                         void* workspace_dev, int64_t workspace_bytes, int phases, void* stream);
+
+/* torch.optim.Adam step (lerp form of exp_avg, bias-corrected), in place on n floats */
+int rlks_adam_step(float* params_dev, const float* grad_dev, float* m_dev, float* v_dev, int64_t n,
+                   float lr, float beta1, float beta2, float eps, int step, void* stream);
+
+/* RLlib update_kl: kl = stats_sum[0] / stats_sum[1]; x1.5 if kl > 2*target, x0.5 if < target/2 */
+int rlks_kl_update(float* dyn_dev, const double* kl_sum_count_dev, float kl_target, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RLKS_H */

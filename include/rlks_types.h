@@ -1,0 +1,99 @@
+/*
+ * rlks_types.h — plain-C types shared by the HIP library (librlks.so) and the CPU oracle.
+ *
+ * The environment model is the reference's K8sMultiCloudEnv
+ * (/root/reference/rl_scheduler/env/k8s_multi_cloud_env.py:36-157), generalised to C clouds
+ * and batched over n_envs independent lanes.  With n_clouds = 2 and nodes_per_cluster = 0
+ * it is the reference env exactly.  nodes_per_cluster > 0 enables
+ * the node-level extension specified in DESIGN.md §4 (no reference exists).
+ */
+#ifndef RLKS_TYPES_H
+#define RLKS_TYPES_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* cpu-noise / randomness source for the observation's utilisation entries */
+enum {
+  RLKS_NOISE_PHILOX = 0,   /* Philox4x32-10, key = seed, counter = (env, episode, t, purpose) */
+  RLKS_NOISE_MT19937 = 1   /* per-lane CPython MT19937 (random.seed / random.random), bit-exact */
+};
+
+/* Philox counter purposes (ctr[3] high half) */
+enum {
+  RLKS_PURPOSE_OBS = 1,
+  RLKS_PURPOSE_ACTION = 2,
+  RLKS_PURPOSE_ARRIVAL = 3,
+  RLKS_PURPOSE_DEPART = 4,
+  RLKS_PURPOSE_OCCUPANCY = 5
+};
+
+typedef struct rlks_env_cfg {
+  int32_t n_envs;        /* lanes */
+  int32_t n_rows;        /* T: table rows (reference: 100, normalized_rl_data.csv) */
+  int32_t n_clouds;      /* C: clusters / actions (reference: 2, :51) */
+  int32_t max_steps;     /* episode length; reference: len(table) - 1 = 99 (:66) */
+  int32_t noise_mode;    /* RLKS_NOISE_* */
+  int32_t autoreset;     /* 1: terminated lanes reset inside step (vector-env semantics) */
+  int32_t env_offset;    /* global id of lane 0 (multi-GPU shard base; Philox counter word 0) */
+  int32_t reserved0;
+  uint64_t seed;         /* Philox key; also the default MT seed when none is given */
+  double cpu_lo;         /* random.uniform(0.1, 0.8) (:87) */
+  double cpu_hi;
+  double w_cost;         /* reward = scale * (w_cost * cost + w_lat * latency)  (:122) */
+  double w_lat;
+  double scale;
+  /* ---- node-level extension; nodes_per_cluster == 0 disables it ---- */
+  int32_t nodes_per_cluster; /* N nodes per cluster */
+  int32_t pod_cpu_m;         /* pod request, millicores (simple-service.yaml:27: 100m) */
+  int32_t pod_mem_mi;        /* pod request, MiB (simple-service.yaml:28: 64Mi) */
+  int32_t arrival_mode;      /* 0: Poisson(arrival_rate); 1: bursty trace (per-step rates) */
+  double arrival_rate;       /* mean pod arrivals per step */
+  double depart_prob;        /* per-step probability that one pod leaves the chosen cluster */
+  double init_occupancy;     /* initial pods per node ~ U(0, init_occupancy * max_pods) */
+  double reject_penalty;     /* subtracted from reward per rejected pod (0: reference reward) */
+} rlks_env_cfg;
+
+/* Multi-layer-perceptron policy/value description (RLlib FCNet, vf_share_layers=False) */
+typedef struct rlks_mlp_desc {
+  int32_t obs_dim;   /* D  (reference: 6) */
+  int32_t hidden;    /* H  (reference: fcnet_hiddens [256, 256]) */
+  int32_t n_actions; /* A  (reference: 2) */
+  int32_t reserved;
+} rlks_mlp_desc;
+
+/* PPO loss coefficients that stay fixed for a run (RLlib PPOConfig names and defaults) */
+typedef struct rlks_ppo_coeffs {
+  float clip_param;      /* 0.3 */
+  float vf_clip_param;   /* 10.0 */
+  float vf_loss_coeff;   /* 1.0 */
+  float entropy_coeff;   /* 0.0 */
+} rlks_ppo_coeffs;
+
+/* Device-resident per-iteration scalars (float[RLKS_DYN_SIZE]); kernels read them so that no
+ * host round trip is needed between rollout, advantage standardisation and the SGD steps. */
+enum {
+  RLKS_DYN_ADV_MEAN = 0,    /* mean of the train batch's advantages */
+  RLKS_DYN_ADV_INVSTD = 1,  /* 1 / max(1e-4, std)  (RLlib standardize_fields) */
+  RLKS_DYN_KL_COEFF = 2,    /* adaptive KL coefficient (initial 0.2) */
+  RLKS_DYN_INV_COUNT = 3,   /* 1 / global minibatch rows: the loss is a mean */
+  RLKS_DYN_SIZE = 8
+};
+
+/* Per-minibatch loss statistics written by rlks_ppo_grad (double[RLKS_STAT_SIZE], sums) */
+enum {
+  RLKS_STAT_POLICY_LOSS = 0, /* sum of -surrogate */
+  RLKS_STAT_VF_LOSS = 1,     /* sum of clipped squared error */
+  RLKS_STAT_KL = 2,          /* sum of KL(old || new) */
+  RLKS_STAT_ENTROPY = 3,     /* sum of entropy */
+  RLKS_STAT_ROWS = 4,        /* rows */
+  RLKS_STAT_SIZE = 8
+};
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RLKS_TYPES_H */

@@ -1,0 +1,229 @@
+/*
+ * rlks_oracle.c — CPU restatement of the reference environment (TEST INFRASTRUCTURE ONLY).
+ *
+ * This file is the parity CHECKER for the HIP path.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product path (librlks.so) never links it.
+ *
+ * What it restates, line by line of /root/reference/rl_scheduler/env/k8s_multi_cloud_env.py:
+ *   _get_live_cpu  (:84-88)   random.uniform(0.1, 0.8) = 0.1 + (0.8-0.1) * random()
+ *   _get_obs       (:90-103)  f32[ cost[0..C), lat[0..C), cpu[0..C) ] of row current_step
+ *   reset          (:106-112) current_step = 0; random.seed(seed) when seed is given
+ *   step           (:115-144) validate; reward = 100*(0.6*cost + 0.4*lat) of row t (f64, no FMA);
+ *                             t += 1; done = t >= max_steps; obs of row t (IndexError past T-1)
+ * plus CPython's MT19937 (Modules/_randommodule.c: init_genrand, init_by_array, genrand_uint32,
+ * random_random = genrand_res53) for the bit-exact "compat" noise mode, and Philox4x32-10
+ * (Salmon et al., SC'11; Random123) for the counter-based mode.
+ *
+ * Pinned by tests/test_oracle_golden.py against tests/golden/ (generated from the reference env
+ * itself by tools/make_goldens.py).  Build: see oracle/Makefile (gcc -O2 -ffp-contract=off).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/rlks_types.h"
+
+#if defined(__FP_FAST_FMA)
+#error "oracle must be built with -ffp-contract=off (reward must not be FMA-contracted)"
+#endif
+
+/* --------------------------------------------------------------------------- Philox4x32-10 */
+void ro_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+  uint32_t k0 = key_in[0], k1 = key_in[1];
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* 53-bit uniform in [0,1) from two 32-bit words, CPython genrand_res53's construction */
+double ro_u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+/* --------------------------------------------------------------------------- MT19937 */
+#define MT_N 624
+#define MT_M 397
+/* state layout: mt[0..623], mt[624] = mti */
+static void mt_init_genrand(uint32_t* mt, uint32_t s) {
+  mt[0] = s;
+  for (int i = 1; i < MT_N; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+  mt[MT_N] = MT_N;
+}
+
+void ro_mt_seed(uint32_t* mt, const uint32_t* key, int keylen) {
+  mt_init_genrand(mt, 19650218u);
+  int i = 1, j = 0;
+  int k = MT_N > keylen ? MT_N : keylen;
+  for (; k; --k) {
+    mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+    ++i; ++j;
+    if (i >= MT_N) { mt[0] = mt[MT_N - 1]; i = 1; }
+    if (j >= keylen) j = 0;
+  }
+  for (k = MT_N - 1; k; --k) {
+    mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+    ++i;
+    if (i >= MT_N) { mt[0] = mt[MT_N - 1]; i = 1; }
+  }
+  mt[0] = 0x80000000u;
+  mt[MT_N] = MT_N;
+}
+
+uint32_t ro_mt_u32(uint32_t* mt) {
+  static const uint32_t mag01[2] = {0x0u, 0x9908b0dfu};
+  uint32_t y;
+  if (mt[MT_N] >= MT_N) {
+    int kk;
+    for (kk = 0; kk < MT_N - MT_M; ++kk) {
+      y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+      mt[kk] = mt[kk + MT_M] ^ (y >> 1) ^ mag01[y & 1u];
+    }
+    for (; kk < MT_N - 1; ++kk) {
+      y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+      mt[kk] = mt[kk + (MT_M - MT_N)] ^ (y >> 1) ^ mag01[y & 1u];
+    }
+    y = (mt[MT_N - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+    mt[MT_N - 1] = mt[MT_M - 1] ^ (y >> 1) ^ mag01[y & 1u];
+    mt[MT_N] = 0;
+  }
+  y = mt[mt[MT_N]++];
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+double ro_mt_random(uint32_t* mt) {
+  uint32_t a = ro_mt_u32(mt), b = ro_mt_u32(mt);
+  return ro_u53(a, b);
+}
+
+/* --------------------------------------------------------------------------- batched env */
+typedef struct ro_env {
+  rlks_env_cfg cfg;
+  double* cost; /* [T][C] */
+  double* lat;  /* [T][C] */
+  int32_t* step;
+  int32_t* episode;
+  uint32_t* mt; /* [n][625] */
+} ro_env;
+
+ro_env* ro_env_create(const rlks_env_cfg* cfg, const double* cost, const double* lat) {
+  if (!cfg || cfg->n_envs <= 0 || cfg->n_rows <= 0 || cfg->n_clouds <= 0) return NULL;
+  ro_env* e = (ro_env*)calloc(1, sizeof(ro_env));
+  e->cfg = *cfg;
+  size_t tc = (size_t)cfg->n_rows * cfg->n_clouds, n = (size_t)cfg->n_envs;
+  e->cost = (double*)malloc(tc * sizeof(double));
+  e->lat = (double*)malloc(tc * sizeof(double));
+  memcpy(e->cost, cost, tc * sizeof(double));
+  memcpy(e->lat, lat, tc * sizeof(double));
+  e->step = (int32_t*)calloc(n, sizeof(int32_t));
+  e->episode = (int32_t*)calloc(n, sizeof(int32_t));
+  e->mt = (uint32_t*)calloc(n * (MT_N + 1), sizeof(uint32_t));
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t s = cfg->seed + (uint64_t)(cfg->env_offset + (int64_t)i); /* random.seed(seed + global id) */
+    uint32_t key[2] = {(uint32_t)s, (uint32_t)(s >> 32)};
+    ro_mt_seed(e->mt + i * (MT_N + 1), key, key[1] ? 2 : 1);
+  }
+  return e;
+}
+
+void ro_env_destroy(ro_env* e) {
+  if (!e) return;
+  free(e->cost); free(e->lat); free(e->step); free(e->episode); free(e->mt); free(e);
+}
+
+int ro_env_seed_lane(ro_env* e, int lane, const uint32_t* key, int keylen) {
+  if (!e || lane < 0 || lane >= e->cfg.n_envs || keylen <= 0) return -1;
+  ro_mt_seed(e->mt + (size_t)lane * (MT_N + 1), key, keylen);
+  return 0;
+}
+
+int32_t ro_env_lane_step(const ro_env* e, int lane) { return e->step[lane]; }
+int32_t ro_env_lane_episode(const ro_env* e, int lane) { return e->episode[lane]; }
+
+static double noise_draw(ro_env* e, int lane, int t, int c) {
+  const rlks_env_cfg* cfg = &e->cfg;
+  double u;
+  if (cfg->noise_mode == RLKS_NOISE_MT19937) {
+    u = ro_mt_random(e->mt + (size_t)lane * (MT_N + 1));
+  } else {
+    uint32_t ctr[4] = {(uint32_t)(cfg->env_offset + lane), (uint32_t)e->episode[lane], (uint32_t)t,
+                       ((uint32_t)RLKS_PURPOSE_OBS << 16) | (uint32_t)(c >> 1)};
+    uint32_t key[2] = {(uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32)};
+    uint32_t x[4];
+    ro_philox4x32_10(ctr, key, x);
+    u = (c & 1) ? ro_u53(x[2], x[3]) : ro_u53(x[0], x[1]);
+  }
+  double span = cfg->cpu_hi - cfg->cpu_lo; /* 0.8 - 0.1 = 0.7000000000000001 */
+  return cfg->cpu_lo + span * u;
+}
+
+/* obs of row t for one lane (consumes C noise draws, AWS first: :92-93) */
+static void write_obs(ro_env* e, int lane, int t, float* obs) {
+  const int C = e->cfg.n_clouds;
+  for (int c = 0; c < C; ++c) obs[c] = (float)e->cost[(size_t)t * C + c];
+  for (int c = 0; c < C; ++c) obs[C + c] = (float)e->lat[(size_t)t * C + c];
+  for (int c = 0; c < C; ++c) obs[2 * C + c] = (float)noise_draw(e, lane, t, c);
+}
+
+int ro_env_reset(ro_env* e, const uint8_t* mask, float* obs) {
+  const int D = 3 * e->cfg.n_clouds;
+  for (int i = 0; i < e->cfg.n_envs; ++i) {
+    if (mask && !mask[i]) continue;
+    e->step[i] = 0;
+    e->episode[i] += 1;
+    write_obs(e, i, 0, obs + (size_t)i * D);
+  }
+  return 0;
+}
+
+/*
+ * status[0] = invalid actions (nothing steps when > 0: the reference asserts before any change)
+ * status[1] = lanes that ran past the table (reference IndexError from iloc, :91 via :144)
+ */
+int ro_env_step(ro_env* e, const int32_t* actions, float* obs, double* reward, uint8_t* term,
+                int32_t* step_out, float* final_obs, int32_t* status) {
+  const rlks_env_cfg* cfg = &e->cfg;
+  const int C = cfg->n_clouds, T = cfg->n_rows, D = 3 * C;
+  status[0] = status[1] = 0;
+  for (int i = 0; i < cfg->n_envs; ++i)
+    if (actions[i] < 0 || actions[i] >= C) status[0]++;
+  if (status[0]) return 0;
+  for (int i = 0; i < cfg->n_envs; ++i) {
+    const int a = actions[i];
+    int t = e->step[i];
+    term[i] = 0;
+    if (t >= T) { status[1]++; reward[i] = 0.0; step_out[i] = t; continue; }
+    double cost = e->cost[(size_t)t * C + a];
+    double lat = e->lat[(size_t)t * C + a];
+    double t1 = cfg->w_cost * cost;
+    double t2 = cfg->w_lat * lat;
+    reward[i] = cfg->scale * (t1 + t2);
+    t += 1;
+    e->step[i] = t;
+    step_out[i] = t;
+    int done = t >= cfg->max_steps;
+    term[i] = (uint8_t)done;
+    if (t >= T) { status[1]++; continue; }
+    float* o = obs + (size_t)i * D;
+    write_obs(e, i, t, o);
+    if (done && cfg->autoreset) {
+      if (final_obs) memcpy(final_obs + (size_t)i * D, o, D * sizeof(float));
+      e->step[i] = 0;
+      e->episode[i] += 1;
+      write_obs(e, i, 0, o);
+    }
+  }
+  return 0;
+}

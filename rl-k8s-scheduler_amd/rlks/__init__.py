@@ -1,0 +1,26 @@
+"""rlks — MI355X-native rollout-and-training engine for the rl_scheduler multi-cloud pod scheduler.
+
+Public surface (mirrors the reference's gymnasium env and RLlib PPO call sites):
+    K8sMultiCloudEnv, VecK8sMultiCloudEnv      rlks.env   (k8s_multi_cloud_env.py:36-157)
+    PPO, PPOConfig                             rlks.ppo   (train_ppo.py:9-31, eval_ppo.py:17-27)
+All compute runs in librlks.so (hand-written gfx950 HIP kernels); there is no CPU fallback.
+"""
+from .tables import Table, load_table, synthetic_table  # noqa: F401
+
+__version__ = "0.1.0"
+
+
+def __getattr__(name):  # lazy: importing the package must not require a GPU
+    if name in ("K8sMultiCloudEnv", "VecK8sMultiCloudEnv"):
+        from . import env
+
+        return getattr(env, name)
+    if name in ("PPO", "PPOConfig"):
+        from . import ppo
+
+        return getattr(ppo, name)
+    if name == "PolicyParams":
+        from .policy import PolicyParams
+
+        return PolicyParams
+    raise AttributeError(name)

@@ -1,0 +1,288 @@
+"""Drop-in environments backed by the HIP env kernel (librlks.so).
+
+`K8sMultiCloudEnv` keeps the reference's surface (k8s_multi_cloud_env.py:36-157):
+    K8sMultiCloudEnv(env_config=None, fast_mode=True)
+    reset(seed=None, options=None) -> (np.float32[6], {})
+    step(action) -> (np.float32[6], float reward, bool done, False, {"chosen_cloud", "step"})
+    attributes action_space, observation_space, max_steps, current_step, static_df;
+    normal_scheduler_step(obs); render(); close()
+    errors: AssertionError("Invalid action ...") (:116), IndexError past the table (:91 via :144),
+            FileNotFoundError for a missing table (:56-64)
+and runs on one GPU lane.  Its utilisation noise uses CPython's MT19937 per env (noise="mt19937"),
+so with a seeded reset the observations are bit-identical to the reference.  Deliberate
+difference: the reference draws from the process-global `random` stream; here each env owns its
+generator (needed for batching).  reset(seed) still reseeds `random` and `np.random` as the
+reference does (:109-111), and an env that was never seeded takes its seed from `random`.
+
+`VecK8sMultiCloudEnv` is the batched form over device tensors (one lane per env, auto-reset,
+Philox noise by default) used by the rollout engine.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+
+from . import _lib
+from .spaces import Box, Discrete
+from .tables import load_table
+
+try:  # subclass gymnasium.Env when it is installed (RLlib registers gymnasium envs)
+    import gymnasium as _gym
+
+    _EnvBase = _gym.Env
+except Exception:  # pragma: no cover - gymnasium absent in this image
+    _EnvBase = object
+
+CLOUD_NAMES = ("aws", "azure")
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _device(device):
+    torch = _torch()
+    if not torch.cuda.is_available():
+        raise _lib.RlksError("librlks needs a HIP device (MI355X); none is visible")
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device(device)
+
+
+def seed_key_words(seed: int) -> list:
+    """32-bit little-endian words of abs(seed), as CPython random_seed() builds init_by_array's key"""
+    n = abs(int(seed))
+    words = []
+    while n:
+        words.append(n & 0xFFFFFFFF)
+        n >>= 32
+    return words or [0]
+
+
+def make_cfg(n_envs, table, *, noise="philox", seed=0, autoreset=True, env_offset=0, max_steps=None):
+    cfg = _lib.EnvCfg()
+    cfg.n_envs = int(n_envs)
+    cfg.n_rows = table.n_rows
+    cfg.n_clouds = table.n_clouds
+    cfg.max_steps = int(max_steps if max_steps is not None else table.n_rows - 1)  # :66
+    cfg.noise_mode = _lib.RLKS_NOISE_MT19937 if noise == "mt19937" else _lib.RLKS_NOISE_PHILOX
+    cfg.autoreset = int(bool(autoreset))
+    cfg.env_offset = int(env_offset)
+    cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    cfg.cpu_lo, cfg.cpu_hi = 0.1, 0.8          # random.uniform(0.1, 0.8) (:87)
+    cfg.w_cost, cfg.w_lat, cfg.scale = 0.6, 0.4, 100.0  # 100 * (0.6*cost + 0.4*latency) (:122)
+    return cfg
+
+
+class DeviceEnv:
+    """Owner of one rlks_env handle (HBM lane state + staged tables)."""
+
+    def __init__(self, cfg: _lib.EnvCfg, table, device=None):
+        import ctypes as C
+
+        self.torch = _torch()
+        self.device = _device(device)
+        self.cfg = cfg
+        self.table = table
+        with self.torch.cuda.device(self.device):
+            h = C.c_void_p()
+            _lib.call("rlks_env_create", C.byref(cfg), table.cost.ctypes.data, table.latency.ctypes.data, C.byref(h))
+        self.handle = h
+        self.n = cfg.n_envs
+        self.obs_dim = 3 * cfg.n_clouds
+
+    @property
+    def stream(self):
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            _lib.lib().rlks_env_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class K8sMultiCloudEnv(_EnvBase):
+    """Single-env drop-in for rl_scheduler.env.k8s_multi_cloud_env.K8sMultiCloudEnv."""
+
+    metadata = {"render_modes": []}
+
+    def __init__(self, env_config=None, fast_mode=True, *, data_path=None, device=None, noise="mt19937"):
+        # env_config is accepted and ignored, as in the reference (:46)
+        self.fast_mode = fast_mode  # slow mode's kubernetes dry-run is out of scope
+        self.action_space = Discrete(2)  # 0 = AWS, 1 = Azure (:51)
+        self.observation_space = Box(low=0.0, high=1.0, shape=(6,), dtype=np.float32)  # (:52)
+        self._table = load_table(data_path)
+        self.static_df = self._table.dataframe()
+        self.max_steps = self._table.n_rows - 1  # (:66)
+        self.current_step = 0
+        torch = _torch()
+        seed0 = random.getrandbits(64)
+        self._dev = DeviceEnv(make_cfg(1, self._table, noise=noise, seed=seed0, autoreset=False), self._table, device)
+        d = self._dev.device
+        self._act = torch.zeros(1, dtype=torch.int32, device=d)
+        self._obs = torch.zeros(1, 6, dtype=torch.float32, device=d)
+        self._rew = torch.zeros(1, dtype=torch.float64, device=d)
+        self._term = torch.zeros(1, dtype=torch.uint8, device=d)
+        self._step = torch.zeros(1, dtype=torch.int32, device=d)
+        self._status = torch.zeros(2, dtype=torch.int32, device=d)
+        self._keys = torch.zeros(1, 8, dtype=torch.int32, device=d)
+        self._keylen = torch.zeros(1, dtype=torch.int32, device=d)
+        self._seeded = False
+
+    # ------------------------------------------------------------------ gymnasium surface
+    def reset(self, seed=None, options=None):
+        torch = _torch()
+        if seed is not None:
+            random.seed(seed)       # process-global side effects of the reference (:109-111)
+            np.random.seed(seed)
+            self._seed_lane(seed)
+        elif not self._seeded:
+            self._seed_lane(random.getrandbits(64))
+        s = self._dev.stream
+        _lib.call("rlks_env_reset", self._dev.handle, None, _lib.ptr(self._obs), s)
+        self.current_step = 0
+        obs = self._obs.cpu().numpy()[0].copy()
+        del torch
+        return obs, {}
+
+    def _seed_lane(self, seed):
+        import torch
+
+        words = seed_key_words(seed)
+        if len(words) > self._keys.shape[1]:
+            self._keys = torch.zeros(1, len(words), dtype=torch.int32, device=self._dev.device)
+        key = np.zeros(self._keys.shape[1], dtype=np.uint32)
+        key[: len(words)] = words
+        self._keys.copy_(torch.from_numpy(key.view(np.int32))[None])
+        self._keylen.fill_(len(words))
+        _lib.call("rlks_env_seed", self._dev.handle, None, _lib.ptr(self._keys), _lib.ptr(self._keylen),
+                  self._keys.shape[1], self._dev.stream)
+        self._seeded = True
+
+    def step(self, action):
+        assert self.action_space.contains(action), f"Invalid action {action}"
+        a = int(action)
+        self._act.fill_(a)
+        _lib.call("rlks_env_step", self._dev.handle, _lib.ptr(self._act), _lib.ptr(self._obs), _lib.ptr(self._rew),
+                  None, _lib.ptr(self._term), None, _lib.ptr(self._step), None, _lib.ptr(self._status),
+                  self._dev.stream)
+        status = self._status.cpu().numpy()
+        self.current_step = int(self._step.item())
+        if status[1]:
+            raise IndexError("single positional indexer is out-of-bounds")
+        reward = float(self._rew.item())
+        done = bool(self._term.item())
+        obs = self._obs.cpu().numpy()[0].copy()
+        info = {"chosen_cloud": "aws" if a == 0 else "azure", "step": self.current_step}
+        return obs, reward, done, False, info
+
+    def render(self):
+        pass
+
+    def close(self):
+        pass
+
+    def normal_scheduler_step(self, obs):
+        """cost-only greedy baseline (:156-157)"""
+        return 0 if obs[0] <= obs[1] else 1
+
+
+class VecK8sMultiCloudEnv:
+    """Batched env over device tensors: one lane per env, all lanes stepped by one kernel launch.
+
+    reset(seed=None) -> obs [N, 3C] float32 (device)
+    step(actions int32 [N]) -> (obs, reward f64 [N], terminated u8 [N], truncated u8 [N], info)
+    info = {"step": int32 [N], "final_observation": [N, 3C] (rows valid where terminated)}
+    With autoreset (default) a terminated lane returns the first observation of its next episode.
+    """
+
+    def __init__(self, num_envs, *, table=None, seed=0, noise="philox", autoreset=True, env_offset=0,
+                 device=None, data_path=None):
+        torch = _torch()
+        self.table = table if table is not None else load_table(data_path)
+        self.num_envs = int(num_envs)
+        self.n_clouds = self.table.n_clouds
+        self.obs_dim = 3 * self.n_clouds
+        self.action_space = Discrete(self.n_clouds)
+        self.observation_space = Box(0.0, 1.0, (self.obs_dim,), np.float32)
+        self.max_steps = self.table.n_rows - 1
+        self.cfg = make_cfg(num_envs, self.table, noise=noise, seed=seed, autoreset=autoreset, env_offset=env_offset)
+        self.dev = DeviceEnv(self.cfg, self.table, device)
+        d = self.dev.device
+        self.device = d
+        N = self.num_envs
+        self._status = torch.zeros(2, dtype=torch.int32, device=d)
+        self.obs = torch.zeros(N, self.obs_dim, dtype=torch.float32, device=d)
+        self.reward = torch.zeros(N, dtype=torch.float64, device=d)
+        self.terminated = torch.zeros(N, dtype=torch.uint8, device=d)
+        self.truncated = torch.zeros(N, dtype=torch.uint8, device=d)
+        self.steps = torch.zeros(N, dtype=torch.int32, device=d)
+        self.final_obs = torch.zeros(N, self.obs_dim, dtype=torch.float32, device=d)
+        self._stats = torch.zeros(2, dtype=torch.float64, device=d)
+
+    @property
+    def handle(self):
+        return self.dev.handle
+
+    def seed(self, seeds, mask=None):
+        """per-lane random.seed(seeds[i]) (MT19937 noise mode only)"""
+        torch = _torch()
+        words = [seed_key_words(s) for s in seeds]
+        width = max(len(w) for w in words)
+        key = np.zeros((self.num_envs, width), np.uint32)
+        for i, w in enumerate(words):
+            key[i, : len(w)] = w
+        keys = torch.from_numpy(key.view(np.int32)).to(self.device)
+        klen = torch.tensor([len(w) for w in words], dtype=torch.int32, device=self.device)
+        m = None if mask is None else torch.as_tensor(mask, dtype=torch.uint8, device=self.device)
+        _lib.call("rlks_env_seed", self.handle, _lib.ptr(m), _lib.ptr(keys), _lib.ptr(klen), width, self.dev.stream)
+
+    def reset(self, seed=None, mask=None):
+        torch = _torch()
+        if seed is not None and self.cfg.noise_mode == _lib.RLKS_NOISE_MT19937:
+            self.seed([int(seed) + i for i in range(self.num_envs)])
+        m = None if mask is None else torch.as_tensor(mask, dtype=torch.uint8, device=self.device)
+        _lib.call("rlks_env_reset", self.handle, _lib.ptr(m), _lib.ptr(self.obs), self.dev.stream)
+        return self.obs
+
+    def step(self, actions):
+        torch = _torch()
+        a = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
+        _lib.call("rlks_env_step", self.handle, _lib.ptr(a), _lib.ptr(self.obs), _lib.ptr(self.reward), None,
+                  _lib.ptr(self.terminated), _lib.ptr(self.truncated), _lib.ptr(self.steps),
+                  _lib.ptr(self.final_obs), _lib.ptr(self._status), self.dev.stream)
+        return self.obs, self.reward, self.terminated, self.truncated, {"step": self.steps,
+                                                                         "final_observation": self.final_obs,
+                                                                         "status": self._status}
+
+    def check_status(self):
+        """raise the reference's exceptions for the last step (synchronises)"""
+        st = self._status.cpu().numpy()
+        if st[0]:
+            raise AssertionError(f"Invalid action in {int(st[0])} lane(s)")
+        if st[1]:
+            raise IndexError("single positional indexer is out-of-bounds")
+
+    def episode_stats(self, clear=True):
+        """(sum of completed-episode returns, count) since the last clear"""
+        _lib.call("rlks_env_episode_stats", self.handle, _lib.ptr(self._stats), int(clear), self.dev.stream)
+        return self._stats
+
+    def lane_state(self):
+        torch = _torch()
+        st = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+        ep = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+        _lib.call("rlks_env_lane_state", self.handle, _lib.ptr(st), _lib.ptr(ep), self.dev.stream)
+        return st, ep
+
+    def close(self):
+        self.dev.close()

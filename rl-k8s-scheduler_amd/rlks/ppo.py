@@ -1,0 +1,425 @@
+"""PPO agent with RLlib's surface, running the whole hot path on the GPU.
+
+Reference call sites:
+  PPOConfig().environment(K8sMultiCloudEnv).framework("torch").rollouts(num_rollout_workers=1)
+      .training(train_batch_size=4000, sgd_minibatch_size=256, num_sgd_iter=10, lr=3e-4, gamma=0.99)
+                                                                         (train_ppo.py:9-21)
+  agent = PPO(config=config); result = agent.train(); result["episode_reward_mean"];
+  agent.save()                                                           (train_ppo.py:23-31)
+  PPO.from_checkpoint(path); compute_single_action(obs[, explore=False]) (eval_ppo.py:17-27,
+                                                                          final_evaluation.py:32-48)
+RLlib itself is absent in this image, so the semantics restated here (GAE, advantage
+standardisation, clipped surrogate + KL + clipped value loss, Adam, KL adaptation) are pinned by
+the torch-CPU oracle under oracle/, not by RLlib: parity unpinned.
+
+One PPO iteration on one GPU (all launches on torch's current stream, no host sync inside):
+  rollout   rlks_rollout: T x (policy forward -> sample -> env step), bootstrap V(s_T)
+  advantages rlks_gae -> rlks_adv_stats -> [all-reduce] -> rlks_adv_finalize
+  update    num_sgd_iter x minibatches x (rlks_ppo_gather -> rlks_ppo_grad -> [all-reduce] ->
+            rlks_adam_step); then rlks_kl_update from the mean KL over all SGD steps
+Multi-GPU (torch.distributed, backend "nccl" = RCCL): each rank owns a contiguous block of lanes
+(env_offset = rank * lanes), the flat gradient and the few scalar sums are all-reduced.
+"""
+from __future__ import annotations
+
+import copy
+import ctypes as C
+import json
+import math
+import time
+from pathlib import Path
+
+import numpy as np
+
+from . import _lib
+from .env import DeviceEnv, make_cfg
+from .policy import PolicyParams
+from .tables import load_table
+
+
+class PPOConfig:
+    """RLlib-style builder.  Defaults are RLlib's old-API-stack PPOConfig defaults."""
+
+    def __init__(self):
+        self.env = None
+        self.env_config = {}
+        self.framework_str = "torch"
+        self.num_rollout_workers = 0
+        self.num_envs_per_worker = 1
+        self.rollout_fragment_length = "auto"
+        self.train_batch_size = 4000
+        self.sgd_minibatch_size = 128
+        self.num_sgd_iter = 30
+        self.lr = 5e-5
+        self.gamma = 0.99
+        self.lambda_ = 1.0
+        self.clip_param = 0.3
+        self.vf_clip_param = 10.0
+        self.vf_loss_coeff = 1.0
+        self.entropy_coeff = 0.0
+        self.kl_coeff = 0.2
+        self.kl_target = 0.01
+        self.grad_clip = None
+        self.model = {"fcnet_hiddens": [256, 256], "fcnet_activation": "tanh", "vf_share_layers": False}
+        self.num_gpus = 0
+        self.seed = None
+        self.explore = True
+        self.evaluation_interval = None
+        self.evaluation_duration = 10
+        # rlks-specific knobs
+        self.num_envs = None          # lanes per GPU (default: workers x envs per worker)
+        self.noise = "philox"         # env utilisation noise: "philox" or "mt19937"
+        self.data_path = None
+        self.table = None
+        self.adam_betas = (0.9, 0.999)
+        self.adam_eps = 1e-8
+
+    # ---- builder methods (names as in RLlib)
+    def environment(self, env=None, env_config=None, **kw):
+        if env is not None:
+            self.env = env
+        if env_config is not None:
+            self.env_config = dict(env_config)
+        return self
+
+    def framework(self, framework="torch", **kw):
+        if framework not in ("torch",):
+            raise ValueError(f"only the torch framework is supported, got {framework!r}")
+        self.framework_str = framework
+        return self
+
+    def rollouts(self, num_rollout_workers=None, num_envs_per_worker=None, rollout_fragment_length=None, **kw):
+        if num_rollout_workers is not None:
+            self.num_rollout_workers = int(num_rollout_workers)
+        if num_envs_per_worker is not None:
+            self.num_envs_per_worker = int(num_envs_per_worker)
+        if rollout_fragment_length is not None:
+            self.rollout_fragment_length = rollout_fragment_length
+        for k, v in kw.items():
+            setattr(self, k, v)
+        return self
+
+    env_runners = rollouts
+
+    def training(self, **kw):
+        alias = {"lambda": "lambda_"}
+        for k, v in kw.items():
+            k = alias.get(k, k)
+            if k == "model":
+                self.model = {**self.model, **v}
+            else:
+                setattr(self, k, v)
+        return self
+
+    def resources(self, num_gpus=None, **kw):
+        if num_gpus is not None:
+            self.num_gpus = num_gpus
+        return self
+
+    def evaluation(self, evaluation_interval=None, evaluation_duration=None, **kw):
+        if evaluation_interval is not None:
+            self.evaluation_interval = evaluation_interval
+        if evaluation_duration is not None:
+            self.evaluation_duration = evaluation_duration
+        return self
+
+    def debugging(self, seed=None, **kw):
+        if seed is not None:
+            self.seed = int(seed)
+        return self
+
+    def exploration(self, explore=None, **kw):
+        if explore is not None:
+            self.explore = bool(explore)
+        return self
+
+    def to_dict(self):
+        d = {k: v for k, v in self.__dict__.items() if k not in ("env", "table")}
+        d["env"] = getattr(self.env, "__name__", str(self.env)) if self.env is not None else None
+        d["lambda"] = d.pop("lambda_")
+        return d
+
+    def copy(self):
+        return copy.deepcopy(self)
+
+    def build(self, **kw):
+        return PPO(config=self, **kw)
+
+    # ---- derived sizes
+    def lanes(self) -> int:
+        if self.num_envs:
+            return int(self.num_envs)
+        return max(1, self.num_rollout_workers) * max(1, self.num_envs_per_worker)
+
+    def hidden(self) -> int:
+        h = list(self.model.get("fcnet_hiddens", [256, 256]))
+        if len(h) != 2 or h[0] != h[1]:
+            raise ValueError(f"fcnet_hiddens must be two equal layers, got {h}")
+        if self.model.get("vf_share_layers", False):
+            raise ValueError("vf_share_layers=True is not supported (RLlib's PPO default is False)")
+        if self.model.get("fcnet_activation", "tanh") != "tanh":
+            raise ValueError("only fcnet_activation='tanh' (RLlib's default) is supported")
+        return int(h[0])
+
+
+def _dist():
+    import torch.distributed as dist
+
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+class PPO:
+    """One instance per GPU (rank).  train() runs one PPO iteration over all local lanes."""
+
+    def __init__(self, config: PPOConfig | None = None, env=None, device=None, **kw):
+        import torch
+
+        self.config = cfg = (config or PPOConfig()).copy()
+        if env is not None:
+            cfg.env = env
+        self.torch = torch
+        dist = _dist()
+        self.rank = dist.get_rank() if dist else 0
+        self.world = dist.get_world_size() if dist else 1
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        table = cfg.table if cfg.table is not None else load_table(cfg.data_path)
+        self.table = table
+        C_ = table.n_clouds
+        self.D, self.A, self.H = 3 * C_, C_, cfg.hidden()
+        self.N = cfg.lanes()
+        self.T = max(1, math.ceil(cfg.train_batch_size / (self.N * self.world)))
+        if cfg.rollout_fragment_length not in (None, "auto"):
+            self.T = int(cfg.rollout_fragment_length)
+        self.samples = self.T * self.N
+        self.mb = int(cfg.sgd_minibatch_size) // self.world  # per-rank rows of a global minibatch
+        if self.mb <= 0 or self.mb % 128:
+            raise ValueError(f"sgd_minibatch_size per rank must be a positive multiple of 128, got {self.mb}")
+        self.n_mb = self.samples // self.mb
+        if self.n_mb == 0:
+            raise ValueError("train batch is smaller than one minibatch")
+        seed = cfg.seed if cfg.seed is not None else 0
+        self.seed = seed
+        with torch.cuda.device(self.device):
+            self.env = DeviceEnv(make_cfg(self.N, table, noise=cfg.noise, seed=seed, autoreset=True,
+                                          env_offset=self.rank * self.N), table, self.device)
+            self.params = PolicyParams(self.D, self.H, self.A, device=self.device, seed=seed)
+            P = self.params.padded
+            f32 = dict(dtype=torch.float32, device=self.device)
+            self.adam_m = torch.zeros(P, **f32)
+            self.adam_v = torch.zeros(P, **f32)
+            self.grad = torch.zeros(P, **f32)
+            self.adam_step = 0
+            self.dyn = torch.zeros(_lib.RLKS_DYN_SIZE, **f32)
+            self.dyn[_lib.RLKS_DYN_KL_COEFF] = float(cfg.kl_coeff)
+            self.dyn[_lib.RLKS_DYN_INV_COUNT] = 1.0 / (self.mb * self.world)
+            T, N, D, A = self.T, self.N, self.D, self.A
+            self.buf = {
+                "obs": torch.zeros(T + 1, N, D, **f32), "logits": torch.zeros(T, N, A, **f32),
+                "values": torch.zeros(T + 1, N, **f32), "actions": torch.zeros(T, N, dtype=torch.int32, device=self.device),
+                "logp": torch.zeros(T, N, **f32), "rewards": torch.zeros(T, N, **f32),
+                "dones": torch.zeros(T, N, dtype=torch.uint8, device=self.device),
+                "adv": torch.zeros(T, N, **f32), "vtarg": torch.zeros(T, N, **f32),
+            }
+            b = self.buf
+            self.bufs = _lib.RolloutBufs(b["obs"].data_ptr(), b["logits"].data_ptr(), b["values"].data_ptr(),
+                                         b["actions"].data_ptr(), b["logp"].data_ptr(), b["rewards"].data_ptr(),
+                                         b["dones"].data_ptr(), b["adv"].data_ptr(), b["vtarg"].data_ptr(), T, N)
+            self.stride = _lib.lib().rlks_minibatch_stride(C.byref(self.params.desc))
+            self.mbuf = torch.zeros(self.mb, self.stride, **f32)
+            wsb = C.c_int64()
+            _lib.call("rlks_ppo_workspace_bytes", C.byref(self.params.desc), self.mb, C.byref(wsb))
+            self.ws = torch.empty(wsb.value, dtype=torch.uint8, device=self.device)
+            self.n_partials = _lib.lib().rlks_gae_partials_count(N)
+            self.gae_part = torch.zeros(self.n_partials, 2, dtype=torch.float64, device=self.device)
+            self.adv_sums = torch.zeros(3, dtype=torch.float64, device=self.device)
+            self.stats = torch.zeros(cfg.num_sgd_iter * self.n_mb, _lib.RLKS_STAT_SIZE, dtype=torch.float64,
+                                     device=self.device)
+            self.kl_sc = torch.zeros(2, dtype=torch.float64, device=self.device)
+            self.ep_stats = torch.zeros(2, dtype=torch.float64, device=self.device)
+            self.coeffs = _lib.PpoCoeffs(cfg.clip_param, cfg.vf_clip_param, cfg.vf_loss_coeff, cfg.entropy_coeff)
+            _lib.call("rlks_env_reset", self.env.handle, None, _lib.ptr(b["obs"][0]), self.stream)
+        self.iteration = 0
+        self.timesteps_total = 0
+        self.episodes_total = 0
+
+    # ------------------------------------------------------------------ internals
+    @property
+    def stream(self):
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def _allreduce(self, t):
+        dist = _dist()
+        if dist is not None and self.world > 1:
+            dist.all_reduce(t)
+
+    def rollout(self, explore=True):
+        s = self.stream
+        b = self.buf
+        _lib.call("rlks_rollout", self.env.handle, C.byref(self.params.desc), _lib.ptr(self.params.flat),
+                  C.byref(self.bufs), int(explore), s)
+
+    def advantages(self):
+        s = self.stream
+        b = self.buf
+        cfg = self.config
+        _lib.call("rlks_gae", _lib.ptr(b["rewards"]), _lib.ptr(b["values"]), _lib.ptr(b["dones"]), float(cfg.gamma),
+                  float(cfg.lambda_), self.T, self.N, _lib.ptr(b["adv"]), _lib.ptr(b["vtarg"]),
+                  _lib.ptr(self.gae_part), s)
+        _lib.call("rlks_adv_stats", _lib.ptr(self.gae_part), self.n_partials, float(self.samples),
+                  _lib.ptr(self.adv_sums), s)
+        self._allreduce(self.adv_sums)
+        _lib.call("rlks_adv_finalize", _lib.ptr(self.adv_sums), _lib.ptr(self.dyn), s)
+
+    def sgd_step(self, epoch, b, stat_row):
+        s = self.stream
+        desc = C.byref(self.params.desc)
+        _lib.call("rlks_ppo_gather", desc, C.byref(self.bufs), (self.seed * 1000003 + self.iteration) & (2**64 - 1),
+                  epoch, b * self.mb, self.mb, _lib.ptr(self.dyn), _lib.ptr(self.mbuf), s)
+        _lib.call("rlks_ppo_grad", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat), _lib.ptr(self.dyn),
+                  _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row), _lib.ptr(self.ws),
+                  self.ws.numel(), s)
+        self._allreduce(self.grad)
+        self.adam_step += 1
+        beta1, beta2 = self.config.adam_betas
+        _lib.call("rlks_adam_step", _lib.ptr(self.params.flat), _lib.ptr(self.grad), _lib.ptr(self.adam_m),
+                  _lib.ptr(self.adam_v), self.params.padded, float(self.config.lr), float(beta1), float(beta2),
+                  float(self.config.adam_eps), self.adam_step, s)
+
+    def update(self):
+        cfg = self.config
+        k = 0
+        for epoch in range(cfg.num_sgd_iter):
+            for b in range(self.n_mb):
+                self.sgd_step(epoch, b, self.stats[k])
+                k += 1
+        self._allreduce(self.stats)
+        st = self.stats
+        # RLlib: learner stats are means over all SGD steps; kl per step = sum KL / rows
+        self.kl_sc[0] = (st[:, _lib.RLKS_STAT_KL] / st[:, _lib.RLKS_STAT_ROWS]).sum()
+        self.kl_sc[1] = float(st.shape[0])
+        _lib.call("rlks_kl_update", _lib.ptr(self.dyn), _lib.ptr(self.kl_sc), float(cfg.kl_target), self.stream)
+
+    def train_step_no_sync(self):
+        """one PPO iteration, enqueued only (bench path)"""
+        self.rollout(explore=self.config.explore)
+        self.advantages()
+        self.update()
+        _lib.call("rlks_env_episode_stats", self.env.handle, _lib.ptr(self.ep_stats), 1, self.stream)
+        self.iteration += 1
+        self.timesteps_total += self.samples * self.world
+
+    # ------------------------------------------------------------------ RLlib surface
+    def train(self):
+        t0 = time.time()
+        kl_before = float(self.dyn[_lib.RLKS_DYN_KL_COEFF].item())
+        self.train_step_no_sync()
+        self._allreduce(self.ep_stats)
+        ep = self.ep_stats.cpu().numpy()
+        st = self.stats.cpu().numpy()
+        rows = st[:, _lib.RLKS_STAT_ROWS]
+        n_ep = int(round(ep[1]))
+        self.episodes_total += n_ep
+        learner = {
+            "policy_loss": float(np.mean(st[:, _lib.RLKS_STAT_POLICY_LOSS] / rows)),
+            "vf_loss": float(np.mean(st[:, _lib.RLKS_STAT_VF_LOSS] / rows)),
+            "kl": float(np.mean(st[:, _lib.RLKS_STAT_KL] / rows)),
+            "entropy": float(np.mean(st[:, _lib.RLKS_STAT_ENTROPY] / rows)),
+            "cur_kl_coeff": kl_before,
+            "cur_lr": float(self.config.lr),
+        }
+        return {
+            "episode_reward_mean": float(ep[0] / n_ep) if n_ep else float("nan"),
+            "episodes_this_iter": n_ep,
+            "episodes_total": self.episodes_total,
+            "training_iteration": self.iteration,
+            "timesteps_total": self.timesteps_total,
+            "num_env_steps_sampled": self.timesteps_total,
+            "time_this_iter_s": time.time() - t0,
+            "info": {"learner": {"default_policy": {"learner_stats": learner}}},
+        }
+
+    def compute_actions(self, obs, explore=None):
+        """batched actions for obs [n, D] (device or host); returns an int32 device tensor"""
+        torch = self.torch
+        explore = self.config.explore if explore is None else explore
+        o = torch.as_tensor(obs, dtype=torch.float32, device=self.device).reshape(-1, self.D)
+        logits, _ = self.params.forward(o)
+        if not explore:
+            return torch.argmax(logits, dim=1).to(torch.int32)
+        return torch.distributions.Categorical(logits=logits).sample().to(torch.int32)
+
+    def compute_single_action(self, observation=None, state=None, *, explore=None, **kw):
+        explore = self.config.explore if explore is None else explore
+        o = np.asarray(observation, dtype=np.float32).reshape(1, self.D)
+        logits, _ = self.params.forward(self.torch.from_numpy(o).to(self.device))
+        lg = logits.cpu().numpy()[0].astype(np.float64)
+        if not explore:
+            return int(np.argmax(lg))
+        p = np.exp(lg - lg.max())
+        p /= p.sum()
+        return int(np.random.choice(len(p), p=p))
+
+    def get_state(self):
+        torch = self.torch
+        steps = torch.zeros(self.N, dtype=torch.int32, device=self.device)
+        eps = torch.zeros(self.N, dtype=torch.int32, device=self.device)
+        _lib.call("rlks_env_lane_state", self.env.handle, _lib.ptr(steps), _lib.ptr(eps), self.stream)
+        return {
+            "weights": self.params.state_dict(),
+            "adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(),
+            "adam_step": self.adam_step, "kl_coeff": float(self.dyn[_lib.RLKS_DYN_KL_COEFF].item()),
+            "iteration": self.iteration, "timesteps_total": self.timesteps_total,
+            "episodes_total": self.episodes_total, "lane_steps": steps.cpu(), "lane_episodes": eps.cpu(),
+        }
+
+    def save(self, checkpoint_dir=None):
+        """RLlib Algorithm.save(): writes <dir>/checkpoint_<iter:06d>/ and returns its path"""
+        import torch
+
+        base = Path(checkpoint_dir) if checkpoint_dir else Path.home() / "rlks_results" / "PPO"
+        path = base / f"checkpoint_{self.iteration:06d}"
+        path.mkdir(parents=True, exist_ok=True)
+        st = self.get_state()
+        tensors = {f"weights/{k}": v for k, v in st.pop("weights").items()}
+        tensors.update({k: st.pop(k) for k in ("adam_m", "adam_v", "lane_steps", "lane_episodes")})
+        torch.save(tensors, path / "state.pt")
+        meta = {"state": st, "config": self.config.to_dict()}
+        (path / "algorithm_state.json").write_text(json.dumps(meta, indent=1, default=str))
+        return str(path)
+
+    def restore(self, checkpoint_path):
+        import torch
+
+        path = Path(checkpoint_path)
+        tensors = torch.load(path / "state.pt", weights_only=True)
+        meta = json.loads((path / "algorithm_state.json").read_text())["state"]
+        self.params.load_state_dict({k[len("weights/"):]: v for k, v in tensors.items() if k.startswith("weights/")})
+        self.adam_m.copy_(tensors["adam_m"].to(self.device))
+        self.adam_v.copy_(tensors["adam_v"].to(self.device))
+        self.adam_step = int(meta["adam_step"])
+        self.dyn[_lib.RLKS_DYN_KL_COEFF] = float(meta["kl_coeff"])
+        self.iteration = int(meta["iteration"])
+        self.timesteps_total = int(meta["timesteps_total"])
+        self.episodes_total = int(meta["episodes_total"])
+
+    @classmethod
+    def from_checkpoint(cls, checkpoint_path, config: PPOConfig | None = None, **kw):
+        path = Path(checkpoint_path)
+        if config is None:
+            d = json.loads((path / "algorithm_state.json").read_text())["config"]
+            config = PPOConfig()
+            for k, v in d.items():
+                if k == "lambda":
+                    config.lambda_ = v
+                elif k == "adam_betas":
+                    config.adam_betas = tuple(v)
+                elif k != "env" and hasattr(config, k):
+                    setattr(config, k, v)
+        algo = cls(config=config, **kw)
+        algo.restore(path)
+        return algo
+
+    def stop(self):
+        self.env.close()

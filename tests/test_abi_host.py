@@ -1,0 +1,186 @@
+"""CPU tests: the C-ABI library loads and exports every declared symbol, the ctypes mirrors match
+the C struct layouts, and the host-side logic (config, tables, layout, seeding) is right."""
+import ctypes as C
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADERS = [ROOT / "include" / "rlks.h"]
+
+
+def declared_symbols():
+    syms = set()
+    for h in HEADERS:
+        txt = h.read_text()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(rlks_[a-z_0-9]+)\s*\(", txt, flags=re.M):
+            syms.add(m.group(1))
+    return syms
+
+
+def test_library_exports_every_declared_symbol():
+    from rlks import _lib
+
+    lib = _lib.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    missing = [s for s in sorted(syms) if not hasattr(lib, s)]
+    assert not missing, missing
+    # and the ctypes signature table covers exactly the header
+    assert set(_lib.SIGNATURES) == syms
+    assert lib.rlks_version().decode().startswith("rlks")
+
+
+def test_nm_exports_plain_c_names():
+    out = subprocess.run(["nm", "-D", "--defined-only", str(ROOT / "rl-k8s-scheduler_amd/rlks/librlks.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert declared_symbols() <= exported
+
+
+def _c_layout(struct, fields):
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "rlks.h"', "int main(void){",
+           f'printf("%zu\\n", sizeof({struct}));']
+    src += [f'printf("%zu\\n", offsetof({struct}, {f}));' for f in fields]
+    src += ["return 0;}"]
+    return "\n".join(src)
+
+
+@pytest.mark.parametrize("struct,py", [("rlks_env_cfg", "EnvCfg"), ("rlks_mlp_desc", "MlpDesc"),
+                                       ("rlks_ppo_coeffs", "PpoCoeffs"), ("rlks_rollout_bufs", "RolloutBufs")])
+def test_ctypes_struct_layout_matches_c(tmp_path, struct, py):
+    from rlks import _lib
+
+    cls = getattr(_lib, py)
+    fields = [f[0] for f in cls._fields_]
+    (tmp_path / "l.c").write_text(_c_layout(struct, fields))
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(tmp_path / "l.c"), "-o", str(tmp_path / "l")], check=True)
+    vals = [int(x) for x in subprocess.run([str(tmp_path / "l")], capture_output=True, text=True).stdout.split()]
+    assert vals[0] == C.sizeof(cls)
+    assert vals[1:] == [getattr(cls, f).offset for f in fields]
+
+
+def test_oracle_struct_matches_library_struct():
+    import oracle
+    from rlks import _lib
+
+    assert oracle.EnvCfg._fields_ == _lib.EnvCfg._fields_
+
+
+def test_mlp_layout_default_net():
+    from rlks.policy import layout, tensor_shapes
+
+    off, padded, real = layout(6, 256, 2)
+    assert real == 135939  # RLlib FCNet [256, 256], separate value net
+    shapes = tensor_shapes(6, 256, 2)
+    o = 0
+    for i, s in enumerate(shapes):
+        assert off[i] == o and off[i] % 64 == 0
+        o += -(-int(np.prod(s)) // 64) * 64
+    assert padded == o
+
+
+def test_seed_key_words_match_cpython():
+    from rlks.env import seed_key_words
+
+    assert seed_key_words(0) == [0]
+    assert seed_key_words(-5) == [5]
+    assert seed_key_words(2**32 + 7) == [7, 1]
+    assert seed_key_words(2**64 + 3) == [3, 0, 1]
+
+
+def test_ppo_config_builder_reference_calls():
+    from rlks.ppo import PPOConfig
+
+    # train_ppo.py:9-21
+    c = (PPOConfig().environment("K8sMultiCloudEnv").framework("torch").rollouts(num_rollout_workers=1)
+         .training(train_batch_size=4000, sgd_minibatch_size=256, num_sgd_iter=10, lr=3e-4, gamma=0.99))
+    assert (c.train_batch_size, c.sgd_minibatch_size, c.num_sgd_iter, c.lr, c.gamma) == (4000, 256, 10, 3e-4, 0.99)
+    assert c.lanes() == 1 and c.hidden() == 256 and c.clip_param == 0.3 and c.kl_coeff == 0.2
+    # train_final.py:6-20
+    c2 = (PPOConfig().environment("x").rollouts(num_rollout_workers=6, num_envs_per_worker=4).framework("torch")
+          .training(train_batch_size=8000, sgd_minibatch_size=512, num_sgd_iter=15, lr=5e-4, gamma=0.995)
+          .resources(num_gpus=0).evaluation(evaluation_interval=5, evaluation_duration=20))
+    assert c2.lanes() == 24 and c2.evaluation_interval == 5 and c2.gamma == 0.995
+    d = c2.to_dict()
+    assert d["lambda"] == 1.0 and d["train_batch_size"] == 8000
+    with pytest.raises(ValueError):
+        PPOConfig().framework("tf2")
+    with pytest.raises(ValueError):
+        PPOConfig().training(model={"vf_share_layers": True}).hidden()
+
+
+def test_tables(golden_table):
+    from rlks.tables import load_table, synthetic_table
+
+    t = load_table()
+    assert t.n_rows == 100 and t.n_clouds == 2
+    np.testing.assert_array_equal(t.cost, golden_table[:, [1, 2]])
+    np.testing.assert_array_equal(t.latency, golden_table[:, [3, 4]])
+    with pytest.raises(FileNotFoundError, match="normalize_data.py"):
+        load_table("/nonexistent/normalized_rl_data.csv")
+    s = synthetic_table(8, seed=42)
+    assert s.cost.shape == (100, 8) and s.cost.min() == 0.0 and s.cost.max() == 1.0
+    assert np.all(s.latency.min(0) == 0.0) and np.all(s.latency.max(0) == 1.0)
+
+
+def test_drop_in_import_paths():
+    import rl_scheduler.env.k8s_multi_cloud_env as m
+    from rl_scheduler.agent import PPO, PPOConfig
+
+    assert m.K8sMultiCloudEnv.__name__ == "K8sMultiCloudEnv"
+    assert PPO.__name__ == "PPO" and PPOConfig.__name__ == "PPOConfig"
+
+
+def test_env_requires_device_without_fallback():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    from rlks import K8sMultiCloudEnv
+    from rlks._lib import RlksError
+
+    with pytest.raises(RlksError, match="HIP device"):
+        K8sMultiCloudEnv()
+
+
+def test_oracle_ppo_grad_matches_finite_differences():
+    """self-check of the torch fp64 loss restatement on a tiny net (H=8)"""
+    import oracle
+
+    rng = np.random.default_rng(0)
+    D, H, A = 6, 8, 2
+    shapes = [(H, D), (H,), (H, H), (H,), (A, H), (A,), (H, D), (H,), (H, H), (H,), (1, H), (1,)]
+    off, o = [], 0
+    for s in shapes:
+        off.append(o)
+        o += int(np.prod(s))
+    flat = rng.standard_normal(o) * 0.5
+    rows = 16
+    mb = np.zeros((rows, D + A + 4))
+    mb[:, :D] = rng.random((rows, D))
+    mb[:, D:D + A] = rng.standard_normal((rows, A))
+    mb[:, D + A] = rng.standard_normal(rows)
+    mb[:, D + A + 1] = rng.standard_normal(rows)
+    mb[:, D + A + 3] = rng.integers(0, A, rows)
+    lo = mb[:, D:D + A]
+    mb[:, D + A + 2] = (lo - np.log(np.exp(lo).sum(1, keepdims=True)))[np.arange(rows), mb[:, D + A + 3].astype(int)]
+    g, _ = oracle.ppo_loss_grad(flat, off, D, H, A, mb)
+
+    def loss(f):
+        import torch
+
+        gg, st = oracle.ppo_loss_grad(f, off, D, H, A, mb)
+        return (st["policy_loss"] + st["vf_loss"]) / rows + 0.2 * st["kl"] / rows
+
+    eps = 1e-6
+    for i in rng.choice(o, 12, replace=False):
+        fp, fm = flat.copy(), flat.copy()
+        fp[i] += eps
+        fm[i] -= eps
+        fd = (loss(fp) - loss(fm)) / (2 * eps)
+        assert abs(fd - g[i]) <= 1e-6 * max(1.0, abs(g[i])), (i, fd, g[i])

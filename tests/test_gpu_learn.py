@@ -1,0 +1,275 @@
+"""GPU parity of GAE (K3), the MLP forward / PPO gradient (K4), Adam, the minibatch gather and one
+end-to-end PPO iteration, against the CPU oracle.
+
+Tolerances (north star: "rewards, advantages and gradients within 1e-5 relative"):
+  - elementwise outputs (GAE, forward logits/values, Adam): |x - ref| <= 1e-5 * |ref| + atol with
+    atol = 1e-5 * max|ref| (fp32 accumulation over K = 256 or T = 128 terms);
+  - gradients (sums over the minibatch rows): per tensor, ||g - ref||_2 <= 1e-5 * ||ref||_2 and
+    elementwise |g - ref| <= 1e-5 * max|ref| + 1e-5 * |ref|.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def close(x, ref, rtol=1e-5):
+    x = np.asarray(x, np.float64)
+    ref = np.asarray(ref, np.float64)
+    atol = rtol * max(1e-30, float(np.abs(ref).max()))
+    err = np.abs(x - ref)
+    ok = err <= rtol * np.abs(ref) + atol
+    assert ok.all(), f"max err {err.max():.3e} vs max|ref| {np.abs(ref).max():.3e}"
+
+
+# ----------------------------------------------------------------------------- GAE
+@pytest.mark.parametrize("T,N,gamma,lam", [(128, 4096, 0.99, 1.0), (64, 1000, 0.995, 0.95), (17, 5, 0.9, 0.0)])
+def test_gae_matches_oracle(T, N, gamma, lam):
+    from rlks import _lib
+
+    d = _dev()
+    rng = np.random.default_rng(T + N)
+    r = rng.random((T, N)).astype(np.float32) * 100
+    v = rng.standard_normal((T + 1, N)).astype(np.float32) * 50
+    dn = (rng.random((T, N)) < 0.01).astype(np.uint8)
+    rt, vt_, dt = (torch.from_numpy(x).to(d) for x in (r, v, dn))
+    adv = torch.zeros(T, N, device=d)
+    vtg = torch.zeros(T, N, device=d)
+    npart = _lib.lib().rlks_gae_partials_count(N)
+    part = torch.zeros(npart, 2, dtype=torch.float64, device=d)
+    sums = torch.zeros(3, dtype=torch.float64, device=d)
+    dyn = torch.zeros(8, device=d)
+    _lib.call("rlks_gae", rt.data_ptr(), vt_.data_ptr(), dt.data_ptr(), gamma, lam, T, N, adv.data_ptr(),
+              vtg.data_ptr(), part.data_ptr(), None)
+    _lib.call("rlks_adv_stats", part.data_ptr(), npart, float(T * N), sums.data_ptr(), None)
+    _lib.call("rlks_adv_finalize", sums.data_ptr(), dyn.data_ptr(), None)
+    ea, ev = oracle.gae(r, v, dn, gamma, lam)
+    close(adv.cpu().numpy(), ea)
+    close(vtg.cpu().numpy(), ev)
+    dd = dyn.cpu().numpy()
+    assert abs(dd[0] - ea.mean()) <= 1e-5 * abs(ea).max()
+    assert abs(1 / dd[1] - max(1e-4, ea.std())) <= 1e-5 * ea.std()
+
+
+def test_gae_golden_vectors():
+    from conftest import GOLDEN
+    from rlks import _lib
+
+    d = _dev()
+    g = np.load(GOLDEN / "gae.npz")
+    for ci in range(3):
+        gamma, lam = g[f"c{ci}_params"]
+        r, v, dn = g[f"c{ci}_r"], g[f"c{ci}_v"], g[f"c{ci}_d"]
+        T, N = r.shape
+        adv = torch.zeros(T, N, device=d)
+        vtg = torch.zeros(T, N, device=d)
+        rt, vt_, dt = (torch.from_numpy(np.ascontiguousarray(x)).to(d) for x in (r, v, dn))
+        _lib.call("rlks_gae", rt.data_ptr(), vt_.data_ptr(), dt.data_ptr(), float(gamma), float(lam), T, N,
+                  adv.data_ptr(), vtg.data_ptr(), None, None)
+        close(adv.cpu().numpy(), g[f"c{ci}_adv"])
+        close(vtg.cpu().numpy(), g[f"c{ci}_vt"])
+
+
+# ----------------------------------------------------------------------------- MLP
+def _params(d, seed=0, D=6, A=2, scale_b=0.1):
+    from rlks.policy import PolicyParams
+
+    p = PolicyParams(D, 256, A, device=d, seed=seed)
+    # non-zero biases so that every bias path is exercised
+    g = torch.Generator().manual_seed(seed + 1)
+    for i in (1, 3, 5, 7, 9, 11):
+        v = p.view(i)
+        v.copy_((torch.randn(v.shape, generator=g) * scale_b).to(d))
+    return p
+
+
+@pytest.mark.parametrize("n", [1, 31, 1000, 70001])
+def test_policy_forward_matches_oracle(n):
+    d = _dev()
+    p = _params(d, seed=n)
+    rng = np.random.default_rng(n)
+    obs = rng.random((n, 6)).astype(np.float32)
+    lg, v = p.forward(torch.from_numpy(obs).to(d))
+    flat = p.flat.cpu().numpy()
+    el, ev = oracle.mlp_forward(flat, p.offsets, 6, 256, 2, obs)
+    close(lg.cpu().numpy(), el)
+    close(v.cpu().numpy(), ev)
+
+
+def _minibatch(rows, rng, D=6, A=2, p=None, d=None):
+    stride = (D + A + 4 + 3) // 4 * 4
+    mb = np.zeros((rows, stride), np.float32)
+    mb[:, :D] = rng.random((rows, D))
+    if p is not None:  # old logits near the current policy, so that ratios straddle the clip range
+        lg, _ = p.forward(torch.from_numpy(mb[:, :D].copy()).to(d))
+        lo = lg.cpu().numpy() + rng.standard_normal((rows, A)).astype(np.float32) * 0.3
+    else:
+        lo = rng.standard_normal((rows, A)).astype(np.float32)
+    mb[:, D:D + A] = lo
+    mb[:, D + A] = rng.standard_normal(rows) * 3 + 0.5
+    mb[:, D + A + 1] = rng.standard_normal(rows) * 2
+    act = rng.integers(0, A, rows)
+    mb[:, D + A + 3] = act
+    lsm = lo - np.log(np.exp(lo - lo.max(1, keepdims=True)).sum(1, keepdims=True)) - lo.max(1, keepdims=True)
+    mb[:, D + A + 2] = lsm[np.arange(rows), act]
+    return mb
+
+
+@pytest.mark.parametrize("rows", [256, 4096])
+def test_ppo_grad_matches_oracle(rows):
+    from rlks import _lib
+
+    d = _dev()
+    p = _params(d, seed=rows)
+    rng = np.random.default_rng(rows)
+    mb = _minibatch(rows, rng, p=p, d=d)
+    # value targets near the current values so that some rows are inside / outside vf_clip
+    _, vv = p.forward(torch.from_numpy(mb[:, :6].copy()).to(d))
+    mb[:, 9] = vv.cpu().numpy() + rng.standard_normal(rows).astype(np.float32) * 4
+    adv_mean, adv_invstd, klc = 0.3, 0.7, 0.2
+    dyn = torch.tensor([adv_mean, adv_invstd, klc, 1.0 / rows, 0, 0, 0, 0], dtype=torch.float32, device=d)
+    co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.01)
+    wsb = C.c_int64()
+    _lib.call("rlks_ppo_workspace_bytes", C.byref(p.desc), rows, C.byref(wsb))
+    ws = torch.empty(wsb.value, dtype=torch.uint8, device=d)
+    grad = torch.zeros(p.padded, device=d)
+    stats = torch.zeros(8, dtype=torch.float64, device=d)
+    mbt = torch.from_numpy(mb).to(d)
+    _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
+              rows, grad.data_ptr(), stats.data_ptr(), ws.data_ptr(), ws.numel(), None)
+    g = grad.cpu().numpy()
+    eg, est = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, 6, 256, 2, mb, entropy_coeff=0.01,
+                                   kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd)
+    from rlks.policy import TENSOR_NAMES
+
+    for i, (name, _, _) in enumerate(TENSOR_NAMES):
+        n = int(np.prod(p.shapes[i]))
+        a = g[p.offsets[i]: p.offsets[i] + n]
+        b = eg[p.offsets[i]: p.offsets[i] + n]
+        assert np.linalg.norm(a - b) <= 1e-5 * np.linalg.norm(b) + 1e-12, name
+        close(a, b)
+    st = stats.cpu().numpy()
+    for k, j in (("policy_loss", 0), ("vf_loss", 1), ("kl", 2), ("entropy", 3)):
+        assert abs(st[j] - est[k]) <= 1e-5 * max(abs(est[k]), 1e-3 * rows), k
+    assert st[4] == rows
+
+
+def test_adam_matches_torch():
+    from rlks import _lib
+
+    d = _dev()
+    rng = np.random.default_rng(0)
+    n = 135939 + 61
+    p, g = rng.standard_normal(n).astype(np.float32), rng.standard_normal(n).astype(np.float32) * 1e-3
+    m, v = rng.standard_normal(n).astype(np.float32) * 1e-4, rng.random(n).astype(np.float32) * 1e-6
+    pt, gt, mt, vt = (torch.from_numpy(x.copy()).to(d) for x in (p, g, m, v))
+    _lib.call("rlks_adam_step", pt.data_ptr(), gt.data_ptr(), mt.data_ptr(), vt.data_ptr(), n, 3e-4, 0.9, 0.999,
+              1e-8, 7, None)
+    ep, em, ev = oracle.adam(p, g, m, v, 7, 3e-4)
+    close(mt.cpu().numpy(), em, 1e-6)
+    close(vt.cpu().numpy(), ev, 1e-6)
+    np.testing.assert_allclose(pt.cpu().numpy(), ep, rtol=0, atol=3e-4 * 1e-4)
+
+
+def test_gather_is_a_permutation_per_epoch():
+    from rlks import _lib
+    from rlks.policy import PolicyParams
+
+    d = _dev()
+    T, N = 128, 4096
+    S = T * N
+    f32 = dict(dtype=torch.float32, device=d)
+    bufs_t = {"obs": torch.zeros(T + 1, N, 6, **f32), "logits": torch.zeros(T, N, 2, **f32),
+              "values": torch.zeros(T + 1, N, **f32), "actions": torch.zeros(T, N, dtype=torch.int32, device=d),
+              "logp": torch.zeros(T, N, **f32), "rewards": torch.zeros(T, N, **f32),
+              "dones": torch.zeros(T, N, dtype=torch.uint8, device=d),
+              "adv": torch.arange(S, dtype=torch.float64, device=d).float().view(T, N), "vtarg": torch.zeros(T, N, **f32)}
+    bufs_t["vtarg"].copy_(torch.arange(S, device=d).view(T, N).float().remainder(4096))
+    b = bufs_t
+    rb = _lib.RolloutBufs(*[b[k].data_ptr() for k in ("obs", "logits", "values", "actions", "logp", "rewards",
+                                                       "dones", "adv", "vtarg")], T, N)
+    desc = _lib.MlpDesc(6, 256, 2, 0)
+    stride = _lib.lib().rlks_minibatch_stride(C.byref(desc))
+    dyn = torch.tensor([0, 1, 0.2, 1, 0, 0, 0, 0], **f32)
+    out = torch.zeros(S, stride, **f32)
+    seen = []
+    for epoch in range(2):
+        for row0 in range(0, S, 65536):
+            _lib.call("rlks_ppo_gather", C.byref(desc), C.byref(rb), 77, epoch, row0, 65536, dyn.data_ptr(),
+                      out[row0:].data_ptr(), None)
+        idx = out[:, 8].double()
+        # adv column carries the sample id (exact in fp32 below 2^24)
+        assert torch.equal(torch.sort(idx).values, torch.arange(S, dtype=torch.float64, device=d))
+        seen.append(idx.clone())
+    assert not torch.equal(seen[0], seen[1])
+
+
+# ----------------------------------------------------------------------------- end to end
+def test_ppo_iteration_parity_and_surface(tmp_path):
+    """one iteration: rollout invariants, GAE vs oracle on the GPU's own buffers, one SGD step's
+    gradient vs the oracle on the gathered minibatch, then the RLlib-style result surface"""
+    from rlks import _lib
+    from rlks.ppo import PPO, PPOConfig
+
+    d = _dev()
+    cfg = (PPOConfig().environment("K8sMultiCloudEnv").framework("torch")
+           .training(train_batch_size=512 * 128, sgd_minibatch_size=8192, num_sgd_iter=2, lr=3e-4, gamma=0.99)
+           .debugging(seed=11))
+    cfg.num_envs = 512
+    algo = PPO(config=cfg, device=d)
+    assert algo.T == 128 and algo.n_mb == 8
+    algo.rollout(explore=True)
+    b = {k: v.cpu().numpy() for k, v in algo.buf.items()}
+    # rollout invariants: rewards are table lookups of the chosen cloud at the lane's step
+    assert set(np.unique(b["actions"])) <= {0, 1}
+    assert b["dones"].sum() > 0
+    # logp consistent with the stored logits
+    lo = b["logits"].astype(np.float64)
+    lsm = lo - np.log(np.exp(lo - lo.max(-1, keepdims=True)).sum(-1, keepdims=True)) - lo.max(-1, keepdims=True)
+    close(np.take_along_axis(lsm, b["actions"][..., None].astype(int), -1)[..., 0], b["logp"], 1e-5)
+    # values of obs[t] recomputed by the oracle
+    flat = algo.params.flat.cpu().numpy()
+    el, ev = oracle.mlp_forward(flat, algo.params.offsets, 6, 256, 2, b["obs"][:4].reshape(-1, 6))
+    close(b["values"][:4].reshape(-1), ev)
+    algo.advantages()
+    ea, evt = oracle.gae(b["rewards"], b["values"], b["dones"], 0.99, 1.0)
+    close(algo.buf["adv"].cpu().numpy(), ea)
+    close(algo.buf["vtarg"].cpu().numpy(), evt)
+    # one SGD step: gradient vs oracle on the gathered minibatch
+    _lib.call("rlks_ppo_gather", C.byref(algo.params.desc), C.byref(algo.bufs), 5, 0, 0, algo.mb,
+              algo.dyn.data_ptr(), algo.mbuf.data_ptr(), None)
+    mb = algo.mbuf.cpu().numpy()
+    dyn = algo.dyn.cpu().numpy()
+    wsb = algo.ws
+    _lib.call("rlks_ppo_grad", C.byref(algo.params.desc), C.byref(algo.coeffs), algo.params.flat.data_ptr(),
+              algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, wsb.data_ptr(),
+              wsb.numel(), None)
+    eg, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 6, 256, 2, mb, kl_coeff=float(dyn[2]),
+                                 adv_mean=float(dyn[0]), adv_inv_std=float(dyn[1]))
+    g = algo.grad.cpu().numpy()
+    assert np.linalg.norm(g - eg) <= 1e-5 * np.linalg.norm(eg)
+    # full iterations through the RLlib-named surface
+    r1 = algo.train()
+    r2 = algo.train()
+    for r in (r1, r2):
+        assert np.isfinite(r["episode_reward_mean"]) and r["episodes_this_iter"] > 0
+        assert 3000 < r["episode_reward_mean"] < 6300  # per-step min/max returns bound it
+        ls = r["info"]["learner"]["default_policy"]["learner_stats"]
+        assert np.isfinite(ls["policy_loss"]) and np.isfinite(ls["vf_loss"]) and ls["kl"] >= 0
+    assert r2["training_iteration"] == algo.iteration and r2["timesteps_total"] == algo.samples * algo.iteration
+    a0 = algo.compute_single_action(np.full(6, 0.5, np.float32), explore=False)
+    path = algo.save(tmp_path)
+    algo2 = PPO.from_checkpoint(path, device=d)
+    assert torch.equal(algo2.params.flat, algo.params.flat) and algo2.iteration == algo.iteration
+    assert algo2.compute_single_action(np.full(6, 0.5, np.float32), explore=False) == a0
