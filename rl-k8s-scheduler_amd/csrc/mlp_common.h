@@ -1,0 +1,121 @@
+// mlp_common.h — shared pieces of the policy/value MLP kernels (K4): flat parameter layout,
+// fp32 MFMA helpers, the fast tanh and the argument blocks of the SGD-step kernels.
+//
+// Reference: RLlib's default torch FCNet behind PPOConfig().framework("torch")
+// (train_ppo.py:12): pi = D -> 256 tanh -> 256 tanh -> A, vf = D -> 256 tanh -> 256 tanh -> 1,
+// vf_share_layers=False.  RLlib is third-party (absent here); see DESIGN.md §3.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rlks_internal.h"
+
+namespace rlks {
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+constexpr int HID = 256;   // hidden width the fused kernels are built for (fcnet_hiddens [256, 256])
+constexpr int MAXA = 8;    // max actions (clusters)
+constexpr int DMAX = 32;   // max obs dim of the VALU input layer
+constexpr int BK = 32;     // reduction chunk staged in LDS
+constexpr int GB = 128;    // F2/F3 block tile (4 waves of 64 x 64)
+
+// v_mfma_f32_32x32x2_f32: exact f32 fma chain in k order (cdna_hip_programming.md §3)
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// row of accumulator register r for lane l (v_mfma_f32_32x32x* C/D map; col = l & 31)
+__device__ __forceinline__ int acc_row(int r, int l) { return (r & 3) + 8 * (r >> 2) + 4 * (l >> 5); }
+
+// tanh in ~14 VALU ops (ocml tanhf is ~35): odd minimax polynomial for |x| < 0.6, else
+// 1 - 2 / (exp(2|x|) + 1) with v_exp_f32 / v_rcp_f32.  Max relative error 1.8e-7 (~3 ulp) over
+// all of fp32, measured against float64 tanh (tools/fit_tanh.py); far inside the 1e-5 parity bar.
+__device__ __forceinline__ float fast_tanh(float x) {
+  const float ax = fabsf(x);
+  const float e = __builtin_amdgcn_exp2f(ax * 2.885390081777927f);
+  const float big = 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+  const float x2 = x * x;
+  float p = -0.006104227155447006f;
+  p = fmaf(p, x2, 0.020971255376935005f);
+  p = fmaf(p, x2, -0.05383438989520073f);
+  p = fmaf(p, x2, 0.1333249807357788f);
+  p = fmaf(p, x2, -0.33333319425582886f);
+  const float small = fmaf(x * x2, p, x);
+  return ax < 0.6f ? small : __builtin_copysignf(big, x);
+}
+
+// ----------------------------------------------------------------------------- layout
+struct Layout {
+  int64_t off[RLKS_N_TENSORS];
+  int64_t padded, real;
+};
+
+inline Layout make_layout(int D, int H, int A) {
+  const int64_t sz[RLKS_N_TENSORS] = {(int64_t)H * D, H, (int64_t)H * H, H, (int64_t)A * H, A,
+                                      (int64_t)H * D, H, (int64_t)H * H, H, H, 1};
+  Layout L{};
+  int64_t o = 0;
+  for (int i = 0; i < RLKS_N_TENSORS; ++i) {
+    L.off[i] = o;
+    o += (sz[i] + 63) / 64 * 64;
+    L.real += sz[i];
+  }
+  L.padded = o;
+  return L;
+}
+
+struct NetPtrs {
+  const float *w1, *b1, *w2, *b2, *w3, *b3;
+};
+
+inline NetPtrs net_ptrs_host(const float* p, const Layout& L, int net) {
+  const int64_t* o = L.off + 6 * net;
+  return NetPtrs{p + o[0], p + o[1], p + o[2], p + o[3], p + o[4], p + o[5]};
+}
+
+// packed minibatch record: [obs D | logits_old A | adv | vtarg | logp_old | action | pad]
+inline int mb_stride(int D, int A) { return (D + A + 4 + 3) / 4 * 4; }
+
+// ----------------------------------------------------------------------------- F1 arguments
+struct FwdArgs {
+  NetPtrs P;          // this net's tensors
+  const float* x;     // row m at x + m * x_stride (obs = first D floats)
+  int x_stride;
+  int M, D, A_pi;     // A_pi: pi action count (record layout)
+  float* out;         // forward-only: logits [M][A] (pi) or values [M] (vf)
+  rlks_ppo_coeffs co;
+  const float* dyn;
+  float* dz2;         // this net's [M][HID]
+  float* part_b2;     // [tiles][HID]
+  float* part_w3;     // [tiles][A_][HID]
+  float* part_b3;     // [tiles][A_]
+  float* part_stat;   // [tiles][4]
+};
+
+// ----------------------------------------------------------------------------- F2 / F3 arguments
+struct Dw2Args {
+  NetPtrs P;
+  const float* x;
+  int x_stride;
+  int M, rows_per_split;
+  const float* dz2;   // this net's [M][HID]
+  float* part;        // [S][HID][HID]
+};
+
+struct Dh1Args {
+  NetPtrs P;
+  const float* x;
+  int x_stride;
+  int M;
+  const float* dz2;   // this net's [M][HID]
+  float* part_w1;     // [tiles][HID][D]
+  float* part_b1;     // [tiles][HID]
+};
+
+// host launchers (mlp_fwd.hip / mlp_bwd.hip)
+int launch_fwd_head(const FwdArgs& a, int net, int A, bool train, hipStream_t s);
+int launch_dw2(const Dw2Args& a, int D, int splits, hipStream_t s);
+int launch_dh1(const Dh1Args& a, int D, hipStream_t s);
+
+}  // namespace rlks

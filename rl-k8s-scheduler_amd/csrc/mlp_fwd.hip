@@ -1,0 +1,345 @@
+// mlp_fwd.hip — F1: fused FCNet forward + head + PPO loss + dZ2 for one net (pi or vf).
+//
+// Per workgroup: BMr = 32*WM rows of the minibatch (or rollout obs), all HID = 256 hidden columns.
+//   H1 = tanh(X W1^T + b1)      VALU (K = D = 6), computed chunk-wise straight into LDS
+//   Z2 = H1 W2^T                v_mfma_f32_32x32x2_f32; W2 chunks staged through LDS, the next
+//                               chunk's global loads in flight (registers) during the MFMAs
+//   H2 = tanh(Z2 + b2)          in the accumulators
+//   out = H2 W3^T + b3          VALU dot + half-wave butterfly reduce-scatter + LDS across waves
+// Forward-only (rollout): write logits / values.  Training additionally:
+//   pi: ratio, clipped surrogate, KL(old||new), entropy -> dlogits     (RLlib ppo_torch_policy.loss)
+//   vf: clamp((V - vt)^2, 0, vf_clip) -> dV
+//   dZ2 = (dout W3) * (1 - H2^2) -> HBM (the only activation that leaves the chip), and per-tile
+//   partial sums of db2 = colsum dZ2, dW3 = dout^T H2, db3, loss stats (fixed-order reduction
+//   later, so the gradient is bit-reproducible run to run).
+#include "mlp_common.h"
+
+namespace rlks {
+
+// reduce 16 per-lane values (register r <-> accumulator row) over the 32 lanes of a half-wave;
+// afterwards lane l holds the total of register ((l >> 1) & 15) (lanes l and l^1 agree)
+__device__ __forceinline__ float half_wave_reduce16(const float (&v)[16], int l) {
+  float v8[8], v4[4], v2[2];
+  {
+    const bool b = (l >> 4) & 1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v8[j] = (b ? v[j + 8] : v[j]) + __shfl_xor(b ? v[j] : v[j + 8], 16, 64);
+  }
+  {
+    const bool b = (l >> 3) & 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v4[j] = (b ? v8[j + 4] : v8[j]) + __shfl_xor(b ? v8[j] : v8[j + 4], 8, 64);
+  }
+  {
+    const bool b = (l >> 2) & 1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) v2[j] = (b ? v4[j + 2] : v4[j]) + __shfl_xor(b ? v4[j] : v4[j + 2], 4, 64);
+  }
+  const bool b = (l >> 1) & 1;
+  float v1 = (b ? v2[1] : v2[0]) + __shfl_xor(b ? v2[0] : v2[1], 2, 64);
+  return v1 + __shfl_xor(v1, 1, 64);
+}
+
+template <int A_, int NET, int WM, int WN, bool TRAIN>
+__global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
+  constexpr int H = HID;
+  constexpr int NT = H / (32 * WN);     // 32-column accumulator tiles per wave
+  constexpr int BMr = 32 * WM;          // rows per workgroup
+  constexpr int NTHR = 64 * WM * WN;
+  constexpr int F4 = H * BK / 4 / NTHR; // float4 of the W2 chunk per thread
+  static_assert(NT * 32 * WN == H && F4 * 4 * NTHR == H * BK, "tile split");
+  static_assert(WM * H * (1 + A_) <= H * (BK + 1) + BK * BMr, "epilogue reduction must fit in the staging buffers");
+  static_assert(BMr <= 128, "loss rows are handled by the first two waves");
+
+  const int D = g.D, ds = g.D + 1;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* sB = lds;                       // [H][BK+1]   W2 chunk [n][k]
+  float* sA = sB + H * (BK + 1);         // [BK][BMr]   H1 chunk [k][m]
+  float* sHead = sA + BK * BMr;          // [WN][BMr][A_]
+  float* sDl = sHead + WN * BMr * A_;    // [BMr][A_]
+  float* sStat = sDl + BMr * A_;         // [2][A_ + 4]
+  float* sb1 = sStat + 2 * (A_ + 4);     // [H]
+  float* sX = sb1 + H;                   // [BMr][D+1]
+  float* sW1 = sX + BMr * ds;            // [H][D+1]
+
+  const NetPtrs& P = g.P;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int h = l >> 5, li = l & 31;
+  const int row0 = blockIdx.x * BMr;
+
+  for (int e = tid; e < BMr * D; e += NTHR) {
+    const int m = e / D, d = e - m * D;
+    sX[m * ds + d] = (row0 + m < g.M) ? g.x[(size_t)(row0 + m) * g.x_stride + d] : 0.f;
+  }
+  for (int e = tid; e < H * D; e += NTHR) sW1[(e / D) * ds + (e % D)] = P.w1[e];
+  for (int e = tid; e < H; e += NTHR) sb1[e] = P.b1[e];
+
+  float4 pre[F4];
+  auto load_w2 = [&](int kc) {
+#pragma unroll
+    for (int j = 0; j < F4; ++j) {
+      const int e = tid + j * NTHR, n = e >> 3, k4 = e & 7;
+      pre[j] = *reinterpret_cast<const float4*>(P.w2 + (size_t)n * H + kc + 4 * k4);
+    }
+  };
+  load_w2(0);
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[nt][r] = 0.f;
+
+  __syncthreads();  // sX / sW1 / sb1 staged
+  for (int kc = 0; kc < H; kc += BK) {
+#pragma unroll
+    for (int j = 0; j < F4; ++j) {
+      const int e = tid + j * NTHR, n = e >> 3, k4 = e & 7;
+      float* dst = sB + n * (BK + 1) + 4 * k4;
+      dst[0] = pre[j].x; dst[1] = pre[j].y; dst[2] = pre[j].z; dst[3] = pre[j].w;
+    }
+    // H1 chunk: sA[k][m] = tanh(b1[k] + X[m] . W1[k])
+    for (int e = tid; e < BK * BMr; e += NTHR) {
+      const int kk = e / BMr, m = e - kk * BMr;
+      const float* wr = sW1 + (kc + kk) * ds;
+      const float* xr = sX + m * ds;
+      float z = sb1[kc + kk];
+      for (int d = 0; d < D; ++d) z = fmaf(xr[d], wr[d], z);
+      sA[kk * BMr + m] = fast_tanh(z);
+    }
+    __syncthreads();
+    if (kc + BK < H) load_w2(kc + BK);  // next chunk in flight during the MFMAs
+#pragma unroll 4
+    for (int s = 0; s < BK / 2; ++s) {
+      const int k = 2 * s + h;
+      const float a = sA[k * BMr + wm * 32 + li];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma32(a, sB[((wn * NT + nt) * 32 + li) * (BK + 1) + k], acc[nt]);
+    }
+    __syncthreads();
+  }
+
+  // ---- H2 = tanh(Z2 + b2); head partial dot products over this wave's columns
+  float w3r[NT][A_];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n = (wn * NT + nt) * 32 + li;
+    const float bb = P.b2[n];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[nt][r] = fast_tanh(acc[nt][r] + bb);
+#pragma unroll
+    for (int a = 0; a < A_; ++a) w3r[nt][a] = P.w3[(size_t)a * H + n];
+  }
+#pragma unroll
+  for (int a = 0; a < A_; ++a) {
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float s = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) s = fmaf(acc[nt][r], w3r[nt][a], s);
+      v[r] = s;
+    }
+    const float tot = half_wave_reduce16(v, l);
+    if ((l & 1) == 0) sHead[(wn * BMr + wm * 32 + acc_row((l >> 1) & 15, l)) * A_ + a] = tot;
+  }
+  __syncthreads();
+
+  // ---- per-row output, loss and dout (one thread per row)
+  float st_pl = 0.f, st_vf = 0.f, st_kl = 0.f, st_ent = 0.f;
+  if (tid < BMr) {
+    const int m = row0 + tid;
+    float out[A_];
+#pragma unroll
+    for (int a = 0; a < A_; ++a) {
+      float s = P.b3[a];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) s += sHead[(j * BMr + tid) * A_ + a];
+      out[a] = s;
+    }
+    if (!TRAIN) {
+      if (m < g.M)
+#pragma unroll
+        for (int a = 0; a < A_; ++a) g.out[(size_t)m * A_ + a] = out[a];
+    } else {
+      float dl[A_];
+#pragma unroll
+      for (int a = 0; a < A_; ++a) dl[a] = 0.f;
+      if (m < g.M) {
+        const float* rec = g.x + (size_t)m * g.x_stride;
+        const float inv_count = g.dyn[RLKS_DYN_INV_COUNT];
+        const int Ap = g.A_pi;
+        if (NET == 0) {
+          const float* lo = rec + D;
+          const float adv = (rec[D + Ap] - g.dyn[RLKS_DYN_ADV_MEAN]) * g.dyn[RLKS_DYN_ADV_INVSTD];
+          const float logp_old = rec[D + Ap + 2];
+          const int act = (int)rec[D + Ap + 3];
+          float mx = out[0], mo = lo[0];
+#pragma unroll
+          for (int a = 1; a < A_; ++a) { mx = fmaxf(mx, out[a]); mo = fmaxf(mo, lo[a]); }
+          float se = 0.f, so = 0.f;
+#pragma unroll
+          for (int a = 0; a < A_; ++a) { se += expf(out[a] - mx); so += expf(lo[a] - mo); }
+          const float lse = mx + logf(se), lso = mo + logf(so);
+          float p[A_], lp[A_], po[A_];
+          float kl = 0.f, ent = 0.f, lpa = 0.f;
+#pragma unroll
+          for (int a = 0; a < A_; ++a) {
+            lp[a] = out[a] - lse;
+            p[a] = expf(lp[a]);
+            const float lpo = lo[a] - lso;
+            po[a] = expf(lpo);
+            kl += po[a] * (lpo - lp[a]);
+            ent -= p[a] * lp[a];
+            lpa = (a == act) ? lp[a] : lpa;
+          }
+          const float ratio = expf(lpa - logp_old);
+          const float lo_c = 1.f - g.co.clip_param, hi_c = 1.f + g.co.clip_param;
+          const float rc = fminf(fmaxf(ratio, lo_c), hi_c);
+          const float s1 = adv * ratio, s2 = adv * rc;
+          // torch.min backward splits ties evenly; torch.clamp passes the gradient on [lo, hi]
+          const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+          const float inr = (ratio >= lo_c && ratio <= hi_c) ? 1.f : 0.f;
+          const float dr = -adv * (w1 + (1.f - w1) * inr) * ratio;  // dL / dlogp(act)
+          const float klc = g.dyn[RLKS_DYN_KL_COEFF];
+#pragma unroll
+          for (int a = 0; a < A_; ++a) {
+            float d = dr * ((a == act ? 1.f : 0.f) - p[a]);
+            d += klc * (p[a] - po[a]);
+            d += g.co.entropy_coeff * p[a] * (lp[a] + ent);
+            dl[a] = d * inv_count;
+          }
+          st_pl = -fminf(s1, s2);
+          st_kl = kl;
+          st_ent = ent;
+        } else {
+          const float diff = out[0] - rec[D + Ap + 1];
+          const float sq = diff * diff;
+          st_vf = fminf(sq, g.co.vf_clip_param);
+          dl[0] = (sq <= g.co.vf_clip_param) ? g.co.vf_loss_coeff * 2.f * diff * inv_count : 0.f;
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < A_; ++a) sDl[tid * A_ + a] = dl[a];
+    }
+  }
+  if (!TRAIN) return;
+  __syncthreads();
+
+  // ---- dZ2 = (dout W3) * (1 - H2^2); column partials of db2 and dW3 over this tile's rows
+  float csum[NT], cw3[NT][A_];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    csum[nt] = 0.f;
+#pragma unroll
+    for (int a = 0; a < A_; ++a) cw3[nt][a] = 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = wm * 32 + acc_row(r, l);
+    float dlr[A_];
+#pragma unroll
+    for (int a = 0; a < A_; ++a) dlr[a] = sDl[row * A_ + a];
+    float* dst = g.dz2 + (size_t)(row0 + row) * H + wn * NT * 32 + li;
+    const bool valid = row0 + row < g.M;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const float h2 = acc[nt][r];
+      float dh = 0.f;
+#pragma unroll
+      for (int a = 0; a < A_; ++a) {
+        dh = fmaf(dlr[a], w3r[nt][a], dh);
+        cw3[nt][a] = fmaf(dlr[a], h2, cw3[nt][a]);
+      }
+      const float dz = dh * (1.f - h2 * h2);
+      csum[nt] += dz;
+      if (valid) dst[nt * 32] = dz;
+    }
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    csum[nt] += __shfl_xor(csum[nt], 32, 64);
+#pragma unroll
+    for (int a = 0; a < A_; ++a) cw3[nt][a] += __shfl_xor(cw3[nt][a], 32, 64);
+  }
+  float* sRed = sB;  // [WM][H] db2, then [WM][A_][H] dW3 (over the dead W2 / H1 chunk buffers)
+  if (l < 32) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = (wn * NT + nt) * 32 + l;
+      sRed[wm * H + n] = csum[nt];
+#pragma unroll
+      for (int a = 0; a < A_; ++a) sRed[WM * H + (wm * A_ + a) * H + n] = cw3[nt][a];
+    }
+  }
+  // db3 and loss stats: rows live in threads < BMr (waves 0, 1)
+  if (w < 2) {
+    float v[A_ + 4];
+#pragma unroll
+    for (int a = 0; a < A_; ++a) v[a] = (tid < BMr) ? sDl[tid * A_ + a] : 0.f;
+    v[A_] = st_pl; v[A_ + 1] = st_vf; v[A_ + 2] = st_kl; v[A_ + 3] = st_ent;
+#pragma unroll
+    for (int c = 0; c < A_ + 4; ++c) {
+      const float s = wave_sum(v[c]);
+      if (l == 0) sStat[w * (A_ + 4) + c] = s;
+    }
+  }
+  __syncthreads();
+  const int tile = blockIdx.x;
+  for (int n = tid; n < H; n += NTHR) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < WM; ++j) s += sRed[j * H + n];
+    g.part_b2[(size_t)tile * H + n] = s;
+#pragma unroll
+    for (int a = 0; a < A_; ++a) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < WM; ++j) t += sRed[WM * H + (j * A_ + a) * H + n];
+      g.part_w3[((size_t)tile * A_ + a) * H + n] = t;
+    }
+  }
+  if (tid < A_ + 4) {
+    const float s = sStat[tid] + sStat[A_ + 4 + tid];
+    if (tid < A_) g.part_b3[(size_t)tile * A_ + tid] = s;
+    else g.part_stat[(size_t)tile * 4 + tid - A_] = s;
+  }
+}
+
+template <int WM, int WN>
+static size_t fwd_lds_bytes(int A_, int D) {
+  constexpr int BMr = 32 * WM;
+  return ((size_t)HID * (BK + 1) + BK * BMr + WN * BMr * A_ + BMr * A_ + 2 * (A_ + 4) + HID +
+          (size_t)(BMr + HID) * (D + 1)) * sizeof(float);
+}
+
+template <int A_, int NET, int WM, int WN, bool TRAIN>
+static int launch_cfg(const FwdArgs& a, hipStream_t s) {
+  constexpr int BMr = 32 * WM;
+  const size_t lds = fwd_lds_bytes<WM, WN>(A_, a.D);
+  hipLaunchKernelGGL((k_fwd_head<A_, NET, WM, WN, TRAIN>), dim3(cdiv(a.M, BMr)), dim3(64 * WM * WN), lds, s, a);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+template <int A_, int NET>
+static int launch_net(const FwdArgs& a, bool train, hipStream_t s) {
+  if (train) return launch_cfg<A_, NET, 4, 2, true>(a, s);
+  // forward only: small batches (rollouts of a few thousand lanes) use 32-row tiles with the
+  // 4 waves split over columns so that more CUs get work; large batches use 128-row tiles
+  if (a.M <= 32 * 1024) return launch_cfg<A_, NET, 1, 4, false>(a, s);
+  return launch_cfg<A_, NET, 4, 2, false>(a, s);
+}
+
+int launch_fwd_head(const FwdArgs& a, int net, int A, bool train, hipStream_t s) {
+  if (net == 1) return launch_net<1, 1>(a, train, s);
+  switch (A) {
+    case 2: return launch_net<2, 0>(a, train, s);
+    case 4: return launch_net<4, 0>(a, train, s);
+    case 8: return launch_net<8, 0>(a, train, s);
+    default: return fail(RLKS_ERR_UNSUPPORTED, "fused policy head is built for 2, 4 or 8 actions");
+  }
+}
+
+}  // namespace rlks

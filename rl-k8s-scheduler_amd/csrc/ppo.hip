@@ -1,0 +1,405 @@
+// ppo.hip — host API of the policy/value MLP and the PPO update (include/rlks.h, section K4):
+// layout, forward, minibatch gather, gradient orchestration (F1 -> F2 -> F3 -> reduce), Adam,
+// KL-coefficient update and the rollout loop.
+//
+// Reference: RLlib PPO behind train_ppo.py:9-31 (train_batch_size 4000, sgd_minibatch_size 256,
+// num_sgd_iter 10, lr 3e-4, gamma 0.99) and train_final.py:6-20.  RLlib is third-party and absent
+// from /root/reference: the restated semantics are pinned against oracle/oracle.py.
+#include <cmath>
+
+#include "mlp_common.h"
+
+namespace rlks {
+
+// ----------------------------------------------------------------------------- reduce
+// out[i] = sum_p part[p * pstride + i] (i < len, p < P) in a fixed order with f64 accumulation.
+// A block = OPB outputs x G partial-groups (OPB * G = 256); G is chosen per task so that every
+// thread sums about 16 partials, so narrow tasks (b3, stats) do not leave a serial tail.
+struct RedTask {
+  const float* part;
+  float* out;        // float output ...
+  double* out64;     // ... or double output (stats)
+  int64_t pstride;
+  int P, len, G;
+  int blk0;
+};
+constexpr int MAX_TASKS = 16;
+struct RedArgs {
+  RedTask t[MAX_TASKS];
+  int ntasks;
+};
+
+__global__ __launch_bounds__(256) void k_reduce(RedArgs g) {
+  __shared__ double sh[256];
+  int ti = 0;
+  while (ti + 1 < g.ntasks && (int)blockIdx.x >= g.t[ti + 1].blk0) ++ti;
+  const RedTask T = g.t[ti];
+  const int opb = 256 / T.G;
+  const int o = threadIdx.x % opb, grp = threadIdx.x / opb;
+  const int i = ((int)blockIdx.x - T.blk0) * opb + o;
+  double s = 0.0;
+  if (i < T.len)
+    for (int p = grp; p < T.P; p += T.G) s += (double)T.part[(int64_t)p * T.pstride + i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  if (grp == 0 && i < T.len) {
+    double t = 0.0;
+    for (int j = 0; j < T.G; ++j) t += sh[j * opb + o];
+    if (T.out64) T.out64[i] = t;
+    else T.out[i] = (float)t;
+  }
+}
+
+struct Reducer {
+  RedArgs a{};
+  int blocks = 0;
+  void add(const float* part, float* out, double* out64, int64_t pstride, int P, int len) {
+    RedTask& t = a.t[a.ntasks++];
+    int G = 1;
+    while (G < 256 && G * 16 < P) G *= 2;
+    t.part = part; t.out = out; t.out64 = out64; t.pstride = pstride; t.P = P; t.len = len; t.G = G;
+    t.blk0 = blocks;
+    blocks += (int)cdiv(len, 256 / G);
+  }
+};
+
+__global__ void k_stats_finish(double* __restrict__ st, const double* __restrict__ s_pi,
+                               const double* __restrict__ s_vf, int rows) {
+  if (threadIdx.x) return;
+  st[RLKS_STAT_POLICY_LOSS] = s_pi[0];
+  st[RLKS_STAT_VF_LOSS] = s_vf[1];
+  st[RLKS_STAT_KL] = s_pi[2];
+  st[RLKS_STAT_ENTROPY] = s_pi[3];
+  st[RLKS_STAT_ROWS] = (double)rows;
+  st[5] = st[6] = st[7] = 0.0;
+}
+
+// ----------------------------------------------------------------------------- Adam
+// torch.optim.Adam (single-tensor path): exp_avg.lerp_(g, 1-b1); exp_avg_sq = b2*v + (1-b2)*g*g;
+// p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, int64_t n, float w1, float b2, float omb2, float step_size,
+                       float bc2_sqrt, float eps) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i];
+  const float mi = m[i] + w1 * (gi - m[i]);
+  const float vi = b2 * v[i] + omb2 * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = p[i] - step_size * (mi / denom);
+}
+
+// RLlib PPO update_kl
+__global__ void k_kl_update(float* __restrict__ dyn, const double* __restrict__ kc, float target) {
+  if (threadIdx.x) return;
+  const double kl = kc[1] > 0 ? kc[0] / kc[1] : 0.0;
+  float c = dyn[RLKS_DYN_KL_COEFF];
+  if (kl > 2.0 * target) c *= 1.5f;
+  else if (kl < 0.5 * target) c *= 0.5f;
+  dyn[RLKS_DYN_KL_COEFF] = c;
+}
+
+// ----------------------------------------------------------------------------- gather
+// Balanced Feistel bijection on [0, 2^(2*half)) with per-epoch round keys, cycle-walked into
+// [0, S): a fresh uniform-looking permutation of the train batch every epoch with no sort.
+struct Perm {
+  uint32_t key[4];
+  uint32_t half, mask;
+  uint64_t S;
+};
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du;
+  x ^= x >> 15; x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint64_t perm_apply(const Perm& P, uint64_t x) {
+  do {
+    uint32_t L = (uint32_t)(x >> P.half), R = (uint32_t)x & P.mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t nl = R;
+      R = (L ^ mix32(R ^ P.key[r])) & P.mask;
+      L = nl;
+    }
+    x = ((uint64_t)L << P.half) | R;
+  } while (x >= P.S);
+  return x;
+}
+
+struct GatherArgs {
+  rlks_rollout_bufs b;
+  Perm perm;
+  int64_t row0;
+  int rows, D, A, stride;
+  float* mb;
+};
+
+__global__ void k_gather(GatherArgs g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.rows) return;
+  const uint64_t s = perm_apply(g.perm, (uint64_t)(g.row0 + i));
+  const int64_t tn = (int64_t)s;  // = t * N + n of the time-major buffers
+  float* rec = g.mb + (size_t)i * g.stride;
+  const float* o = g.b.obs + tn * g.D;
+  for (int d = 0; d < g.D; ++d) rec[d] = o[d];
+  const float* lo = g.b.logits + tn * g.A;
+  for (int a = 0; a < g.A; ++a) rec[g.D + a] = lo[a];
+  rec[g.D + g.A] = g.b.adv[tn];
+  rec[g.D + g.A + 1] = g.b.vtarg[tn];
+  rec[g.D + g.A + 2] = g.b.logp[tn];
+  rec[g.D + g.A + 3] = (float)g.b.actions[tn];
+  for (int j = g.D + g.A + 4; j < g.stride; ++j) rec[j] = 0.f;
+}
+
+static Perm make_perm(uint64_t seed, int epoch, uint64_t S) {
+  Perm P{};
+  uint32_t bits = 2;
+  while ((1ull << bits) < S) ++bits;
+  if (bits & 1) ++bits;
+  P.half = bits / 2;
+  P.mask = (P.half >= 32) ? 0xffffffffu : ((1u << P.half) - 1u);
+  P.S = S;
+  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(epoch + 1));
+  for (int r = 0; r < 4; ++r) {  // splitmix64 round keys
+    z += 0x9E3779B97F4A7C15ull;
+    uint64_t x = z;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    P.key[r] = (uint32_t)(x ^ (x >> 31));
+  }
+  return P;
+}
+
+// ----------------------------------------------------------------------------- workspace
+struct NetWs {
+  float *dz2, *part_b2, *part_w3, *part_b3, *part_stat, *part_w2, *part_w1, *part_b1;
+};
+struct Ws {
+  NetWs n[2];
+  double* stat64;  // [2][4]
+  int64_t bytes;
+  int tiles, splits;
+};
+
+static int pick_splits(int M) {
+  // F2 grid = 4 tiles x 2 nets x S: about two workgroups per CU, >= 4 chunks of rows per split
+  int s = 1;
+  while (s * 2 * 8 <= 512 && (M / (s * 2)) % BK == 0 && M / (s * 2) >= 4 * BK) s *= 2;
+  return s;
+}
+
+static Ws ws_layout(int D, int A, int M, char* base) {
+  Ws w{};
+  w.tiles = M / GB;
+  w.splits = pick_splits(M);
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    char* p = base ? base + o : nullptr;
+    o += (bytes + 255) / 256 * 256;
+    return p;
+  };
+  for (int net = 0; net < 2; ++net) {
+    const int An = net == 0 ? A : 1;
+    NetWs& n = w.n[net];
+    n.dz2 = (float*)take(4LL * M * HID);
+    n.part_b2 = (float*)take(4LL * w.tiles * HID);
+    n.part_w3 = (float*)take(4LL * w.tiles * An * HID);
+    n.part_b3 = (float*)take(4LL * w.tiles * An);
+    n.part_stat = (float*)take(4LL * w.tiles * 4);
+    n.part_w2 = (float*)take(4LL * w.splits * HID * HID);
+    n.part_w1 = (float*)take(4LL * w.tiles * HID * D);
+    n.part_b1 = (float*)take(4LL * w.tiles * HID);
+  }
+  w.stat64 = (double*)take(8 * 8);
+  w.bytes = o;
+  return w;
+}
+
+static int check_desc(const rlks_mlp_desc* d) {
+  RLKS_REQUIRE(d, RLKS_ERR_ARG, "null mlp desc");
+  RLKS_REQUIRE(d->obs_dim > 0 && d->obs_dim <= DMAX, RLKS_ERR_UNSUPPORTED, "obs_dim must be in [1, 32]");
+  RLKS_REQUIRE(d->n_actions == 2 || d->n_actions == 4 || d->n_actions == 8, RLKS_ERR_UNSUPPORTED,
+               "n_actions must be 2, 4 or 8");
+  RLKS_REQUIRE(d->hidden == HID, RLKS_ERR_UNSUPPORTED, "fused MLP kernels are built for hidden = 256");
+  return RLKS_OK;
+}
+
+}  // namespace rlks
+
+using namespace rlks;
+
+extern "C" {
+
+int rlks_mlp_layout(const rlks_mlp_desc* d, int64_t* offsets, int64_t* padded, int64_t* real) {
+  RLKS_REQUIRE(d && d->obs_dim > 0 && d->hidden > 0 && d->n_actions > 0, RLKS_ERR_ARG, "rlks_mlp_layout: bad desc");
+  const Layout L = make_layout(d->obs_dim, d->hidden, d->n_actions);
+  if (offsets)
+    for (int i = 0; i < RLKS_N_TENSORS; ++i) offsets[i] = L.off[i];
+  if (padded) *padded = L.padded;
+  if (real) *real = L.real;
+  return RLKS_OK;
+}
+
+int rlks_policy_forward(const rlks_mlp_desc* d, const float* params, const float* obs, int n, float* logits,
+                        float* values, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(params && obs && n >= 0, RLKS_ERR_ARG, "rlks_policy_forward: bad argument");
+  if (n == 0) return RLKS_OK;
+  const Layout L = make_layout(d->obs_dim, d->hidden, d->n_actions);
+  hipStream_t s = (hipStream_t)stream;
+  for (int net = 0; net < 2; ++net) {
+    float* out = net == 0 ? logits : values;
+    if (!out) continue;
+    FwdArgs a{};
+    a.P = net_ptrs_host(params, L, net);
+    a.x = obs; a.x_stride = d->obs_dim; a.M = n; a.D = d->obs_dim; a.A_pi = d->n_actions; a.out = out;
+    if (int rc = launch_fwd_head(a, net, d->n_actions, false, s)) return rc;
+  }
+  return RLKS_OK;
+}
+
+int rlks_minibatch_stride(const rlks_mlp_desc* d) { return d ? mb_stride(d->obs_dim, d->n_actions) : 0; }
+
+int rlks_ppo_gather(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, uint64_t perm_seed, int epoch,
+                    int64_t row0, int rows, const float* dyn, float* mb, void* stream) {
+  RLKS_REQUIRE(d && b && mb && rows >= 0, RLKS_ERR_ARG, "rlks_ppo_gather: bad argument");
+  (void)dyn;  // advantages are standardised inside the loss kernel from dyn
+  const uint64_t S = (uint64_t)b->T * (uint64_t)b->N;
+  RLKS_REQUIRE(row0 >= 0 && (uint64_t)(row0 + rows) <= S, RLKS_ERR_ARG, "rlks_ppo_gather: rows out of range");
+  if (rows == 0) return RLKS_OK;
+  GatherArgs g{};
+  g.b = *b;
+  g.perm = make_perm(perm_seed, epoch, S);
+  g.row0 = row0;
+  g.rows = rows;
+  g.D = d->obs_dim;
+  g.A = d->n_actions;
+  g.stride = mb_stride(d->obs_dim, d->n_actions);
+  g.mb = mb;
+  hipLaunchKernelGGL(k_gather, dim3(cdiv(rows, 256)), dim3(256), 0, (hipStream_t)stream, g);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_ppo_workspace_bytes(const rlks_mlp_desc* d, int rows, int64_t* bytes) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(bytes && rows > 0 && rows % GB == 0, RLKS_ERR_ARG,
+               "rlks_ppo_workspace_bytes: rows must be a positive multiple of 128");
+  *bytes = ws_layout(d->obs_dim, d->n_actions, rows, nullptr).bytes;
+  return RLKS_OK;
+}
+
+int rlks_ppo_grad_phases(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
+                         const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes,
+                         int phases, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(co && params && dyn && mb && grad && workspace, RLKS_ERR_ARG, "rlks_ppo_grad: null argument");
+  RLKS_REQUIRE(M > 0 && M % GB == 0, RLKS_ERR_ARG, "rlks_ppo_grad: rows must be a positive multiple of 128");
+  const int D = d->obs_dim, A = d->n_actions, H = HID;
+  const Ws w = ws_layout(D, A, M, (char*)workspace);
+  RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_ppo_grad: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const Layout L = make_layout(D, H, A);
+  const int stride = mb_stride(D, A);
+
+  if (phases & RLKS_PHASE_FWD)
+    for (int net = 0; net < 2; ++net) {
+      FwdArgs f{};
+      f.P = net_ptrs_host(params, L, net);
+      f.x = mb; f.x_stride = stride; f.M = M; f.D = D; f.A_pi = A;
+      f.co = *co; f.dyn = dyn;
+      const NetWs& n = w.n[net];
+      f.dz2 = n.dz2; f.part_b2 = n.part_b2; f.part_w3 = n.part_w3; f.part_b3 = n.part_b3; f.part_stat = n.part_stat;
+      if (int rc = launch_fwd_head(f, net, A, true, s)) return rc;
+    }
+  for (int net = 0; net < 2; ++net) {
+    const NetWs& n = w.n[net];
+    if (phases & RLKS_PHASE_DW2) {
+      Dw2Args a{};
+      a.P = net_ptrs_host(params, L, net); a.x = mb; a.x_stride = stride; a.M = M;
+      a.rows_per_split = M / w.splits; a.dz2 = n.dz2; a.part = n.part_w2;
+      if (int rc = launch_dw2(a, D, w.splits, s)) return rc;
+    }
+    if (phases & RLKS_PHASE_DH1) {
+      Dh1Args a{};
+      a.P = net_ptrs_host(params, L, net); a.x = mb; a.x_stride = stride; a.M = M;
+      a.dz2 = n.dz2; a.part_w1 = n.part_w1; a.part_b1 = n.part_b1;
+      if (int rc = launch_dh1(a, D, s)) return rc;
+    }
+  }
+  if (!(phases & RLKS_PHASE_REDUCE)) return RLKS_OK;
+  Reducer R;
+  for (int net = 0; net < 2; ++net) {
+    const int An = net == 0 ? A : 1;
+    const int64_t* o = L.off + 6 * net;
+    const NetWs& n = w.n[net];
+    R.add(n.part_w1, grad + o[0], nullptr, (int64_t)H * D, w.tiles, H * D);
+    R.add(n.part_b1, grad + o[1], nullptr, H, w.tiles, H);
+    R.add(n.part_w2, grad + o[2], nullptr, (int64_t)H * H, w.splits, H * H);
+    R.add(n.part_b2, grad + o[3], nullptr, H, w.tiles, H);
+    R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, w.tiles, An * H);
+    R.add(n.part_b3, grad + o[5], nullptr, An, w.tiles, An);
+    if (stats) R.add(n.part_stat, nullptr, w.stat64 + 4 * net, 4, w.tiles, 4);
+  }
+  hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
+  RLKS_LAUNCHED();
+  if (stats) {
+    hipLaunchKernelGGL(k_stats_finish, dim3(1), dim3(64), 0, s, stats, w.stat64, w.stat64 + 4, M);
+    RLKS_LAUNCHED();
+  }
+  return RLKS_OK;
+}
+
+int rlks_ppo_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
+                  const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes,
+                  void* stream) {
+  return rlks_ppo_grad_phases(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, stream);
+}
+
+int rlks_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                   float eps, int step, void* stream) {
+  RLKS_REQUIRE(p && g && m && v && n >= 0 && step >= 1, RLKS_ERR_ARG, "rlks_adam_step: bad argument");
+  if (n == 0) return RLKS_OK;
+  const double bc1 = 1.0 - std::pow((double)beta1, step);
+  const double bc2 = 1.0 - std::pow((double)beta2, step);
+  hipLaunchKernelGGL(k_adam, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, 1.f - beta1,
+                     beta2, 1.f - beta2, (float)(lr / bc1), (float)std::sqrt(bc2), eps);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_kl_update(float* dyn, const double* kc, float target, void* stream) {
+  RLKS_REQUIRE(dyn && kc, RLKS_ERR_ARG, "rlks_kl_update: null argument");
+  hipLaunchKernelGGL(k_kl_update, dim3(1), dim3(64), 0, (hipStream_t)stream, dyn, kc, target);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, const rlks_rollout_bufs* b,
+                 int explore, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(env && params && b && b->T > 0 && b->N > 0, RLKS_ERR_ARG, "rlks_rollout: bad argument");
+  rlks_env_cfg cfg;
+  rlks_env_config(env, &cfg);
+  RLKS_REQUIRE(cfg.n_envs == b->N && 3 * cfg.n_clouds == d->obs_dim && cfg.n_clouds == d->n_actions,
+               RLKS_ERR_ARG, "rlks_rollout: env / policy / buffer shapes disagree");
+  const int N = b->N, D = d->obs_dim, A = d->n_actions;
+  for (int t = 0; t < b->T; ++t) {
+    if (int rc = rlks_policy_forward(d, params, b->obs + (size_t)t * N * D, N, b->logits + (size_t)t * N * A,
+                                     b->values + (size_t)t * N, stream))
+      return rc;
+    if (int rc = rlks_env_sample_step(env, b->logits + (size_t)t * N * A, explore, b->actions + (size_t)t * N,
+                                      b->logp + (size_t)t * N, b->obs + (size_t)(t + 1) * N * D,
+                                      b->rewards + (size_t)t * N, b->dones + (size_t)t * N, stream))
+      return rc;
+  }
+  return rlks_policy_forward(d, params, b->obs + (size_t)b->T * N * D, N, nullptr, b->values + (size_t)b->T * N,
+                             stream);
+}
+
+}  // extern "C"

@@ -179,7 +179,9 @@ def test_adam_matches_torch():
     ep, em, ev = oracle.adam(p, g, m, v, 7, 3e-4)
     close(mt.cpu().numpy(), em, 1e-6)
     close(vt.cpu().numpy(), ev, 1e-6)
-    np.testing.assert_allclose(pt.cpu().numpy(), ep, rtol=0, atol=3e-4 * 1e-4)
+    # parameters: the stored value may differ from torch's by the final rounding of p - step
+    # (<= 2 ulp of p) plus 1e-5 of the lr-sized update; m and v above agree to 1e-6
+    np.testing.assert_allclose(pt.cpu().numpy(), ep, rtol=2.5e-7, atol=1e-5 * 3e-4)
 
 
 def test_gather_is_a_permutation_per_epoch():
