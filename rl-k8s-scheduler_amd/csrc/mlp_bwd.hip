@@ -24,21 +24,23 @@ __global__ __launch_bounds__(256) void k_dw2(Dw2Args g) {
   float* sW1 = sb1 + GB;          // [GB][DD+1]
   float* sX = sW1 + GB * ds;      // [2][BK][DD+1] double-buffered X rows
 
-  const int tn = blockIdx.x >> 1, tk = blockIdx.x & 1;
+  const int tn = blockIdx.x >> 1, tk = blockIdx.x & 1, net = blockIdx.z;
   const int n0 = tn * GB, k0 = tk * GB;
+  const NetPtrs P = g.P[net];
+  const float* dz2 = g.dz2[net];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int h = l >> 5, li = l & 31;
   const int mbeg = blockIdx.y * g.rows_per_split, mend = mbeg + g.rows_per_split;
 
-  for (int e = tid; e < GB * DD; e += 256) sW1[(e / DD) * ds + (e % DD)] = g.P.w1[(size_t)k0 * DD + e];
-  for (int e = tid; e < GB; e += 256) sb1[e] = g.P.b1[k0 + e];
+  for (int e = tid; e < GB * DD; e += 256) sW1[(e / DD) * ds + (e % DD)] = P.w1[(size_t)k0 * DD + e];
+  for (int e = tid; e < GB; e += 256) sb1[e] = P.b1[k0 + e];
 
   float4 pa0, pa1, pa2, pa3;
   float px = 0.f;
 #define DW2_LOAD(mc)                                                                                \
   do {                                                                                              \
-    const float* src_ = g.dz2 + (size_t)((mc) + (tid >> 5)) * H + n0 + 4 * (tid & 31);              \
+    const float* src_ = dz2 + (size_t)((mc) + (tid >> 5)) * H + n0 + 4 * (tid & 31);                   \
     pa0 = *reinterpret_cast<const float4*>(src_);                                                   \
     pa1 = *reinterpret_cast<const float4*>(src_ + 8 * H);                                           \
     pa2 = *reinterpret_cast<const float4*>(src_ + 16 * H);                                          \
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(256) void k_dw2(Dw2Args g) {
     __syncthreads();
     buf ^= 1;
   }
-  float* out = g.part + (size_t)blockIdx.y * H * H;
+  float* out = g.part[net] + (size_t)blockIdx.y * H * H;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -127,24 +129,26 @@ __global__ __launch_bounds__(256) void k_dh1(Dh1Args g) {
   float* sRed = sA;                   // epilogue reuse: [2][GB][DD+1]
   static_assert(2 * GB * ds <= GB * (BK + 1) + BK * GB, "dW1 reduction must fit in the staging buffers");
 
-  const int tile = blockIdx.x, tk = blockIdx.y;
+  const int tile = blockIdx.x, tk = blockIdx.y, net = blockIdx.z;
   const int m0 = tile * GB, k0 = tk * GB;
+  const NetPtrs P = g.P[net];
+  const float* dz2 = g.dz2[net];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int h = l >> 5, li = l & 31;
 
   for (int e = tid; e < GB * DD; e += 256) {
     sX[(e / DD) * ds + (e % DD)] = g.x[(size_t)(m0 + e / DD) * g.x_stride + (e % DD)];
-    sW1[(e / DD) * ds + (e % DD)] = g.P.w1[(size_t)k0 * DD + e];
+    sW1[(e / DD) * ds + (e % DD)] = P.w1[(size_t)k0 * DD + e];
   }
-  for (int e = tid; e < GB; e += 256) sb1[e] = g.P.b1[k0 + e];
+  for (int e = tid; e < GB; e += 256) sb1[e] = P.b1[k0 + e];
 
   // per thread: dZ2 rows (tid >> 3) + 32 j, columns 4 (tid & 7); W2 rows (tid >> 5) + 8 j
   float4 pa0, pa1, pa2, pa3, pb0, pb1, pb2, pb3;
 #define DH1_LOAD(nc)                                                                                 \
   do {                                                                                               \
-    const float* sa_ = g.dz2 + (size_t)(m0 + (tid >> 3)) * H + (nc) + 4 * (tid & 7);                 \
-    const float* sb_ = g.P.w2 + (size_t)((nc) + (tid >> 5)) * H + k0 + 4 * (tid & 31);               \
+    const float* sa_ = dz2 + (size_t)(m0 + (tid >> 3)) * H + (nc) + 4 * (tid & 7);                   \
+    const float* sb_ = P.w2 + (size_t)((nc) + (tid >> 5)) * H + k0 + 4 * (tid & 31);                 \
     pa0 = *reinterpret_cast<const float4*>(sa_);                                                     \
     pa1 = *reinterpret_cast<const float4*>(sa_ + 32 * H);                                            \
     pa2 = *reinterpret_cast<const float4*>(sa_ + 64 * H);                                            \
@@ -246,9 +250,9 @@ __global__ __launch_bounds__(256) void k_dh1(Dh1Args g) {
     const int kk = e / ds, d = e - kk * ds;
     const float s = sRed[kk * ds + d] + sRed[(GB + kk) * ds + d];
     if (d == DD)
-      g.part_b1[(size_t)tile * H + k0 + kk] = s;
+      g.part_b1[net][(size_t)tile * H + k0 + kk] = s;
     else
-      g.part_w1[((size_t)tile * H + k0 + kk) * DD + d] = s;
+      g.part_w1[net][((size_t)tile * H + k0 + kk) * DD + d] = s;
   }
 }
 
@@ -258,11 +262,12 @@ __global__ __launch_bounds__(256) void k_dh1(Dh1Args g) {
 
 int launch_dw2(const Dw2Args& a, int D, int splits, hipStream_t s) {
   const size_t lds = ((size_t)2 * BK * GB + GB + (size_t)GB * (D + 1) + (size_t)2 * BK * (D + 1)) * sizeof(float);
-  const dim3 grid((HID / GB) * (HID / GB), splits);
+  const dim3 grid((HID / GB) * (HID / GB), splits, 2);
   switch (D) {
     case 6: hipLaunchKernelGGL(k_dw2<6>, grid, dim3(256), lds, s, a); break;
+    case 12: hipLaunchKernelGGL(k_dw2<12>, grid, dim3(256), lds, s, a); break;
     case 24: hipLaunchKernelGGL(k_dw2<24>, grid, dim3(256), lds, s, a); break;
-    default: return fail(RLKS_ERR_UNSUPPORTED, "PPO gradient kernels are built for obs_dim 6 or 24");
+    default: return fail(RLKS_ERR_UNSUPPORTED, "PPO gradient kernels are built for obs_dim 6, 12 or 24");
   }
   RLKS_LAUNCHED();
   return RLKS_OK;
@@ -270,11 +275,12 @@ int launch_dw2(const Dw2Args& a, int D, int splits, hipStream_t s) {
 
 int launch_dh1(const Dh1Args& a, int D, hipStream_t s) {
   const size_t lds = ((size_t)GB * (BK + 1) + BK * GB + GB + (size_t)2 * GB * (D + 1)) * sizeof(float);
-  const dim3 grid(a.M / GB, HID / GB);
+  const dim3 grid(a.M / GB, HID / GB, 2);
   switch (D) {
     case 6: hipLaunchKernelGGL(k_dh1<6>, grid, dim3(256), lds, s, a); break;
+    case 12: hipLaunchKernelGGL(k_dh1<12>, grid, dim3(256), lds, s, a); break;
     case 24: hipLaunchKernelGGL(k_dh1<24>, grid, dim3(256), lds, s, a); break;
-    default: return fail(RLKS_ERR_UNSUPPORTED, "PPO gradient kernels are built for obs_dim 6 or 24");
+    default: return fail(RLKS_ERR_UNSUPPORTED, "PPO gradient kernels are built for obs_dim 6, 12 or 24");
   }
   RLKS_LAUNCHED();
   return RLKS_OK;

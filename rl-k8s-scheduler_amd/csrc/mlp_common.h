@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "env_device.h"
 #include "rlks_internal.h"
 
 namespace rlks {
@@ -91,30 +92,42 @@ struct FwdArgs {
   float* part_w3;     // [tiles][A_][HID]
   float* part_b3;     // [tiles][A_]
   float* part_stat;   // [tiles][4]
+  // rollout mode: sample an action from the logits and step the env lane (row m = lane m)
+  EnvView env;
+  const double* tab_cost;  // [T][C]
+  const double* tab_lat;   // [T][C]
+  int explore;
+  float* obs_next;         // [M][D]
+  float* logp;             // [M]
+  int32_t* actions;        // [M]
+  float* rewards;          // [M]
+  uint8_t* dones;          // [M]
 };
 
 // ----------------------------------------------------------------------------- F2 / F3 arguments
+// one launch covers both nets: blockIdx.z selects pi (0) or vf (1)
 struct Dw2Args {
-  NetPtrs P;
+  NetPtrs P[2];
   const float* x;
   int x_stride;
   int M, rows_per_split;
-  const float* dz2;   // this net's [M][HID]
-  float* part;        // [S][HID][HID]
+  const float* dz2[2];  // per net [M][HID]
+  float* part[2];       // per net [S][HID][HID]
 };
 
 struct Dh1Args {
-  NetPtrs P;
+  NetPtrs P[2];
   const float* x;
   int x_stride;
   int M;
-  const float* dz2;   // this net's [M][HID]
-  float* part_w1;     // [tiles][HID][D]
-  float* part_b1;     // [tiles][HID]
+  const float* dz2[2];  // per net [M][HID]
+  float* part_w1[2];    // per net [tiles][HID][D]
+  float* part_b1[2];    // per net [tiles][HID]
 };
 
 // host launchers (mlp_fwd.hip / mlp_bwd.hip)
-int launch_fwd_head(const FwdArgs& a, int net, int A, bool train, hipStream_t s);
+enum { FWD_ONLY = 0, FWD_TRAIN = 1, FWD_ROLLOUT = 2 };
+int launch_fwd_head(const FwdArgs& a, int net, int A, int mode, hipStream_t s);
 int launch_dw2(const Dw2Args& a, int D, int splits, hipStream_t s);
 int launch_dh1(const Dh1Args& a, int D, hipStream_t s);
 

@@ -40,27 +40,33 @@ __device__ __forceinline__ float half_wave_reduce16(const float (&v)[16], int l)
   return v1 + __shfl_xor(v1, 1, 64);
 }
 
-template <int A_, int NET, int WM, int WN, bool TRAIN>
+template <int A_, int NET, int WM, int WN, int MODE, int DD>
 __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
+  constexpr bool TRAIN = MODE == FWD_TRAIN;
+  static_assert(MODE != FWD_ROLLOUT || NET == 0, "rollout mode drives the policy net");
   constexpr int H = HID;
   constexpr int NT = H / (32 * WN);     // 32-column accumulator tiles per wave
   constexpr int BMr = 32 * WM;          // rows per workgroup
   constexpr int NTHR = 64 * WM * WN;
   constexpr int F4 = H * BK / 4 / NTHR; // float4 of the W2 chunk per thread
   static_assert(NT * 32 * WN == H && F4 * 4 * NTHR == H * BK, "tile split");
-  static_assert(WM * H * (1 + A_) <= H * (BK + 1) + BK * BMr, "epilogue reduction must fit in the staging buffers");
+  static_assert(WM * H * (1 + A_) <= 2 * H * (BK + 1), "epilogue reduction must fit in the staging buffers");
   static_assert(BMr <= 128, "loss rows are handled by the first two waves");
 
-  const int D = g.D, ds = g.D + 1;
+  constexpr int D = DD, ds = DD + 1;
+  constexpr int SB = H * (BK + 1), SA = BK * BMr;
+  constexpr int HPT = SA / NTHR;         // H1 elements per thread per chunk
+  static_assert(HPT * NTHR == SA && (BK / 2) % HPT == 0, "H1 chunk split over the MFMA steps");
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* sB = lds;                       // [H][BK+1]   W2 chunk [n][k]
-  float* sA = sB + H * (BK + 1);         // [BK][BMr]   H1 chunk [k][m]
-  float* sHead = sA + BK * BMr;          // [WN][BMr][A_]
+  float* sB = lds;                       // [2][H][BK+1]  W2 chunks [n][k] (double buffer)
+  float* sA = sB + 2 * SB;               // [2][BK][BMr]  H1 chunks [k][m] (double buffer)
+  float* sHead = sA + 2 * SA;            // [WN][BMr][A_]
   float* sDl = sHead + WN * BMr * A_;    // [BMr][A_]
   float* sStat = sDl + BMr * A_;         // [2][A_ + 4]
   float* sb1 = sStat + 2 * (A_ + 4);     // [H]
   float* sX = sb1 + H;                   // [BMr][D+1]
   float* sW1 = sX + BMr * ds;            // [H][D+1]
+  double* sTab = reinterpret_cast<double*>(sW1 + ((H * ds + 1) & ~1));  // rollout: [2][T][C] tables
 
   const NetPtrs& P = g.P;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -74,51 +80,83 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
   }
   for (int e = tid; e < H * D; e += NTHR) sW1[(e / D) * ds + (e % D)] = P.w1[e];
   for (int e = tid; e < H; e += NTHR) sb1[e] = P.b1[e];
+  if (MODE == FWD_ROLLOUT)
+    for (int e = tid; e < g.env.T * g.env.C; e += NTHR) {
+      sTab[e] = g.tab_cost[e];
+      sTab[g.env.T * g.env.C + e] = g.tab_lat[e];
+    }
 
   float4 pre[F4];
-  auto load_w2 = [&](int kc) {
-#pragma unroll
-    for (int j = 0; j < F4; ++j) {
-      const int e = tid + j * NTHR, n = e >> 3, k4 = e & 7;
-      pre[j] = *reinterpret_cast<const float4*>(P.w2 + (size_t)n * H + kc + 4 * k4);
-    }
-  };
-  load_w2(0);
+#define F1_LOAD_W2(kc)                                                                     \
+  _Pragma("unroll") for (int j = 0; j < F4; ++j) {                                         \
+    const int e_ = tid + j * NTHR;                                                         \
+    pre[j] = *reinterpret_cast<const float4*>(P.w2 + (size_t)(e_ >> 3) * H + (kc) + 4 * (e_ & 7)); \
+  }
+#define F1_STORE_W2(buf)                                                                   \
+  _Pragma("unroll") for (int j = 0; j < F4; ++j) {                                         \
+    const int e_ = tid + j * NTHR;                                                         \
+    float* dst_ = sB + (buf) * SB + (e_ >> 3) * (BK + 1) + 4 * (e_ & 7);                   \
+    dst_[0] = pre[j].x; dst_[1] = pre[j].y; dst_[2] = pre[j].z; dst_[3] = pre[j].w;        \
+  }
+  // one H1 element of chunk kc: sA[buf][k][m] = tanh(b1[k] + X[m] . W1[k])
+#define F1_H1(kc, buf, idx)                                                                \
+  {                                                                                        \
+    const int e_ = tid + (idx) * NTHR, kk_ = e_ / BMr, m_ = e_ - kk_ * BMr;                 \
+    const float* wr_ = sW1 + ((kc) + kk_) * ds;                                            \
+    const float* xr_ = sX + m_ * ds;                                                       \
+    float z_ = sb1[(kc) + kk_];                                                            \
+    _Pragma("unroll") for (int d_ = 0; d_ < D; ++d_) z_ = fmaf(xr_[d_], wr_[d_], z_);    \
+    sA[(buf) * SA + kk_ * BMr + m_] = fast_tanh(z_);                                       \
+  }
 
+  F1_LOAD_W2(0);
   f32x16 acc[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[nt][r] = 0.f;
-
   __syncthreads();  // sX / sW1 / sb1 staged
-  for (int kc = 0; kc < H; kc += BK) {
+  F1_STORE_W2(0);
 #pragma unroll
-    for (int j = 0; j < F4; ++j) {
-      const int e = tid + j * NTHR, n = e >> 3, k4 = e & 7;
-      float* dst = sB + n * (BK + 1) + 4 * k4;
-      dst[0] = pre[j].x; dst[1] = pre[j].y; dst[2] = pre[j].z; dst[3] = pre[j].w;
-    }
-    // H1 chunk: sA[k][m] = tanh(b1[k] + X[m] . W1[k])
-    for (int e = tid; e < BK * BMr; e += NTHR) {
-      const int kk = e / BMr, m = e - kk * BMr;
-      const float* wr = sW1 + (kc + kk) * ds;
-      const float* xr = sX + m * ds;
-      float z = sb1[kc + kk];
-      for (int d = 0; d < D; ++d) z = fmaf(xr[d], wr[d], z);
-      sA[kk * BMr + m] = fast_tanh(z);
-    }
-    __syncthreads();
-    if (kc + BK < H) load_w2(kc + BK);  // next chunk in flight during the MFMAs
-#pragma unroll 4
+  for (int i = 0; i < HPT; ++i) F1_H1(0, 0, i);
+  F1_LOAD_W2(BK);
+  __syncthreads();
+
+  // chunk c: MFMAs on buffer c&1 while this thread computes its H1 share of chunk c+1 into the
+  // other buffer between them and parks W2 chunk c+1 / issues the loads of chunk c+2: one
+  // barrier per chunk, the tanh work overlapping the matrix pipe.
+  constexpr int NC = H / BK, SPH = (BK / 2) / HPT;  // chunks; MFMA steps per H1 element
+  for (int c = 0; c < NC - 1; ++c) {
+    const int cur = c & 1, nxt = cur ^ 1;
+    F1_STORE_W2(nxt);
+    if (c + 2 < NC) { F1_LOAD_W2((c + 2) * BK); }
+    const float* a_src = sA + cur * SA + wm * 32 + li;
+    const float* b_src = sB + cur * SB + (wn * NT * 32 + li) * (BK + 1);
+#pragma unroll
     for (int s = 0; s < BK / 2; ++s) {
       const int k = 2 * s + h;
-      const float a = sA[k * BMr + wm * 32 + li];
+      const float a = a_src[k * BMr];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma32(a, sB[((wn * NT + nt) * 32 + li) * (BK + 1) + k], acc[nt]);
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma32(a, b_src[nt * 32 * (BK + 1) + k], acc[nt]);
+      if (s % SPH == 0) F1_H1((c + 1) * BK, nxt, s / SPH);
     }
     __syncthreads();
   }
+  {
+    const float* a_src = sA + ((NC - 1) & 1) * SA + wm * 32 + li;
+    const float* b_src = sB + ((NC - 1) & 1) * SB + (wn * NT * 32 + li) * (BK + 1);
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      const int k = 2 * s + h;
+      const float a = a_src[k * BMr];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma32(a, b_src[nt * 32 * (BK + 1) + k], acc[nt]);
+    }
+    __syncthreads();
+  }
+#undef F1_LOAD_W2
+#undef F1_STORE_W2
+#undef F1_H1
 
   // ---- H2 = tanh(Z2 + b2); head partial dot products over this wave's columns
   float w3r[NT][A_];
@@ -158,10 +196,49 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
       for (int j = 0; j < WN; ++j) s += sHead[(j * BMr + tid) * A_ + a];
       out[a] = s;
     }
-    if (!TRAIN) {
+    if (MODE == FWD_ONLY) {
       if (m < g.M)
 #pragma unroll
         for (int a = 0; a < A_; ++a) g.out[(size_t)m * A_ + a] = out[a];
+    } else if (MODE == FWD_ROLLOUT) {
+      if (m < g.M) {
+        // TorchCategorical: sample (Philox, counter = lane/episode/step) or argmax (explore=False)
+        float mx = out[0];
+        int amax = 0;
+#pragma unroll
+        for (int a = 1; a < A_; ++a)
+          if (out[a] > mx) { mx = out[a]; amax = a; }
+        float e[A_], se = 0.f;
+#pragma unroll
+        for (int a = 0; a < A_; ++a) { e[a] = expf(out[a] - mx); se += e[a]; }
+        int act = amax;
+        const EnvView& v = g.env;
+        if (g.explore) {
+          const u32x4 x = philox4x32_10(u32x4{(uint32_t)(v.env_offset + m), (uint32_t)v.episode[m],
+                                              (uint32_t)v.step[m], (uint32_t)RLKS_PURPOSE_ACTION << 16},
+                                        v.k0, v.k1);
+          const float u = (float)u53(x.x, x.y) * se;
+          float c = 0.f;
+          act = A_ - 1;
+          bool found = false;
+#pragma unroll
+          for (int a = 0; a < A_; ++a) {
+            c += e[a];
+            if (!found && u < c) { act = a; found = true; }
+          }
+        }
+        float la = out[0];
+#pragma unroll
+        for (int a = 0; a < A_; ++a) {
+          g.out[(size_t)m * A_ + a] = out[a];
+          la = (a == act) ? out[a] : la;
+        }
+        g.actions[m] = act;
+        g.logp[m] = la - mx - logf(se);
+        const StepOut r = step_lane(v, sTab, m, act, g.obs_next + (size_t)m * D, nullptr);
+        g.rewards[m] = (float)r.reward;
+        g.dones[m] = (uint8_t)r.done;
+      }
     } else {
       float dl[A_];
 #pragma unroll
@@ -241,8 +318,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
     float dlr[A_];
 #pragma unroll
     for (int a = 0; a < A_; ++a) dlr[a] = sDl[row * A_ + a];
-    float* dst = g.dz2 + (size_t)(row0 + row) * H + wn * NT * 32 + li;
-    const bool valid = row0 + row < g.M;
+    float* dst = g.dz2 + (size_t)(row0 + row) * H + wn * NT * 32 + li;  // M % BMr == 0 in training
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const float h2 = acc[nt][r];
@@ -254,7 +330,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
       }
       const float dz = dh * (1.f - h2 * h2);
       csum[nt] += dz;
-      if (valid) dst[nt * 32] = dz;
+      dst[nt * 32] = dz;
     }
   }
 #pragma unroll
@@ -263,7 +339,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
 #pragma unroll
     for (int a = 0; a < A_; ++a) cw3[nt][a] += __shfl_xor(cw3[nt][a], 32, 64);
   }
-  float* sRed = sB;  // [WM][H] db2, then [WM][A_][H] dW3 (over the dead W2 / H1 chunk buffers)
+  float* sRed = sB;  // [WM][H] db2, then [WM][A_][H] dW3 (over the dead W2 chunk buffers)
   if (l < 32) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -308,36 +384,44 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
 }
 
 template <int WM, int WN>
-static size_t fwd_lds_bytes(int A_, int D) {
+static size_t fwd_lds_bytes(int A_, int D, int table_doubles) {
   constexpr int BMr = 32 * WM;
-  return ((size_t)HID * (BK + 1) + BK * BMr + WN * BMr * A_ + BMr * A_ + 2 * (A_ + 4) + HID +
-          (size_t)(BMr + HID) * (D + 1)) * sizeof(float);
+  const size_t f = (size_t)2 * HID * (BK + 1) + 2 * BK * BMr + WN * BMr * A_ + BMr * A_ + 2 * (A_ + 4) + HID +
+                   (size_t)BMr * (D + 1) + (((size_t)HID * (D + 1) + 1) & ~(size_t)1);
+  return f * sizeof(float) + (size_t)table_doubles * sizeof(double);
 }
 
-template <int A_, int NET, int WM, int WN, bool TRAIN>
+template <int A_, int NET, int WM, int WN, int MODE, int DD>
 static int launch_cfg(const FwdArgs& a, hipStream_t s) {
   constexpr int BMr = 32 * WM;
-  const size_t lds = fwd_lds_bytes<WM, WN>(A_, a.D);
-  hipLaunchKernelGGL((k_fwd_head<A_, NET, WM, WN, TRAIN>), dim3(cdiv(a.M, BMr)), dim3(64 * WM * WN), lds, s, a);
+  const size_t lds = fwd_lds_bytes<WM, WN>(A_, DD, MODE == FWD_ROLLOUT ? 2 * a.env.T * a.env.C : 0);
+  hipLaunchKernelGGL((k_fwd_head<A_, NET, WM, WN, MODE, DD>), dim3(cdiv(a.M, BMr)), dim3(64 * WM * WN), lds, s, a);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }
 
-template <int A_, int NET>
-static int launch_net(const FwdArgs& a, bool train, hipStream_t s) {
-  if (train) return launch_cfg<A_, NET, 4, 2, true>(a, s);
-  // forward only: small batches (rollouts of a few thousand lanes) use 32-row tiles with the
-  // 4 waves split over columns so that more CUs get work; large batches use 128-row tiles
-  if (a.M <= 32 * 1024) return launch_cfg<A_, NET, 1, 4, false>(a, s);
-  return launch_cfg<A_, NET, 4, 2, false>(a, s);
+template <int A_, int NET, int DD>
+static int launch_net(const FwdArgs& a, int mode, hipStream_t s) {
+  if (mode == FWD_TRAIN) return launch_cfg<A_, NET, 4, 2, FWD_TRAIN, DD>(a, s);
+  // small batches (rollouts of a few thousand lanes) use 32-row tiles with the 4 waves split
+  // over columns so that more CUs get work; large batches use 128-row tiles
+  const bool small = a.M <= 32 * 1024;
+  if (mode == FWD_ROLLOUT) {
+    if constexpr (NET == 0) {
+      return small ? launch_cfg<A_, 0, 1, 4, FWD_ROLLOUT, DD>(a, s) : launch_cfg<A_, 0, 4, 2, FWD_ROLLOUT, DD>(a, s);
+    }
+    return fail(RLKS_ERR_ARG, "rollout mode drives the policy net");
+  }
+  return small ? launch_cfg<A_, NET, 1, 4, FWD_ONLY, DD>(a, s) : launch_cfg<A_, NET, 4, 2, FWD_ONLY, DD>(a, s);
 }
 
-int launch_fwd_head(const FwdArgs& a, int net, int A, bool train, hipStream_t s) {
-  if (net == 1) return launch_net<1, 1>(a, train, s);
+// obs_dim = 3 x clusters (cost, latency, utilisation per cluster): C = 2, 4, 8 -> D = 6, 12, 24
+int launch_fwd_head(const FwdArgs& a, int net, int A, int mode, hipStream_t s) {
+  if (a.D != 3 * A) return fail(RLKS_ERR_UNSUPPORTED, "fused MLP kernels expect obs_dim = 3 x n_actions");
   switch (A) {
-    case 2: return launch_net<2, 0>(a, train, s);
-    case 4: return launch_net<4, 0>(a, train, s);
-    case 8: return launch_net<8, 0>(a, train, s);
+    case 2: return net ? launch_net<1, 1, 6>(a, mode, s) : launch_net<2, 0, 6>(a, mode, s);
+    case 4: return net ? launch_net<1, 1, 12>(a, mode, s) : launch_net<4, 0, 12>(a, mode, s);
+    case 8: return net ? launch_net<1, 1, 24>(a, mode, s) : launch_net<8, 0, 24>(a, mode, s);
     default: return fail(RLKS_ERR_UNSUPPORTED, "fused policy head is built for 2, 4 or 8 actions");
   }
 }

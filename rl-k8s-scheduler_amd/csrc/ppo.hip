@@ -187,9 +187,9 @@ struct Ws {
 };
 
 static int pick_splits(int M) {
-  // F2 grid = 4 tiles x 2 nets x S: about two workgroups per CU, >= 4 chunks of rows per split
+  // F2 grid = 4 tiles x 2 nets x S: about four workgroups per CU, >= 4 chunks of rows per split
   int s = 1;
-  while (s * 2 * 8 <= 512 && (M / (s * 2)) % BK == 0 && M / (s * 2) >= 4 * BK) s *= 2;
+  while (s * 2 * 8 <= 1024 && (M / (s * 2)) % BK == 0 && M / (s * 2) >= 4 * BK) s *= 2;
   return s;
 }
 
@@ -258,7 +258,7 @@ int rlks_policy_forward(const rlks_mlp_desc* d, const float* params, const float
     FwdArgs a{};
     a.P = net_ptrs_host(params, L, net);
     a.x = obs; a.x_stride = d->obs_dim; a.M = n; a.D = d->obs_dim; a.A_pi = d->n_actions; a.out = out;
-    if (int rc = launch_fwd_head(a, net, d->n_actions, false, s)) return rc;
+    if (int rc = launch_fwd_head(a, net, d->n_actions, FWD_ONLY, s)) return rc;
   }
   return RLKS_OK;
 }
@@ -315,22 +315,28 @@ int rlks_ppo_grad_phases(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, cons
       f.co = *co; f.dyn = dyn;
       const NetWs& n = w.n[net];
       f.dz2 = n.dz2; f.part_b2 = n.part_b2; f.part_w3 = n.part_w3; f.part_b3 = n.part_b3; f.part_stat = n.part_stat;
-      if (int rc = launch_fwd_head(f, net, A, true, s)) return rc;
+      if (int rc = launch_fwd_head(f, net, A, FWD_TRAIN, s)) return rc;
     }
-  for (int net = 0; net < 2; ++net) {
-    const NetWs& n = w.n[net];
-    if (phases & RLKS_PHASE_DW2) {
-      Dw2Args a{};
-      a.P = net_ptrs_host(params, L, net); a.x = mb; a.x_stride = stride; a.M = M;
-      a.rows_per_split = M / w.splits; a.dz2 = n.dz2; a.part = n.part_w2;
-      if (int rc = launch_dw2(a, D, w.splits, s)) return rc;
+  if (phases & RLKS_PHASE_DW2) {
+    Dw2Args a{};
+    a.x = mb; a.x_stride = stride; a.M = M; a.rows_per_split = M / w.splits;
+    for (int net = 0; net < 2; ++net) {
+      a.P[net] = net_ptrs_host(params, L, net);
+      a.dz2[net] = w.n[net].dz2;
+      a.part[net] = w.n[net].part_w2;
     }
-    if (phases & RLKS_PHASE_DH1) {
-      Dh1Args a{};
-      a.P = net_ptrs_host(params, L, net); a.x = mb; a.x_stride = stride; a.M = M;
-      a.dz2 = n.dz2; a.part_w1 = n.part_w1; a.part_b1 = n.part_b1;
-      if (int rc = launch_dh1(a, D, s)) return rc;
+    if (int rc = launch_dw2(a, D, w.splits, s)) return rc;
+  }
+  if (phases & RLKS_PHASE_DH1) {
+    Dh1Args a{};
+    a.x = mb; a.x_stride = stride; a.M = M;
+    for (int net = 0; net < 2; ++net) {
+      a.P[net] = net_ptrs_host(params, L, net);
+      a.dz2[net] = w.n[net].dz2;
+      a.part_w1[net] = w.n[net].part_w1;
+      a.part_b1[net] = w.n[net].part_b1;
     }
+    if (int rc = launch_dh1(a, D, s)) return rc;
   }
   if (!(phases & RLKS_PHASE_REDUCE)) return RLKS_OK;
   Reducer R;
@@ -389,17 +395,28 @@ int rlks_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, con
   RLKS_REQUIRE(cfg.n_envs == b->N && 3 * cfg.n_clouds == d->obs_dim && cfg.n_clouds == d->n_actions,
                RLKS_ERR_ARG, "rlks_rollout: env / policy / buffer shapes disagree");
   const int N = b->N, D = d->obs_dim, A = d->n_actions;
+  hipStream_t s = (hipStream_t)stream;
+  const Layout L = make_layout(D, d->hidden, A);
+  // per step: policy forward fused with sampling and the env step (one launch, pi net only)
+  FwdArgs f{};
+  f.P = net_ptrs_host(params, L, 0);
+  f.x_stride = D; f.M = N; f.D = D; f.A_pi = A;
+  f.env = view(env); f.tab_cost = env->d_cost; f.tab_lat = env->d_lat; f.explore = explore;
   for (int t = 0; t < b->T; ++t) {
-    if (int rc = rlks_policy_forward(d, params, b->obs + (size_t)t * N * D, N, b->logits + (size_t)t * N * A,
-                                     b->values + (size_t)t * N, stream))
-      return rc;
-    if (int rc = rlks_env_sample_step(env, b->logits + (size_t)t * N * A, explore, b->actions + (size_t)t * N,
-                                      b->logp + (size_t)t * N, b->obs + (size_t)(t + 1) * N * D,
-                                      b->rewards + (size_t)t * N, b->dones + (size_t)t * N, stream))
-      return rc;
+    f.x = b->obs + (size_t)t * N * D;
+    f.out = b->logits + (size_t)t * N * A;
+    f.obs_next = b->obs + (size_t)(t + 1) * N * D;
+    f.logp = b->logp + (size_t)t * N;
+    f.actions = b->actions + (size_t)t * N;
+    f.rewards = b->rewards + (size_t)t * N;
+    f.dones = b->dones + (size_t)t * N;
+    if (int rc = launch_fwd_head(f, 0, A, FWD_ROLLOUT, s)) return rc;
   }
-  return rlks_policy_forward(d, params, b->obs + (size_t)b->T * N * D, N, nullptr, b->values + (size_t)b->T * N,
-                             stream);
+  // values of every visited observation (incl. the bootstrap obs[T]) in one batched pass
+  FwdArgs v{};
+  v.P = net_ptrs_host(params, L, 1);
+  v.x = b->obs; v.x_stride = D; v.M = (b->T + 1) * N; v.D = D; v.A_pi = A; v.out = b->values;
+  return launch_fwd_head(v, 1, A, FWD_ONLY, s);
 }
 
 }  // extern "C"
