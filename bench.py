@@ -108,6 +108,22 @@ def kernel_timing(algo, torch, reps=20):
     # T fused (pi forward + sample + env step) launches + one batched value pass over (T+1) N rows
     flops = (T * N + (T + 1) * N) * 269824 / 2
     out["rollout"] = {"ms": ms, "env_steps_per_s": T * N / (ms * 1e-3), "tflops": flops / (ms * 1e-3) / 1e12}
+    # the standalone env step kernel at a size where HBM, not launch latency, bounds it
+    from rlks import VecK8sMultiCloudEnv
+
+    big = 1 << 24
+    venv = VecK8sMultiCloudEnv(big, table=algo.table, seed=1, device=algo.device)
+    venv.reset()
+    acts = torch.randint(0, 2, (big,), dtype=torch.int32, device=algo.device)
+    ms = timed(lambda: venv.step(acts), n=10)
+    alg = ENV_BYTES_PER_STEP * big / (ms * 1e-3) / 1e9
+    # bytes the kernel actually moves per lane: action 4, step 4+4, episode 4, ep_ret 8+8,
+    # obs 24, reward f64 8, terminated 1, truncated 1, step_out 4
+    moved = 70 * big / (ms * 1e-3) / 1e9
+    out["k_env_step_16M"] = {"ms": ms, "lanes": big, "GBps_algorithmic": alg, "frac_hbm": alg / HBM_PEAK_GBS,
+                             "GBps_moved": moved, "env_steps_per_s": big / (ms * 1e-3)}
+    venv.close()
+    del venv, acts
     return out
 
 

@@ -32,6 +32,7 @@ from pathlib import Path
 import numpy as np
 
 from . import _lib
+from . import distributed as ddp
 from .env import DeviceEnv, make_cfg
 from .policy import PolicyParams
 from .tables import load_table
@@ -162,12 +163,6 @@ class PPOConfig:
         return int(h[0])
 
 
-def _dist():
-    import torch.distributed as dist
-
-    return dist if dist.is_available() and dist.is_initialized() else None
-
-
 class PPO:
     """One instance per GPU (rank).  train() runs one PPO iteration over all local lanes."""
 
@@ -178,9 +173,7 @@ class PPO:
         if env is not None:
             cfg.env = env
         self.torch = torch
-        dist = _dist()
-        self.rank = dist.get_rank() if dist else 0
-        self.world = dist.get_world_size() if dist else 1
+        self.rank, self.world = ddp.rank_world()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -203,7 +196,7 @@ class PPO:
         self.seed = seed
         with torch.cuda.device(self.device):
             self.env = DeviceEnv(make_cfg(self.N, table, noise=cfg.noise, seed=seed, autoreset=True,
-                                          env_offset=self.rank * self.N), table, self.device)
+                                          env_offset=ddp.lane_range(self.N, self.rank)[0]), table, self.device)
             self.params = PolicyParams(self.D, self.H, self.A, device=self.device, seed=seed)
             P = self.params.padded
             f32 = dict(dtype=torch.float32, device=self.device)
@@ -213,7 +206,7 @@ class PPO:
             self.adam_step = 0
             self.dyn = torch.zeros(_lib.RLKS_DYN_SIZE, **f32)
             self.dyn[_lib.RLKS_DYN_KL_COEFF] = float(cfg.kl_coeff)
-            self.dyn[_lib.RLKS_DYN_INV_COUNT] = 1.0 / (self.mb * self.world)
+            self.dyn[_lib.RLKS_DYN_INV_COUNT] = ddp.loss_scale(self.mb, self.world)
             T, N, D, A = self.T, self.N, self.D, self.A
             self.buf = {
                 "obs": torch.zeros(T + 1, N, D, **f32), "logits": torch.zeros(T, N, A, **f32),
@@ -250,9 +243,7 @@ class PPO:
         return self.torch.cuda.current_stream(self.device).cuda_stream
 
     def _allreduce(self, t):
-        dist = _dist()
-        if dist is not None and self.world > 1:
-            dist.all_reduce(t)
+        ddp.allreduce_sum_(t)
 
     def rollout(self, explore=True):
         s = self.stream
