@@ -34,8 +34,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 dense peak (MI355X_MICRO
 # algorithmic work per row of each SGD-step kernel (D = 6, H = 256, A = 2, both nets)
 D_, H_, A_ = 6, 256, 2
 FLOPS_PER_ROW = {
-    # forward 2(DH + H^2 + HA) per net + head backward (dlogits W3 and dW3): 2*2*H*(A+1)
-    "k_fwd_head": 2 * (D_ * H_ + H_ * H_ + H_ * A_) + 2 * (D_ * H_ + H_ * H_ + H_) + 4 * H_ * (A_ + 1),
+    # per net: forward 2(DH + H^2 + H*A_net) + head backward (dout W3 and dW3) 4*H*A_net
+    "k_fwd_head_pi": 2 * (D_ * H_ + H_ * H_ + H_ * A_) + 4 * H_ * A_,
+    "k_fwd_head_vf": 2 * (D_ * H_ + H_ * H_ + H_) + 4 * H_,
     "k_dw2": 2 * 2 * H_ * H_,                       # dW2 = dZ2^T H1, both nets
     "k_dh1": 2 * 2 * H_ * H_ + 2 * 2 * D_ * H_,     # dH1 = dZ2 W2 and dW1 = dZ1^T X, both nets
 }
@@ -83,8 +84,9 @@ def kernel_timing(algo, torch, reps=20):
 
     _lib.call("rlks_ppo_gather", desc, C.byref(algo.bufs), 1, 0, 0, algo.mb, algo.dyn.data_ptr(),
               algo.mbuf.data_ptr(), s.cuda_stream)
-    for name, mask in (("k_fwd_head", _lib.RLKS_PHASE_FWD), ("k_dw2", _lib.RLKS_PHASE_DW2),
-                       ("k_dh1", _lib.RLKS_PHASE_DH1), ("k_reduce", _lib.RLKS_PHASE_REDUCE)):
+    for name, mask in (("k_fwd_head_pi", _lib.RLKS_PHASE_FWD_PI), ("k_fwd_head_vf", _lib.RLKS_PHASE_FWD_VF),
+                       ("k_dw2", _lib.RLKS_PHASE_DW2), ("k_dh1", _lib.RLKS_PHASE_DH1),
+                       ("k_reduce", _lib.RLKS_PHASE_REDUCE)):
         ms = timed(phase(mask))
         rec = {"ms": ms}
         if name in FLOPS_PER_ROW:
@@ -195,14 +197,17 @@ def main():
     if rank == 0:
         roofline = None
         if kernels:
-            dom = max(("k_fwd_head", "k_dw2", "k_dh1"), key=lambda k: kernels[k]["ms"])
+            # the dominant kernel as rocprofv3 --stats ranks them: largest share of GPU time (each
+            # runs once per SGD step, so: the longest launch)
+            dom = max(("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1"), key=lambda k: kernels[k]["ms"])
             k = kernels[dom]
             roofline = {"bound": "mfma", "kernel": dom, "achieved": k["tflops"], "peak": FP32_MFMA_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": k["tflops"] / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
                         "flop_per_launch": FLOPS_PER_ROW[dom] * algo.mb, "avg_launch_ms": k["ms"]}
             pmc = pmc_traffic()
-            if pmc and pmc.get("kernel") == dom:
-                roofline["traffic"] = pmc.get("hbm_bytes_per_launch")
+            if pmc and dom in pmc:
+                roofline["traffic"] = pmc[dom]["hbm_bytes_per_launch"]
+                roofline["traffic_source"] = pmc["source"]
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             sys.path.insert(0, str(ROOT / "oracle"))

@@ -307,8 +307,8 @@ int rlks_ppo_grad_phases(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, cons
   const Layout L = make_layout(D, H, A);
   const int stride = mb_stride(D, A);
 
-  if (phases & RLKS_PHASE_FWD)
-    for (int net = 0; net < 2; ++net) {
+  for (int net = 0; net < 2; ++net)
+    if ((phases & RLKS_PHASE_FWD) || (phases & (net ? RLKS_PHASE_FWD_VF : RLKS_PHASE_FWD_PI))) {
       FwdArgs f{};
       f.P = net_ptrs_host(params, L, net);
       f.x = mb; f.x_stride = stride; f.M = M; f.D = D; f.A_pi = A;

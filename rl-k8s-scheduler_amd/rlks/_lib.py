@@ -21,6 +21,7 @@ RLKS_DYN_SIZE = 8
 RLKS_DYN_ADV_MEAN, RLKS_DYN_ADV_INVSTD, RLKS_DYN_KL_COEFF, RLKS_DYN_INV_COUNT = 0, 1, 2, 3
 RLKS_STAT_SIZE = 8
 RLKS_PHASE_FWD, RLKS_PHASE_DW2, RLKS_PHASE_DH1, RLKS_PHASE_REDUCE, RLKS_PHASE_ALL = 1, 2, 4, 8, 15
+RLKS_PHASE_FWD_PI, RLKS_PHASE_FWD_VF = 16, 32
 RLKS_STAT_POLICY_LOSS, RLKS_STAT_VF_LOSS, RLKS_STAT_KL, RLKS_STAT_ENTROPY, RLKS_STAT_ROWS = 0, 1, 2, 3, 4
 
 

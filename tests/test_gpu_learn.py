@@ -219,31 +219,46 @@ def test_gather_is_a_permutation_per_epoch():
 
 # ----------------------------------------------------------------------------- end to end
 def test_ppo_iteration_parity_and_surface(tmp_path):
-    """one iteration: rollout invariants, GAE vs oracle on the GPU's own buffers, one SGD step's
-    gradient vs the oracle on the gathered minibatch, then the RLlib-style result surface"""
+    """one iteration at the c2 size (4,096 lanes x 128 steps): the fused rollout's env transitions
+    replayed bit-exactly by the C oracle, values / GAE vs the oracle, one SGD step's gradient vs the
+    fp64 oracle on the gathered minibatch, then the RLlib-style result surface"""
     from rlks import _lib
     from rlks.ppo import PPO, PPOConfig
+    from rlks.tables import load_table
 
     d = _dev()
+    N, T = 4096, 128
     cfg = (PPOConfig().environment("K8sMultiCloudEnv").framework("torch")
-           .training(train_batch_size=512 * 128, sgd_minibatch_size=8192, num_sgd_iter=2, lr=3e-4, gamma=0.99)
+           .training(train_batch_size=N * T, sgd_minibatch_size=8192, num_sgd_iter=2, lr=3e-4, gamma=0.99)
            .debugging(seed=11))
-    cfg.num_envs = 512
+    cfg.num_envs = N
     algo = PPO(config=cfg, device=d)
-    assert algo.T == 128 and algo.n_mb == 8
+    assert algo.T == T and algo.n_mb == 64
     algo.rollout(explore=True)
     b = {k: v.cpu().numpy() for k, v in algo.buf.items()}
-    # rollout invariants: rewards are table lookups of the chosen cloud at the lane's step
-    assert set(np.unique(b["actions"])) <= {0, 1}
+    assert set(np.unique(b["actions"])) <= {0, 1} and 0 < b["actions"].mean() < 1
     assert b["dones"].sum() > 0
+    # env transitions of the fused kernel == the C oracle fed the same actions (bit-exact)
+    tab = load_table()
+    ora = oracle.OracleEnv(oracle.make_cfg(N, tab.n_rows, tab.n_clouds, noise_mode=0, seed=11, autoreset=1),
+                           tab.cost, tab.latency)
+    np.testing.assert_array_equal(ora.reset().view(np.uint32), b["obs"][0].view(np.uint32))
+    for t in range(T):
+        o, r, term, _, _, _ = ora.step(b["actions"][t])
+        np.testing.assert_array_equal(o.view(np.uint32), b["obs"][t + 1].view(np.uint32))
+        np.testing.assert_array_equal(r.astype(np.float32).view(np.uint32), b["rewards"][t].view(np.uint32))
+        np.testing.assert_array_equal(term, b["dones"][t])
     # logp consistent with the stored logits
     lo = b["logits"].astype(np.float64)
     lsm = lo - np.log(np.exp(lo - lo.max(-1, keepdims=True)).sum(-1, keepdims=True)) - lo.max(-1, keepdims=True)
     close(np.take_along_axis(lsm, b["actions"][..., None].astype(int), -1)[..., 0], b["logp"], 1e-5)
-    # values of obs[t] recomputed by the oracle
+    # logits and values of visited observations recomputed by the oracle
     flat = algo.params.flat.cpu().numpy()
-    el, ev = oracle.mlp_forward(flat, algo.params.offsets, 6, 256, 2, b["obs"][:4].reshape(-1, 6))
-    close(b["values"][:4].reshape(-1), ev)
+    for t in (0, 57, T):
+        el, ev = oracle.mlp_forward(flat, algo.params.offsets, 6, 256, 2, b["obs"][t])
+        close(b["values"][t], ev)
+        if t < T:
+            close(b["logits"][t], el)
     algo.advantages()
     ea, evt = oracle.gae(b["rewards"], b["values"], b["dones"], 0.99, 1.0)
     close(algo.buf["adv"].cpu().numpy(), ea)
