@@ -46,6 +46,12 @@ typedef struct rlks_env rlks_env;
  * lane state (step, episode, optional MT19937 state) in HBM.  Synchronises. */
 int rlks_env_create(const rlks_env_cfg* cfg, const double* cost_host, const double* lat_host,
                     rlks_env** out);
+/* Same, with the node-level extension when cfg->nodes_per_cluster > 0: node_cpu_m
+ * and node_mem_mi are per-cluster node capacities [n_clouds]; arrival_trace [n_trace] gives the
+ * per-step Poisson rate for arrival_mode 1 (bursty), indexed by step mod n_trace. */
+int rlks_env_create_ext(const rlks_env_cfg* cfg, const double* cost_host, const double* lat_host,
+                        const int32_t* node_cpu_m_host, const int32_t* node_mem_mi_host,
+                        const double* arrival_trace_host, int n_trace, rlks_env** out);
 int rlks_env_destroy(rlks_env* env);
 int rlks_env_config(const rlks_env* env, rlks_env_cfg* out);
 
@@ -76,6 +82,14 @@ int rlks_env_sample_step(rlks_env* env, const float* logits_dev, int explore, in
 /* Sum of completed-episode returns and their count over all lanes (double[2]); clear != 0
  * zeroes the accumulators (PPO result "episode_reward_mean", train_ppo.py:29-30). */
 int rlks_env_episode_stats(rlks_env* env, double* out_dev, int clear, void* stream);
+
+/* node-level extension: free millicores / MiB per node as [n_envs][n_clouds][nodes] and the
+ * per-cluster used millicores [n_envs][n_clouds] (any pointer may be NULL) */
+int rlks_env_node_state(rlks_env* env, int32_t* free_cpu_dev, int32_t* free_mem_dev, int32_t* used_cpu_dev,
+                        void* stream);
+/* placement counters {nodes scanned, pods placed, pods rejected} (u64[3]) copied to out_dev when
+ * non-NULL; enable = 1 / 0 turns counting on (zeroed) / off, -1 leaves it unchanged */
+int rlks_env_counters(rlks_env* env, int enable, unsigned long long* out_dev, void* stream);
 
 /* copy lane counters (current_step, episode index) into caller buffers (either may be NULL) */
 int rlks_env_lane_state(rlks_env* env, int32_t* steps_dev, int32_t* episodes_dev, void* stream);

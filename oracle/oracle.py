@@ -61,6 +61,9 @@ def lib():
         h.ro_env_seed_lane.argtypes = [C.c_void_p, C.c_int, u32p, C.c_int]
         h.ro_env_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         h.ro_env_step.argtypes = [C.c_void_p] + [C.c_void_p] * 7
+        h.ro_env_enable_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        h.ro_env_node_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        h.ro_env_counters.argtypes = [C.c_void_p, C.c_void_p]
         h.ro_env_lane_step.argtypes = [C.c_void_p, C.c_int]
         h.ro_env_lane_episode.argtypes = [C.c_void_p, C.c_int]
         _lib = h
@@ -98,25 +101,49 @@ def mt_random(seed: int, n: int) -> np.ndarray:
     return np.array([lib().ro_mt_random(sp) for _ in range(n)], dtype=np.float64)
 
 
-def make_cfg(n_envs, n_rows, n_clouds, *, noise_mode=1, seed=0, autoreset=0, env_offset=0, max_steps=None):
+def make_cfg(n_envs, n_rows, n_clouds, *, noise_mode=1, seed=0, autoreset=0, env_offset=0, max_steps=None,
+             nodes=0, pod_cpu_m=100, pod_mem_mi=64, arrival_mode=0, arrival_rate=1.0, depart_prob=0.5,
+             init_occupancy=0.5, reject_penalty=0.0):
     cfg = EnvCfg()
     cfg.n_envs, cfg.n_rows, cfg.n_clouds = n_envs, n_rows, n_clouds
     cfg.max_steps = n_rows - 1 if max_steps is None else max_steps
     cfg.noise_mode, cfg.autoreset, cfg.env_offset, cfg.seed = noise_mode, autoreset, env_offset, seed
     cfg.cpu_lo, cfg.cpu_hi, cfg.w_cost, cfg.w_lat, cfg.scale = 0.1, 0.8, 0.6, 0.4, 100.0
+    cfg.nodes_per_cluster, cfg.pod_cpu_m, cfg.pod_mem_mi = nodes, pod_cpu_m, pod_mem_mi
+    cfg.arrival_mode, cfg.arrival_rate, cfg.depart_prob = arrival_mode, arrival_rate, depart_prob
+    cfg.init_occupancy, cfg.reject_penalty = init_occupancy, reject_penalty
     return cfg
 
 
 class OracleEnv:
     """Batched CPU env with the same semantics as librlks' env kernel."""
 
-    def __init__(self, cfg: EnvCfg, cost: np.ndarray, lat: np.ndarray):
+    def __init__(self, cfg: EnvCfg, cost: np.ndarray, lat: np.ndarray, cap_cpu=None, cap_mem=None, trace=None):
         self.cfg = cfg
         self.cost = np.ascontiguousarray(cost, dtype=np.float64)
         self.lat = np.ascontiguousarray(lat, dtype=np.float64)
         dp = C.POINTER(C.c_double)
         self.h = lib().ro_env_create(C.byref(cfg), self.cost.ctypes.data_as(dp), self.lat.ctypes.data_as(dp))
         self.n, self.D = cfg.n_envs, 3 * cfg.n_clouds
+        if cfg.nodes_per_cluster > 0:
+            cc = np.ascontiguousarray(cap_cpu, np.int32)
+            cm = np.ascontiguousarray(cap_mem, np.int32)
+            tr = np.ascontiguousarray(trace if trace is not None else [cfg.arrival_rate], np.float64)
+            rc = lib().ro_env_enable_nodes(self.h, cc.ctypes.data, cm.ctypes.data, tr.ctypes.data, len(tr))
+            assert rc == 0
+
+    def node_state(self):
+        C_, N = self.cfg.n_clouds, self.cfg.nodes_per_cluster
+        fc = np.zeros((self.n, C_, N), np.int32)
+        fm = np.zeros((self.n, C_, N), np.int32)
+        used = np.zeros((self.n, C_), np.int32)
+        lib().ro_env_node_state(self.h, fc.ctypes.data, fm.ctypes.data, used.ctypes.data)
+        return fc, fm, used
+
+    def counters(self):
+        c = np.zeros(3, np.int64)
+        lib().ro_env_counters(self.h, c.ctypes.data)
+        return c
 
     def seed(self, lane, seed):
         k, kp = _u32(seed_words(seed))

@@ -116,6 +116,18 @@ typedef struct ro_env {
   int32_t* step;
   int32_t* episode;
   uint32_t* mt; /* [n][625] */
+  /* node-level extension; NULL / 0 when nodes_per_cluster == 0 */
+  int32_t* cap_cpu;   /* [C] millicores per node */
+  int32_t* cap_mem;   /* [C] MiB per node */
+  int32_t* init_max;  /* [C] max initial pods per node = floor(init_occupancy * max_pods) */
+  int32_t* free_cpu;  /* [n][C][N] */
+  int32_t* free_mem;  /* [n][C][N] */
+  int32_t* used_cpu;  /* [n][C] */
+  double* lam;        /* arrival rates: [1] (Poisson) or [n_trace] (bursty) */
+  double* enl;        /* exp(-lam), computed once on the host */
+  int n_trace;
+  uint32_t p_dep;     /* depart_prob as a 32-bit threshold */
+  int64_t counters[3]; /* nodes scanned, pods placed, pods rejected */
 } ro_env;
 
 ro_env* ro_env_create(const rlks_env_cfg* cfg, const double* cost, const double* lat) {
@@ -140,8 +152,143 @@ ro_env* ro_env_create(const rlks_env_cfg* cfg, const double* cost, const double*
 
 void ro_env_destroy(ro_env* e) {
   if (!e) return;
-  free(e->cost); free(e->lat); free(e->step); free(e->episode); free(e->mt); free(e);
+  free(e->cost); free(e->lat); free(e->step); free(e->episode); free(e->mt);
+  free(e->cap_cpu); free(e->cap_mem); free(e->init_max); free(e->free_cpu); free(e->free_mem);
+  free(e->used_cpu); free(e->lam); free(e->enl);
+  free(e);
 }
+
+/* ---------------------------------------------------------------- node-level extension
+ * Spec (builder-defined, the reference has no node state).  Per env, C clusters
+ * x N nodes with integer free millicores / MiB; homogeneous pods (req_cpu, req_mem).
+ *  reset: node g = c*N + n gets pods0 = (x * (init_max[c] + 1)) >> 32 with x = word (g & 3) of
+ *         Philox(ctr = {gid, episode, g >> 2, OCCUPANCY << 16}).
+ *  step(a) at row t:
+ *   1. departures: for every cluster c, x = Philox({gid, episode, t, DEPART << 16 | c >> 1}),
+ *      (w0, w1) = words (2(c&1), 2(c&1)+1); if w0 < p_dep: node n = (w1 * N) >> 32 of cluster c
+ *      loses one pod if it has any;
+ *   2. arrivals: k ~ Poisson(lam) by inverse transform on u53 of Philox({gid, episode, t,
+ *      ARRIVAL << 16}) words (0, 1): p = exp(-lam); F = p; while (u > F && k < 64)
+ *      { k++; p = p * lam / k; F += p; }  (f64, no FMA; lam = rate, or trace[t mod n_trace]);
+ *   3. first-fit: each pod goes to the lowest-index node of cluster a with free cpu >= req_cpu
+ *      and free mem >= req_mem (the scan resumes where the previous pod landed); none -> rejected;
+ *   4. reward = scale * (w_cost * cost[t][a] + w_lat * lat[t][a]) - penalty * rejected;
+ *   5. t += 1; obs = [cost[t][.], lat[t][.], used_cpu[c] / (N * cap_cpu[c])] (f64 -> f32). */
+static void nodes_reset_lane(ro_env* e, int lane) {
+  const rlks_env_cfg* cfg = &e->cfg;
+  const int C = cfg->n_clouds, N = cfg->nodes_per_cluster;
+  int32_t* fc = e->free_cpu + (size_t)lane * C * N;
+  int32_t* fm = e->free_mem + (size_t)lane * C * N;
+  int32_t* used = e->used_cpu + (size_t)lane * C;
+  uint32_t key[2] = {(uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32)};
+  for (int c = 0; c < C; ++c) used[c] = 0;
+  for (int g = 0; g < C * N; ++g) {
+    uint32_t x[4];
+    uint32_t ctr[4] = {(uint32_t)(cfg->env_offset + lane), (uint32_t)e->episode[lane], (uint32_t)(g >> 2),
+                       (uint32_t)RLKS_PURPOSE_OCCUPANCY << 16};
+    ro_philox4x32_10(ctr, key, x);
+    const int c = g / N;
+    const int32_t pods = (int32_t)(((uint64_t)x[g & 3] * (uint64_t)(e->init_max[c] + 1)) >> 32);
+    fc[g] = e->cap_cpu[c] - pods * cfg->pod_cpu_m;
+    fm[g] = e->cap_mem[c] - pods * cfg->pod_mem_mi;
+    used[c] += pods * cfg->pod_cpu_m;
+  }
+}
+
+/* returns rejected pods */
+static int nodes_step_lane(ro_env* e, int lane, int a, int t) {
+  const rlks_env_cfg* cfg = &e->cfg;
+  const int C = cfg->n_clouds, N = cfg->nodes_per_cluster;
+  int32_t* fc = e->free_cpu + (size_t)lane * C * N;
+  int32_t* fm = e->free_mem + (size_t)lane * C * N;
+  int32_t* used = e->used_cpu + (size_t)lane * C;
+  uint32_t key[2] = {(uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32)};
+  const uint32_t gid = (uint32_t)(cfg->env_offset + lane), ep = (uint32_t)e->episode[lane];
+  for (int c = 0; c < C; ++c) {
+    uint32_t x[4];
+    uint32_t ctr[4] = {gid, ep, (uint32_t)t, ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)(c >> 1)};
+    ro_philox4x32_10(ctr, key, x);
+    const uint32_t w0 = x[2 * (c & 1)], w1 = x[2 * (c & 1) + 1];
+    if (w0 < e->p_dep) {
+      const int n = (int)(((uint64_t)w1 * (uint64_t)N) >> 32);
+      const int g = c * N + n;
+      if (fc[g] < e->cap_cpu[c]) {
+        fc[g] += cfg->pod_cpu_m;
+        fm[g] += cfg->pod_mem_mi;
+        used[c] -= cfg->pod_cpu_m;
+      }
+    }
+  }
+  uint32_t x[4];
+  uint32_t ctr[4] = {gid, ep, (uint32_t)t, (uint32_t)RLKS_PURPOSE_ARRIVAL << 16};
+  ro_philox4x32_10(ctr, key, x);
+  const double u = ro_u53(x[0], x[1]);
+  const int j = cfg->arrival_mode ? t % e->n_trace : 0;
+  const double lam = e->lam[j];
+  double p = e->enl[j], F = p;
+  int k = 0;
+  while (u > F && k < 64) {
+    k += 1;
+    p = p * lam / (double)k;
+    F = F + p;
+  }
+  int n = 0, rejected = 0;
+  int32_t* ac = fc + (size_t)a * N;
+  int32_t* am = fm + (size_t)a * N;
+  for (int i = 0; i < k; ++i) {
+    while (n < N && !(ac[n] >= cfg->pod_cpu_m && am[n] >= cfg->pod_mem_mi)) ++n;
+    e->counters[0] += (n < N) ? 1 : 0;
+    if (n == N) { rejected = k - i; break; }
+    ac[n] -= cfg->pod_cpu_m;
+    am[n] -= cfg->pod_mem_mi;
+    used[a] += cfg->pod_cpu_m;
+    e->counters[1] += 1;
+  }
+  e->counters[0] += n;
+  e->counters[2] += rejected;
+  return rejected;
+}
+
+int ro_env_enable_nodes(ro_env* e, const int32_t* cap_cpu, const int32_t* cap_mem, const double* lam,
+                        int n_trace) {
+  const rlks_env_cfg* cfg = &e->cfg;
+  const int C = cfg->n_clouds, N = cfg->nodes_per_cluster;
+  const size_t n = (size_t)cfg->n_envs;
+  if (N <= 0 || cfg->pod_cpu_m <= 0 || cfg->pod_mem_mi <= 0) return -1;
+  e->cap_cpu = (int32_t*)malloc(C * sizeof(int32_t));
+  e->cap_mem = (int32_t*)malloc(C * sizeof(int32_t));
+  e->init_max = (int32_t*)malloc(C * sizeof(int32_t));
+  for (int c = 0; c < C; ++c) {
+    e->cap_cpu[c] = cap_cpu[c];
+    e->cap_mem[c] = cap_mem[c];
+    int mp = cap_cpu[c] / cfg->pod_cpu_m;
+    if (cap_mem[c] / cfg->pod_mem_mi < mp) mp = cap_mem[c] / cfg->pod_mem_mi;
+    e->init_max[c] = (int32_t)floor(cfg->init_occupancy * (double)mp);
+  }
+  e->n_trace = cfg->arrival_mode ? n_trace : 1;
+  e->lam = (double*)malloc(e->n_trace * sizeof(double));
+  e->enl = (double*)malloc(e->n_trace * sizeof(double));
+  for (int i = 0; i < e->n_trace; ++i) {
+    e->lam[i] = cfg->arrival_mode ? lam[i] : cfg->arrival_rate;
+    e->enl[i] = exp(-e->lam[i]);
+  }
+  const double pd = cfg->depart_prob * 4294967296.0;
+  e->p_dep = pd >= 4294967295.0 ? 0xffffffffu : (pd <= 0 ? 0u : (uint32_t)pd);
+  e->free_cpu = (int32_t*)calloc(n * C * N, sizeof(int32_t));
+  e->free_mem = (int32_t*)calloc(n * C * N, sizeof(int32_t));
+  e->used_cpu = (int32_t*)calloc(n * C, sizeof(int32_t));
+  for (size_t i = 0; i < n; ++i) nodes_reset_lane(e, (int)i);
+  return 0;
+}
+
+void ro_env_node_state(const ro_env* e, int32_t* free_cpu, int32_t* free_mem, int32_t* used_cpu) {
+  const size_t n = (size_t)e->cfg.n_envs, CN = (size_t)e->cfg.n_clouds * e->cfg.nodes_per_cluster;
+  if (free_cpu) memcpy(free_cpu, e->free_cpu, n * CN * sizeof(int32_t));
+  if (free_mem) memcpy(free_mem, e->free_mem, n * CN * sizeof(int32_t));
+  if (used_cpu) memcpy(used_cpu, e->used_cpu, n * e->cfg.n_clouds * sizeof(int32_t));
+}
+
+void ro_env_counters(const ro_env* e, int64_t* out3) { memcpy(out3, e->counters, sizeof(e->counters)); }
 
 int ro_env_seed_lane(ro_env* e, int lane, const uint32_t* key, int keylen) {
   if (!e || lane < 0 || lane >= e->cfg.n_envs || keylen <= 0) return -1;
@@ -171,10 +318,15 @@ static double noise_draw(ro_env* e, int lane, int t, int c) {
 
 /* obs of row t for one lane (consumes C noise draws, AWS first: :92-93) */
 static void write_obs(ro_env* e, int lane, int t, float* obs) {
-  const int C = e->cfg.n_clouds;
+  const int C = e->cfg.n_clouds, N = e->cfg.nodes_per_cluster;
   for (int c = 0; c < C; ++c) obs[c] = (float)e->cost[(size_t)t * C + c];
   for (int c = 0; c < C; ++c) obs[C + c] = (float)e->lat[(size_t)t * C + c];
-  for (int c = 0; c < C; ++c) obs[2 * C + c] = (float)noise_draw(e, lane, t, c);
+  if (N > 0) {
+    for (int c = 0; c < C; ++c)
+      obs[2 * C + c] = (float)((double)e->used_cpu[(size_t)lane * C + c] / ((double)N * (double)e->cap_cpu[c]));
+  } else {
+    for (int c = 0; c < C; ++c) obs[2 * C + c] = (float)noise_draw(e, lane, t, c);
+  }
 }
 
 int ro_env_reset(ro_env* e, const uint8_t* mask, float* obs) {
@@ -183,6 +335,7 @@ int ro_env_reset(ro_env* e, const uint8_t* mask, float* obs) {
     if (mask && !mask[i]) continue;
     e->step[i] = 0;
     e->episode[i] += 1;
+    if (e->cfg.nodes_per_cluster > 0) nodes_reset_lane(e, i);
     write_obs(e, i, 0, obs + (size_t)i * D);
   }
   return 0;
@@ -205,11 +358,13 @@ int ro_env_step(ro_env* e, const int32_t* actions, float* obs, double* reward, u
     int t = e->step[i];
     term[i] = 0;
     if (t >= T) { status[1]++; reward[i] = 0.0; step_out[i] = t; continue; }
+    int rejected = cfg->nodes_per_cluster > 0 ? nodes_step_lane(e, i, a, t) : 0;
     double cost = e->cost[(size_t)t * C + a];
     double lat = e->lat[(size_t)t * C + a];
     double t1 = cfg->w_cost * cost;
     double t2 = cfg->w_lat * lat;
     reward[i] = cfg->scale * (t1 + t2);
+    if (cfg->reject_penalty != 0.0) reward[i] = reward[i] - cfg->reject_penalty * (double)rejected;
     t += 1;
     e->step[i] = t;
     step_out[i] = t;
@@ -222,6 +377,7 @@ int ro_env_step(ro_env* e, const int32_t* actions, float* obs, double* reward, u
       if (final_obs) memcpy(final_obs + (size_t)i * D, o, D * sizeof(float));
       e->step[i] = 0;
       e->episode[i] += 1;
+      if (cfg->nodes_per_cluster > 0) nodes_reset_lane(e, i);
       write_obs(e, i, 0, o);
     }
   }

@@ -9,7 +9,10 @@
 // that 100*(0.6*cost + 0.4*latency) is bit-identical to CPython (no FMA contraction).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstring>
+#include <vector>
 #include <mutex>
 #include <new>
 
@@ -75,7 +78,14 @@ __global__ void k_env_reset(EnvView v, const double* __restrict__ cost, const do
   v.episode[lane] = ep;
   v.step[lane] = 0;
   v.ep_ret[lane] = 0.0;
+  if (v.nodes > 0) nodes_reset_lane(v, lane, ep);
   emit_obs(v, s_tab, lane, 0, ep, obs + (size_t)lane * 3 * v.C);
+}
+
+// node occupancy at creation (episode 0), so that stepping before the first reset is defined
+__global__ void k_nodes_init(EnvView v) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane < v.N) nodes_reset_lane(v, lane, v.episode[lane]);
 }
 
 __global__ void k_validate(int N, int C, const int32_t* __restrict__ actions, int32_t* __restrict__ status) {
@@ -184,6 +194,23 @@ __global__ void k_lane_state(int N, const int32_t* __restrict__ step, const int3
   if (ep_out) ep_out[i] = ep[i];
 }
 
+// [C*N][n_envs] -> [n_envs][C][N] (test / inspection surface)
+__global__ void k_node_transpose(EnvView v, int32_t* __restrict__ fc, int32_t* __restrict__ fm) {
+  const size_t cn = (size_t)v.C * v.nodes;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // destination index
+  if (i >= cn * v.N) return;
+  const size_t lane = i / cn, g = i % cn;
+  if (fc) fc[i] = v.free_cpu[g * v.N + lane];
+  if (fm) fm[i] = v.free_mem[g * v.N + lane];
+}
+
+__global__ void k_used_transpose(EnvView v, int32_t* __restrict__ used) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)v.C * v.N) return;
+  const size_t lane = i / v.C, c = i % v.C;
+  used[i] = v.used_cpu[c * v.N + lane];
+}
+
 __global__ void k_philox(const uint32_t* __restrict__ ctr, const uint32_t* __restrict__ key,
                          uint32_t* __restrict__ out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -205,22 +232,40 @@ using namespace rlks;
 extern "C" {
 
 int rlks_env_create(const rlks_env_cfg* cfg, const double* cost, const double* lat, rlks_env** out) {
+  RLKS_REQUIRE(cfg, RLKS_ERR_ARG, "rlks_env_create: null cfg");
+  RLKS_REQUIRE(cfg->nodes_per_cluster == 0, RLKS_ERR_ARG,
+               "rlks_env_create: node-level clusters need per-cluster capacities (rlks_env_create_ext)");
+  return rlks_env_create_ext(cfg, cost, lat, nullptr, nullptr, nullptr, 0, out);
+}
+
+int rlks_env_create_ext(const rlks_env_cfg* cfg, const double* cost, const double* lat, const int32_t* node_cpu_m,
+                        const int32_t* node_mem_mi, const double* arrival_trace, int n_trace, rlks_env** out) {
   RLKS_REQUIRE(cfg && cost && lat && out, RLKS_ERR_ARG, "rlks_env_create: null argument");
   RLKS_REQUIRE(cfg->n_envs > 0 && cfg->n_rows > 0 && cfg->n_clouds > 0, RLKS_ERR_ARG,
                "rlks_env_create: n_envs, n_rows and n_clouds must be positive");
   RLKS_REQUIRE(cfg->max_steps > 0, RLKS_ERR_ARG, "rlks_env_create: max_steps must be positive");
   RLKS_REQUIRE(cfg->noise_mode == RLKS_NOISE_PHILOX || cfg->noise_mode == RLKS_NOISE_MT19937,
                RLKS_ERR_ARG, "rlks_env_create: unknown noise_mode");
-  RLKS_REQUIRE(cfg->nodes_per_cluster == 0, RLKS_ERR_UNSUPPORTED,
-               "rlks_env_create: node-level clusters are built by rlks_cluster_create");
   RLKS_REQUIRE((size_t)2 * cfg->n_rows * cfg->n_clouds * sizeof(double) <= (size_t)MAX_TABLE_BYTES,
                RLKS_ERR_UNSUPPORTED, "rlks_env_create: tables exceed the LDS budget");
+  const int C = cfg->n_clouds, NN = cfg->nodes_per_cluster;
+  if (NN > 0) {
+    RLKS_REQUIRE(node_cpu_m && node_mem_mi, RLKS_ERR_ARG, "rlks_env_create_ext: per-cluster capacities required");
+    RLKS_REQUIRE(NN % 4 == 0, RLKS_ERR_ARG, "rlks_env_create_ext: nodes_per_cluster must be a multiple of 4");
+    RLKS_REQUIRE(cfg->pod_cpu_m > 0 && cfg->pod_mem_mi > 0, RLKS_ERR_ARG, "rlks_env_create_ext: bad pod request");
+    RLKS_REQUIRE(cfg->arrival_mode == 0 || (arrival_trace && n_trace > 0), RLKS_ERR_ARG,
+                 "rlks_env_create_ext: bursty arrivals need a trace");
+    RLKS_REQUIRE(cfg->arrival_rate >= 0 && cfg->depart_prob >= 0 && cfg->init_occupancy >= 0, RLKS_ERR_ARG,
+                 "rlks_env_create_ext: rates must be non-negative");
+    for (int c = 0; c < C; ++c)
+      RLKS_REQUIRE(node_cpu_m[c] > 0 && node_mem_mi[c] > 0, RLKS_ERR_ARG, "rlks_env_create_ext: bad capacity");
+  }
   *out = nullptr;
   rlks_env* e = new (std::nothrow) rlks_env();
   RLKS_REQUIRE(e, RLKS_ERR_STATE, "rlks_env_create: out of host memory");
   e->cfg = *cfg;
   e->span = cfg->cpu_hi - cfg->cpu_lo;
-  const size_t N = cfg->n_envs, TC = (size_t)cfg->n_rows * cfg->n_clouds;
+  const size_t N = cfg->n_envs, TC = (size_t)cfg->n_rows * C;
   hipError_t err = hipSuccess;
   auto alloc = [&](void** p, size_t bytes) {
     if (err == hipSuccess) err = hipMalloc(p, bytes);
@@ -234,9 +279,40 @@ int rlks_env_create(const rlks_env_cfg* cfg, const double* cost, const double* l
   alloc((void**)&e->d_ret_sum, N * sizeof(double));
   alloc((void**)&e->d_ep_cnt, N * sizeof(int32_t));
   alloc((void**)&e->d_status, 4 * sizeof(int32_t));
+  alloc((void**)&e->d_counters, 4 * sizeof(unsigned long long));
   if (cfg->noise_mode == RLKS_NOISE_MT19937) alloc((void**)&e->d_mt, (size_t)(MT_N + 1) * N * sizeof(uint32_t));
   if (err == hipSuccess) err = hipMemcpy(e->d_cost, cost, TC * sizeof(double), hipMemcpyHostToDevice);
   if (err == hipSuccess) err = hipMemcpy(e->d_lat, lat, TC * sizeof(double), hipMemcpyHostToDevice);
+  if (NN > 0) {
+    // host-side constants, computed exactly as oracle/rlks_oracle.c:ro_env_enable_nodes does
+    std::vector<int32_t> cap(3 * C);
+    for (int c = 0; c < C; ++c) {
+      cap[c] = node_cpu_m[c];
+      cap[C + c] = node_mem_mi[c];
+      const int mp = std::min(node_cpu_m[c] / cfg->pod_cpu_m, node_mem_mi[c] / cfg->pod_mem_mi);
+      cap[2 * C + c] = (int32_t)std::floor(cfg->init_occupancy * (double)mp);
+    }
+    e->n_trace = cfg->arrival_mode ? n_trace : 1;
+    std::vector<double> lam(2 * e->n_trace);
+    for (int i = 0; i < e->n_trace; ++i) {
+      lam[i] = cfg->arrival_mode ? arrival_trace[i] : cfg->arrival_rate;
+      lam[e->n_trace + i] = std::exp(-lam[i]);
+    }
+    const double pd = cfg->depart_prob * 4294967296.0;
+    e->p_dep = pd >= 4294967295.0 ? 0xffffffffu : (pd <= 0 ? 0u : (uint32_t)pd);
+    const size_t cells = (size_t)C * NN * N;
+    alloc((void**)&e->d_cap, cap.size() * sizeof(int32_t));
+    alloc((void**)&e->d_lam, lam.size() * sizeof(double));
+    alloc((void**)&e->d_free_cpu, cells * sizeof(int32_t));
+    alloc((void**)&e->d_free_mem, cells * sizeof(int32_t));
+    alloc((void**)&e->d_used_cpu, (size_t)C * N * sizeof(int32_t));
+    if (err == hipSuccess) err = hipMemcpy(e->d_cap, cap.data(), cap.size() * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(e->d_lam, lam.data(), lam.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (err == hipSuccess) {
+      hipLaunchKernelGGL(k_nodes_init, dim3(cdiv(N, ENV_BLOCK)), dim3(ENV_BLOCK), 0, 0, view(e));
+      err = hipGetLastError();
+    }
+  }
   if (err == hipSuccess && e->d_mt) {
     hipLaunchKernelGGL(k_mt_seed, dim3(cdiv(N, ENV_BLOCK)), dim3(ENV_BLOCK), 0, 0, view(e), nullptr,
                        nullptr, nullptr, 0, cfg->seed);
@@ -256,7 +332,13 @@ int rlks_env_destroy(rlks_env* e) {
   hipDeviceSynchronize();
   hipFree(e->d_cost); hipFree(e->d_lat); hipFree(e->d_step); hipFree(e->d_episode);
   hipFree(e->d_ep_ret); hipFree(e->d_ret_sum); hipFree(e->d_ep_cnt); hipFree(e->d_status);
+  hipFree(e->d_counters);
   if (e->d_mt) hipFree(e->d_mt);
+  if (e->d_cap) hipFree(e->d_cap);
+  if (e->d_lam) hipFree(e->d_lam);
+  if (e->d_free_cpu) hipFree(e->d_free_cpu);
+  if (e->d_free_mem) hipFree(e->d_free_mem);
+  if (e->d_used_cpu) hipFree(e->d_used_cpu);
   delete e;
   return RLKS_OK;
 }
@@ -328,6 +410,35 @@ int rlks_env_lane_state(rlks_env* e, int32_t* steps, int32_t* episodes, void* st
   hipLaunchKernelGGL(k_lane_state, dim3(cdiv(e->cfg.n_envs, ENV_BLOCK)), dim3(ENV_BLOCK), 0,
                      (hipStream_t)stream, e->cfg.n_envs, e->d_step, e->d_episode, steps, episodes);
   RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_env_node_state(rlks_env* e, int32_t* free_cpu, int32_t* free_mem, int32_t* used_cpu, void* stream) {
+  RLKS_REQUIRE(e, RLKS_ERR_ARG, "rlks_env_node_state: null env");
+  RLKS_REQUIRE(e->cfg.nodes_per_cluster > 0, RLKS_ERR_STATE, "rlks_env_node_state: env has no nodes");
+  const EnvView v = view(e);
+  const size_t cells = (size_t)v.C * v.nodes * v.N;
+  hipStream_t s = (hipStream_t)stream;
+  if (free_cpu || free_mem) {
+    hipLaunchKernelGGL(k_node_transpose, dim3(cdiv((long)cells, 256)), dim3(256), 0, s, v, free_cpu, free_mem);
+    RLKS_LAUNCHED();
+  }
+  if (used_cpu) {
+    hipLaunchKernelGGL(k_used_transpose, dim3(cdiv((long)v.C * v.N, 256)), dim3(256), 0, s, v, used_cpu);
+    RLKS_LAUNCHED();
+  }
+  return RLKS_OK;
+}
+
+int rlks_env_counters(rlks_env* e, int enable, unsigned long long* out_dev, void* stream) {
+  RLKS_REQUIRE(e, RLKS_ERR_ARG, "rlks_env_counters: null env");
+  hipStream_t s = (hipStream_t)stream;
+  if (out_dev) RLKS_HIP(hipMemcpyAsync(out_dev, e->d_counters, 3 * sizeof(unsigned long long),
+                                       hipMemcpyDeviceToDevice, s));
+  if (enable >= 0) {
+    if (enable && !e->counters_on) RLKS_HIP(hipMemsetAsync(e->d_counters, 0, 3 * sizeof(unsigned long long), s));
+    e->counters_on = enable;
+  }
   return RLKS_OK;
 }
 

@@ -26,6 +26,16 @@ struct rlks_env {
   int32_t* d_ep_cnt;  // [N] completed episodes since last clear
   uint32_t* d_mt;     // [625][N] (MT19937 mode only)
   int32_t* d_status;  // [4] scratch
+  // node-level extension, allocated when cfg.nodes_per_cluster > 0
+  int32_t* d_cap;       // [3][C]: node cpu (m), node mem (MiB), max initial pods per node
+  double* d_lam;        // [2][n_trace]: arrival rate, exp(-rate)
+  int n_trace;
+  uint32_t p_dep;       // depart_prob as a 32-bit threshold
+  int32_t* d_free_cpu;  // [C*N][n_envs]
+  int32_t* d_free_mem;  // [C*N][n_envs]
+  int32_t* d_used_cpu;  // [C][n_envs]
+  unsigned long long* d_counters;  // [3] nodes scanned, pods placed, pods rejected (opt-in)
+  int counters_on;
 };
 
 namespace rlks {
@@ -43,6 +53,16 @@ struct EnvView {
   double* ret_sum;
   int32_t* ep_cnt;
   uint32_t* mt;
+  // node-level extension; nodes == 0 is the reference env
+  int nodes, pod_cpu, pod_mem, arrival_mode, n_trace;
+  uint32_t p_dep;
+  double penalty;
+  const int32_t* cap;   // [3][C]
+  const double* lam;    // [2][n_trace]
+  int32_t* free_cpu;    // [C*N][n_envs]
+  int32_t* free_mem;
+  int32_t* used_cpu;    // [C][n_envs]
+  unsigned long long* counters;  // null unless enabled
 };
 
 inline EnvView view(const rlks_env* e) {
@@ -54,6 +74,11 @@ inline EnvView view(const rlks_env* e) {
   v.scale = e->cfg.scale;
   v.step = e->d_step; v.episode = e->d_episode; v.ep_ret = e->d_ep_ret; v.ret_sum = e->d_ret_sum;
   v.ep_cnt = e->d_ep_cnt; v.mt = e->d_mt;
+  v.nodes = e->cfg.nodes_per_cluster; v.pod_cpu = e->cfg.pod_cpu_m; v.pod_mem = e->cfg.pod_mem_mi;
+  v.arrival_mode = e->cfg.arrival_mode; v.n_trace = e->n_trace; v.p_dep = e->p_dep;
+  v.penalty = e->cfg.reject_penalty;
+  v.cap = e->d_cap; v.lam = e->d_lam; v.free_cpu = e->d_free_cpu; v.free_mem = e->d_free_mem;
+  v.used_cpu = e->d_used_cpu; v.counters = e->counters_on ? e->d_counters : nullptr;
   return v;
 }
 
@@ -81,13 +106,107 @@ __device__ __forceinline__ double noise(const EnvView& v, int lane, int t, int c
   return __dadd_rn(v.cpu_lo, __dmul_rn(v.span, u));
 }
 
+// ---------------------------------------------------------------- node-level extension
+// DESIGN.md §4 (builder-defined; same algorithm, same Philox counters and the same f64 operation
+// order as oracle/rlks_oracle.c: nodes_reset_lane / nodes_step_lane).  Node state is SoA
+// [C*N][n_envs]: one lane's nodes are n_envs apart, so a wave's scan of node n is coalesced.
+__device__ __forceinline__ void nodes_reset_lane(const EnvView& v, int lane, int episode) {
+  const int C = v.C, N = v.nodes, S = v.N;
+  const uint32_t gid = (uint32_t)(v.env_offset + lane);
+  for (int c = 0; c < C; ++c) {
+    const int32_t cc = v.cap[c], cm = v.cap[C + c], m1 = v.cap[2 * C + c] + 1;
+    int32_t used = 0;
+    for (int n4 = 0; n4 < N; n4 += 4) {
+      const int g0 = c * N + n4;  // N % 4 == 0: a Philox block never straddles clusters
+      const u32x4 x = philox4x32_10(u32x4{gid, (uint32_t)episode, (uint32_t)(g0 >> 2),
+                                          (uint32_t)RLKS_PURPOSE_OCCUPANCY << 16}, v.k0, v.k1);
+      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int32_t pods = (int32_t)(((uint64_t)w[j] * (uint64_t)m1) >> 32);
+        v.free_cpu[(size_t)(g0 + j) * S + lane] = cc - pods * v.pod_cpu;
+        v.free_mem[(size_t)(g0 + j) * S + lane] = cm - pods * v.pod_mem;
+        used += pods * v.pod_cpu;
+      }
+    }
+    v.used_cpu[(size_t)c * S + lane] = used;
+  }
+}
+
+// departures, Poisson arrivals and first-fit placement in cluster a at row t; returns rejected pods
+__device__ __forceinline__ int nodes_step_lane(const EnvView& v, int lane, int a, int t, int episode) {
+  const int C = v.C, N = v.nodes, S = v.N;
+  const uint32_t gid = (uint32_t)(v.env_offset + lane);
+  for (int c2 = 0; c2 < C; c2 += 2) {
+    const u32x4 x = philox4x32_10(u32x4{gid, (uint32_t)episode, (uint32_t)t,
+                                        ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)(c2 >> 1)}, v.k0, v.k1);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = c2 + j;
+      if (c < C && w[2 * j] < v.p_dep) {
+        const int n = (int)(((uint64_t)w[2 * j + 1] * (uint64_t)N) >> 32);
+        const size_t i = (size_t)(c * N + n) * S + lane;
+        const int32_t fc = v.free_cpu[i];
+        if (fc < v.cap[c]) {
+          v.free_cpu[i] = fc + v.pod_cpu;
+          v.free_mem[i] += v.pod_mem;
+          v.used_cpu[(size_t)c * S + lane] -= v.pod_cpu;
+        }
+      }
+    }
+  }
+  const u32x4 x = philox4x32_10(u32x4{gid, (uint32_t)episode, (uint32_t)t, (uint32_t)RLKS_PURPOSE_ARRIVAL << 16},
+                                v.k0, v.k1);
+  const double u = u53(x.x, x.y);
+  const int j = v.arrival_mode ? t % v.n_trace : 0;
+  const double lam = v.lam[j];
+  double p = v.lam[v.n_trace + j], F = p;
+  int k = 0;
+  while (u > F && k < 64) {
+    k += 1;
+    p = __ddiv_rn(__dmul_rn(p, lam), (double)k);
+    F = __dadd_rn(F, p);
+  }
+  int n = 0, rejected = 0, placed = 0;
+  const size_t base = (size_t)a * N * S + lane;
+  int32_t used_add = 0;
+  for (int i = 0; i < k; ++i) {
+    int32_t fc = 0, fm = 0;
+    while (n < N) {
+      fc = v.free_cpu[base + (size_t)n * S];
+      fm = v.free_mem[base + (size_t)n * S];
+      if (fc >= v.pod_cpu && fm >= v.pod_mem) break;
+      ++n;
+    }
+    if (n == N) { rejected = k - i; break; }
+    v.free_cpu[base + (size_t)n * S] = fc - v.pod_cpu;
+    v.free_mem[base + (size_t)n * S] = fm - v.pod_mem;
+    used_add += v.pod_cpu;
+    ++placed;
+  }
+  if (used_add) v.used_cpu[(size_t)a * S + lane] += used_add;
+  if (v.counters) {
+    atomicAdd(&v.counters[0], (unsigned long long)(n + placed));
+    atomicAdd(&v.counters[1], (unsigned long long)placed);
+    atomicAdd(&v.counters[2], (unsigned long long)rejected);
+  }
+  return rejected;
+}
+
 // _get_obs (:90-103): f32[cost[0..C), lat[0..C), cpu[0..C)] of row t
 __device__ __forceinline__ void emit_obs(const EnvView& v, const double* s_tab, int lane, int t,
                                          int episode, float* __restrict__ o) {
   const int C = v.C, TC = v.T * v.C;
   for (int c = 0; c < C; ++c) o[c] = (float)s_tab[t * C + c];
   for (int c = 0; c < C; ++c) o[C + c] = (float)s_tab[TC + t * C + c];
-  for (int c = 0; c < C; ++c) o[2 * C + c] = (float)noise(v, lane, t, c, episode);
+  if (v.nodes > 0) {  // utilisation of each cluster from its nodes (extension)
+    for (int c = 0; c < C; ++c)
+      o[2 * C + c] = (float)__ddiv_rn((double)v.used_cpu[(size_t)c * v.N + lane],
+                                      __dmul_rn((double)v.nodes, (double)v.cap[c]));
+  } else {
+    for (int c = 0; c < C; ++c) o[2 * C + c] = (float)noise(v, lane, t, c, episode);
+  }
 }
 
 struct StepOut {
@@ -108,9 +227,12 @@ __device__ __forceinline__ StepOut step_lane(const EnvView& v, const double* s_t
     r.overrun = true;
     return r;
   }
+  int ep = v.episode[lane];
+  const int rejected = v.nodes > 0 ? nodes_step_lane(v, lane, a, t, ep) : 0;
   const double cost = s_tab[t * C + a];
   const double lat = s_tab[TC + t * C + a];
   r.reward = __dmul_rn(v.scale, __dadd_rn(__dmul_rn(v.w_cost, cost), __dmul_rn(v.w_lat, lat)));
+  if (v.penalty != 0.0) r.reward = __dsub_rn(r.reward, __dmul_rn(v.penalty, (double)rejected));
   t += 1;
   v.step[lane] = t;
   r.step = t;
@@ -119,7 +241,6 @@ __device__ __forceinline__ StepOut step_lane(const EnvView& v, const double* s_t
     r.overrun = true;
     return r;
   }
-  int ep = v.episode[lane];
   emit_obs(v, s_tab, lane, t, ep, o);
   // episode return bookkeeping (PPO result episode_reward_mean)
   double ret = v.ep_ret[lane] + r.reward;
@@ -135,6 +256,7 @@ __device__ __forceinline__ StepOut step_lane(const EnvView& v, const double* s_t
       for (int j = 0; j < D; ++j) final_o[j] = o[j];
     v.step[lane] = 0;
     v.episode[lane] = ep + 1;
+    if (v.nodes > 0) nodes_reset_lane(v, lane, ep + 1);
     emit_obs(v, s_tab, lane, 0, ep + 1, o);
   }
   return r;

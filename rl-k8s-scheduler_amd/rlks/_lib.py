@@ -64,7 +64,10 @@ SIGNATURES = {
     "rlks_last_error": [],
     "rlks_version": [],
     "rlks_env_create": [C.POINTER(EnvCfg), _P, _P, C.POINTER(_P)],
+    "rlks_env_create_ext": [C.POINTER(EnvCfg), _P, _P, _P, _P, _P, _I, C.POINTER(_P)],
     "rlks_env_destroy": [_P],
+    "rlks_env_node_state": [_P, _P, _P, _P, _P],
+    "rlks_env_counters": [_P, _I, _P, _P],
     "rlks_env_config": [_P, C.POINTER(EnvCfg)],
     "rlks_env_seed": [_P, _P, _P, _P, _I, _P],
     "rlks_env_reset": [_P, _P, _P, _P],

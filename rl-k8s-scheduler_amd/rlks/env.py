@@ -62,7 +62,10 @@ def seed_key_words(seed: int) -> list:
     return words or [0]
 
 
-def make_cfg(n_envs, table, *, noise="philox", seed=0, autoreset=True, env_offset=0, max_steps=None):
+def make_cfg(n_envs, table, *, noise="philox", seed=0, autoreset=True, env_offset=0, max_steps=None,
+             nodes=None):
+    """rlks_env_cfg for `n_envs` lanes over `table`; `nodes` (a NodeSpec) enables the node-level
+    extension"""
     cfg = _lib.EnvCfg()
     cfg.n_envs = int(n_envs)
     cfg.n_rows = table.n_rows
@@ -74,22 +77,71 @@ def make_cfg(n_envs, table, *, noise="philox", seed=0, autoreset=True, env_offse
     cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     cfg.cpu_lo, cfg.cpu_hi = 0.1, 0.8          # random.uniform(0.1, 0.8) (:87)
     cfg.w_cost, cfg.w_lat, cfg.scale = 0.6, 0.4, 100.0  # 100 * (0.6*cost + 0.4*latency) (:122)
+    if nodes is not None:
+        cfg.nodes_per_cluster = nodes.nodes_per_cluster
+        cfg.pod_cpu_m, cfg.pod_mem_mi = nodes.pod_cpu_m, nodes.pod_mem_mi
+        cfg.arrival_mode = 1 if nodes.arrival_trace is not None else 0
+        cfg.arrival_rate, cfg.depart_prob = nodes.arrival_rate, nodes.depart_prob
+        cfg.init_occupancy, cfg.reject_penalty = nodes.init_occupancy, nodes.reject_penalty
     return cfg
+
+
+class NodeSpec:
+    """Node-level cluster model (builder-defined, the reference has no node state).
+
+    Defaults follow the reference manifests: pod request 100m / 64Mi (simple-service.yaml:25-28);
+    node types t3.micro-like (2 vCPU / 1 GiB) and Standard_B2s-like (2 vCPU / 4 GiB)
+    (aws-/azure-cluster-config.yaml:12) alternating over the clusters.
+    """
+
+    def __init__(self, n_clouds, nodes_per_cluster=256, *, node_cpu_m=None, node_mem_mi=None, pod_cpu_m=100,
+                 pod_mem_mi=64, arrival_rate=1.0, arrival_trace=None, depart_prob=0.5, init_occupancy=0.5,
+                 reject_penalty=0.0):
+        self.n_clouds = int(n_clouds)
+        self.nodes_per_cluster = int(nodes_per_cluster)
+        self.node_cpu_m = np.ascontiguousarray(node_cpu_m if node_cpu_m is not None else [2000] * self.n_clouds,
+                                               np.int32)
+        self.node_mem_mi = np.ascontiguousarray(
+            node_mem_mi if node_mem_mi is not None else [1024 if c % 2 == 0 else 4096 for c in range(self.n_clouds)],
+            np.int32)
+        self.pod_cpu_m, self.pod_mem_mi = int(pod_cpu_m), int(pod_mem_mi)
+        self.arrival_rate = float(arrival_rate)
+        self.arrival_trace = None if arrival_trace is None else np.ascontiguousarray(arrival_trace, np.float64)
+        self.depart_prob, self.init_occupancy = float(depart_prob), float(init_occupancy)
+        self.reject_penalty = float(reject_penalty)
+
+
+def bursty_trace(n=100, base=1.0, peak=2.0, ramp=20, burst_every=25, burst=4.0):
+    """Per-step Poisson rates with the shape of the reference's Locust runs
+    (data/local_aws_load_stats_history.csv: a 0 -> 20 user ramp, then a ~10 rps plateau):
+    a linear ramp to `peak` over `ramp` steps, then `base` with a `burst` every `burst_every` steps."""
+    lam = np.full(n, base, np.float64)
+    lam[:ramp] = peak * np.arange(ramp) / ramp
+    lam[ramp::burst_every] = burst
+    return lam
 
 
 class DeviceEnv:
     """Owner of one rlks_env handle (HBM lane state + staged tables)."""
 
-    def __init__(self, cfg: _lib.EnvCfg, table, device=None):
+    def __init__(self, cfg: _lib.EnvCfg, table, device=None, nodes: NodeSpec | None = None):
         import ctypes as C
 
         self.torch = _torch()
         self.device = _device(device)
         self.cfg = cfg
         self.table = table
+        self.nodes = nodes
         with self.torch.cuda.device(self.device):
             h = C.c_void_p()
-            _lib.call("rlks_env_create", C.byref(cfg), table.cost.ctypes.data, table.latency.ctypes.data, C.byref(h))
+            if nodes is None:
+                _lib.call("rlks_env_create", C.byref(cfg), table.cost.ctypes.data, table.latency.ctypes.data,
+                          C.byref(h))
+            else:
+                tr = nodes.arrival_trace
+                _lib.call("rlks_env_create_ext", C.byref(cfg), table.cost.ctypes.data, table.latency.ctypes.data,
+                          nodes.node_cpu_m.ctypes.data, nodes.node_mem_mi.ctypes.data,
+                          None if tr is None else tr.ctypes.data, 0 if tr is None else len(tr), C.byref(h))
         self.handle = h
         self.n = cfg.n_envs
         self.obs_dim = 3 * cfg.n_clouds
@@ -206,17 +258,19 @@ class VecK8sMultiCloudEnv:
     """
 
     def __init__(self, num_envs, *, table=None, seed=0, noise="philox", autoreset=True, env_offset=0,
-                 device=None, data_path=None):
+                 device=None, data_path=None, nodes: NodeSpec | None = None):
         torch = _torch()
         self.table = table if table is not None else load_table(data_path)
+        self.nodes = nodes
         self.num_envs = int(num_envs)
         self.n_clouds = self.table.n_clouds
         self.obs_dim = 3 * self.n_clouds
         self.action_space = Discrete(self.n_clouds)
         self.observation_space = Box(0.0, 1.0, (self.obs_dim,), np.float32)
         self.max_steps = self.table.n_rows - 1
-        self.cfg = make_cfg(num_envs, self.table, noise=noise, seed=seed, autoreset=autoreset, env_offset=env_offset)
-        self.dev = DeviceEnv(self.cfg, self.table, device)
+        self.cfg = make_cfg(num_envs, self.table, noise=noise, seed=seed, autoreset=autoreset, env_offset=env_offset,
+                            nodes=nodes)
+        self.dev = DeviceEnv(self.cfg, self.table, device, nodes)
         d = self.dev.device
         self.device = d
         N = self.num_envs
@@ -283,6 +337,23 @@ class VecK8sMultiCloudEnv:
         ep = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
         _lib.call("rlks_env_lane_state", self.handle, _lib.ptr(st), _lib.ptr(ep), self.dev.stream)
         return st, ep
+
+    def node_state(self):
+        """(free_cpu [N, C, nodes], free_mem [N, C, nodes], used_cpu [N, C]) int32 device tensors"""
+        torch = _torch()
+        n, C_, k = self.num_envs, self.n_clouds, self.nodes.nodes_per_cluster
+        fc = torch.empty(n, C_, k, dtype=torch.int32, device=self.device)
+        fm = torch.empty(n, C_, k, dtype=torch.int32, device=self.device)
+        used = torch.empty(n, C_, dtype=torch.int32, device=self.device)
+        _lib.call("rlks_env_node_state", self.handle, _lib.ptr(fc), _lib.ptr(fm), _lib.ptr(used), self.dev.stream)
+        return fc, fm, used
+
+    def counters(self, enable=-1):
+        """{nodes scanned, pods placed, pods rejected} since counting was enabled (enable=1 resets)"""
+        torch = _torch()
+        out = torch.zeros(3, dtype=torch.int64, device=self.device)
+        _lib.call("rlks_env_counters", self.handle, int(enable), _lib.ptr(out), self.dev.stream)
+        return out
 
     def close(self):
         self.dev.close()
