@@ -25,6 +25,8 @@ import sys
 import time
 from pathlib import Path
 
+import numpy as np
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "rl-k8s-scheduler_amd"))
 
@@ -126,7 +128,72 @@ def kernel_timing(algo, torch, reps=20):
                              "GBps_moved": moved, "env_steps_per_s": big / (ms * 1e-3)}
     venv.close()
     del venv, acts
+    out["k_node_step_c3"] = node_env_timing(algo, torch, timed)
+    out["k_node_step_c3_churn"] = node_env_timing(algo, torch, timed, depart_prob=0.02)
     return out
+
+
+def node_env_timing(algo, torch, timed, n=65536, C=8, nodes=256, depart_prob="stationary"):
+    """BASELINE configs[2]: the node-level step kernel k_node_step (65,536 envs x 8 clusters x 256
+    nodes, Poisson(1) arrivals, first-fit, per-pod departures: "stationary" = arrivals balance
+    departures at the initial occupancy U(0, 50%); a float = that per-pod probability).
+
+    Timed as a production driver runs it: ABI steps on preallocated buffers captured once into a
+    HIP graph and replayed.  `ms` = the kernel alone (trusted actions: status = NULL);
+    `ms_validated` = the full checked step (status memset + k_validate + k_node_step)."""
+    from rlks import VecK8sMultiCloudEnv, _lib
+    from rlks.env import NodeSpec
+    from rlks.tables import synthetic_table
+
+    spec = NodeSpec(C, nodes, arrival_rate=1.0, depart_prob=depart_prob, init_occupancy=0.5)
+    venv = VecK8sMultiCloudEnv(n, table=synthetic_table(C, 100, seed=42), seed=42, nodes=spec, device=algo.device)
+    venv.reset()
+    acts = [torch.randint(0, C, (n,), dtype=torch.int32, device=algo.device) for _ in range(8)]
+    for t in range(60):
+        venv.step(acts[t % 8])
+    venv.counters(enable=1)  # placement / departure statistics from an untimed eager pass
+    cnt_steps = 32
+    for t in range(cnt_steps):
+        venv.step(acts[t % 8])
+    cnt = venv.counters(enable=0).cpu().numpy().astype(np.float64) / (cnt_steps * n)  # per env-step
+    venv.check_status()
+    torch.cuda.synchronize()
+    reps = 64
+
+    def graph(checked):
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                cs = torch.cuda.current_stream().cuda_stream
+                for t in range(reps):
+                    _lib.call("rlks_env_step", venv.handle, acts[t % 8].data_ptr(), venv.obs.data_ptr(),
+                              venv.reward.data_ptr(), None, venv.terminated.data_ptr(), venv.truncated.data_ptr(),
+                              venv.steps.data_ptr(), venv.final_obs.data_ptr(),
+                              venv._status.data_ptr() if checked else None, cs)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        return g
+
+    g_kernel, g_checked = graph(False), graph(True)
+    ms = timed(g_kernel.replay, n=5) / reps
+    ms_checked = timed(g_checked.replay, n=5) / reps
+    venv.check_status()
+    checks, placed, rejected, departed, written = cnt
+    # algorithmic bytes per env-step: every node read once (8 B), written nodes 8 B, obs 12C,
+    # used aggregates 4C, action 4, step r/w 8, episode 4, ep_ret r/w 16, reward 8, done 1, trunc 1, step_out 4
+    read_nodes = 8.0 * C * nodes
+    algo_bytes = read_nodes + 8 * written + 12 * C + 4 * C + 4 + 8 + 4 + 16 + 8 + 1 + 1 + 4
+    gbs = algo_bytes * n / (ms * 1e-3) / 1e9
+    res = {"kernel": "k_node_step", "depart_prob": spec.depart_prob, "ms": ms, "ms_validated": ms_checked, "envs": n, "clusters": C,
+           "nodes": nodes, "env_steps_per_s": n / (ms * 1e-3), "env_steps_per_s_validated": n / (ms_checked * 1e-3),
+           "node_checks_per_step": checks, "placed_per_step": placed, "rejected_per_step": rejected,
+           "departed_per_step": departed, "nodes_written_per_step": written,
+           "bytes_per_step": algo_bytes, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
+    venv.close()
+    return res
 
 
 def pmc_traffic():

@@ -67,14 +67,18 @@ int rlks_env_reset(rlks_env* env, const uint8_t* mask_dev, float* obs_dev, void*
 /* step(action) (:115-144) for all lanes.  status_dev[0] = invalid actions (when > 0 NO lane
  * steps: the reference asserts before any change, :116); status_dev[1] = lanes that ran past the
  * last table row (the reference's IndexError, :91).  reward64 is bit-exact f64 (no FMA);
- * reward32/truncated/step_out/final_obs may be NULL. */
+ * reward32/truncated/step_out/final_obs may be NULL.  Node-level envs (nodes_per_cluster > 0)
+ * run the node sweep (departures, arrivals, first-fit) in the same call.
+ * status_dev == NULL declares the actions trusted (produced by rlks sampling): no validation
+ * launch and no status report. */
 int rlks_env_step(rlks_env* env, const int32_t* actions_dev, float* obs_dev, double* reward64_dev,
                   float* reward32_dev, uint8_t* terminated_dev, uint8_t* truncated_dev,
                   int32_t* step_out_dev, float* final_obs_dev, int32_t* status_dev, void* stream);
 
 /* Fused action sampling + step for the rollout (RLlib sampler + TorchCategorical): action =
  * Categorical(logits) via Philox (explore != 0) or argmax (explore == 0, compute_single_action
- * explore=False); logp of the chosen action; env step; auto-reset; episode-return tracking. */
+ * explore=False); logp of the chosen action; env step; auto-reset; episode-return tracking.
+ * Table envs only (RLKS_ERR_UNSUPPORTED for node-level envs). */
 int rlks_env_sample_step(rlks_env* env, const float* logits_dev, int explore, int32_t* actions_dev,
                          float* logp_dev, float* obs_next_dev, float* reward_dev, uint8_t* done_dev,
                          void* stream);
@@ -87,8 +91,9 @@ int rlks_env_episode_stats(rlks_env* env, double* out_dev, int clear, void* stre
  * per-cluster used millicores [n_envs][n_clouds] (any pointer may be NULL) */
 int rlks_env_node_state(rlks_env* env, int32_t* free_cpu_dev, int32_t* free_mem_dev, int32_t* used_cpu_dev,
                         void* stream);
-/* placement counters {nodes scanned, pods placed, pods rejected} (u64[3]) copied to out_dev when
- * non-NULL; enable = 1 / 0 turns counting on (zeroed) / off, -1 leaves it unchanged */
+/* node counters {node checks by first fit, pods placed, pods rejected, pods departed, nodes written}
+ * (u64[5]) copied to out_dev when non-NULL; enable = 1 / 0 turns counting on (zeroed) / off, -1
+ * leaves it unchanged.  The flag is read when a step is launched (a captured graph keeps it). */
 int rlks_env_counters(rlks_env* env, int enable, unsigned long long* out_dev, void* stream);
 
 /* copy lane counters (current_step, episode index) into caller buffers (either may be NULL) */

@@ -52,7 +52,7 @@ typedef struct rlks_env_cfg {
   int32_t pod_mem_mi;        /* pod request, MiB (simple-service.yaml:28: 64Mi) */
   int32_t arrival_mode;      /* 0: Poisson(arrival_rate); 1: bursty trace (per-step rates) */
   double arrival_rate;       /* mean pod arrivals per step */
-  double depart_prob;        /* per-step probability that one pod leaves the chosen cluster */
+  double depart_prob;        /* per-step probability that a running pod leaves (every pod) */
   double init_occupancy;     /* initial pods per node ~ U(0, init_occupancy * max_pods) */
   double reject_penalty;     /* subtracted from reward per rejected pod (0: reference reward) */
 } rlks_env_cfg;

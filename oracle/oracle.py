@@ -64,6 +64,7 @@ def lib():
         h.ro_env_enable_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         h.ro_env_node_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         h.ro_env_counters.argtypes = [C.c_void_p, C.c_void_p]
+        h.ro_binom_cdf32.argtypes = [C.c_int, C.c_double, C.c_void_p]
         h.ro_env_lane_step.argtypes = [C.c_void_p, C.c_int]
         h.ro_env_lane_episode.argtypes = [C.c_void_p, C.c_int]
         _lib = h
@@ -102,7 +103,7 @@ def mt_random(seed: int, n: int) -> np.ndarray:
 
 
 def make_cfg(n_envs, n_rows, n_clouds, *, noise_mode=1, seed=0, autoreset=0, env_offset=0, max_steps=None,
-             nodes=0, pod_cpu_m=100, pod_mem_mi=64, arrival_mode=0, arrival_rate=1.0, depart_prob=0.5,
+             nodes=0, pod_cpu_m=100, pod_mem_mi=64, arrival_mode=0, arrival_rate=1.0, depart_prob=0.02,
              init_occupancy=0.5, reject_penalty=0.0):
     cfg = EnvCfg()
     cfg.n_envs, cfg.n_rows, cfg.n_clouds = n_envs, n_rows, n_clouds
@@ -141,7 +142,8 @@ class OracleEnv:
         return fc, fm, used
 
     def counters(self):
-        c = np.zeros(3, np.int64)
+        """[node checks, pods placed, pods rejected, pods departed, nodes written]"""
+        c = np.zeros(5, np.int64)
         lib().ro_env_counters(self.h, c.ctypes.data)
         return c
 
@@ -278,3 +280,10 @@ def adam(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8):
     denom = (vt.sqrt() / (bc2 ** 0.5)).add_(eps)
     pt.addcdiv_(mt, denom, value=-(lr / bc1))
     return pt.numpy(), mt.numpy(), vt.numpy()
+
+
+def binom_cdf32(maxp, p):
+    """[maxp+1][maxp+1] Binomial(n, p) CDF table in units of 2^-32 (departure draws)"""
+    out = np.zeros((maxp + 1, maxp + 1), np.uint32)
+    lib().ro_binom_cdf32(int(maxp), float(p), out.ctypes.data)
+    return out

@@ -126,8 +126,9 @@ typedef struct ro_env {
   double* lam;        /* arrival rates: [1] (Poisson) or [n_trace] (bursty) */
   double* enl;        /* exp(-lam), computed once on the host */
   int n_trace;
-  uint32_t p_dep;     /* depart_prob as a 32-bit threshold */
-  int64_t counters[3]; /* nodes scanned, pods placed, pods rejected */
+  int maxp;           /* most pods a node can hold */
+  uint32_t* cdf;      /* [maxp+1][maxp+1] Binomial(n, depart_prob) CDF in units of 2^-32 */
+  int64_t counters[5]; /* node checks, pods placed, pods rejected, pods departed, nodes written */
 } ro_env;
 
 ro_env* ro_env_create(const rlks_env_cfg* cfg, const double* cost, const double* lat) {
@@ -154,7 +155,7 @@ void ro_env_destroy(ro_env* e) {
   if (!e) return;
   free(e->cost); free(e->lat); free(e->step); free(e->episode); free(e->mt);
   free(e->cap_cpu); free(e->cap_mem); free(e->init_max); free(e->free_cpu); free(e->free_mem);
-  free(e->used_cpu); free(e->lam); free(e->enl);
+  free(e->used_cpu); free(e->lam); free(e->enl); free(e->cdf);
   free(e);
 }
 
@@ -164,16 +165,48 @@ void ro_env_destroy(ro_env* e) {
  *  reset: node g = c*N + n gets pods0 = (x * (init_max[c] + 1)) >> 32 with x = word (g & 3) of
  *         Philox(ctr = {gid, episode, g >> 2, OCCUPANCY << 16}).
  *  step(a) at row t:
- *   1. departures: for every cluster c, x = Philox({gid, episode, t, DEPART << 16 | c >> 1}),
- *      (w0, w1) = words (2(c&1), 2(c&1)+1); if w0 < p_dep: node n = (w1 * N) >> 32 of cluster c
- *      loses one pod if it has any;
+ *   1. departures (geometric per pod-slot): for every node g = c*N + n holding
+ *      pods = (cap_cpu[c] - free_cpu[g]) / req_cpu pods, u = word (g & 3) of
+ *      Philox({gid, episode, t, DEPART << 16 | g >> 2}); d = 0; while (d < pods && u >=
+ *      cdf[pods][d]) d++; d pods leave.  cdf = ro_binom_cdf32(maxp, depart_prob) is the
+ *      Binomial(pods, p) CDF in units of 2^-32.  (Nodes are processed in blocks of 4 that share
+ *      one Philox call; a block whose 4 nodes are all empty draws nothing.)
  *   2. arrivals: k ~ Poisson(lam) by inverse transform on u53 of Philox({gid, episode, t,
  *      ARRIVAL << 16}) words (0, 1): p = exp(-lam); F = p; while (u > F && k < 64)
  *      { k++; p = p * lam / k; F += p; }  (f64, no FMA; lam = rate, or trace[t mod n_trace]);
  *   3. first-fit: each pod goes to the lowest-index node of cluster a with free cpu >= req_cpu
  *      and free mem >= req_mem (the scan resumes where the previous pod landed); none -> rejected;
  *   4. reward = scale * (w_cost * cost[t][a] + w_lat * lat[t][a]) - penalty * rejected;
- *   5. t += 1; obs = [cost[t][.], lat[t][.], used_cpu[c] / (N * cap_cpu[c])] (f64 -> f32). */
+ *   5. t += 1; obs = [cost[t][.], lat[t][.], (float)used_cpu[c] / (float)(N * cap_cpu[c])]. */
+
+/* Binomial(n, p) CDF rows n = 0..maxp: P(X <= j) * 2^32 rounded half-up, capped at 2^32 - 1
+ * (columns j >= n hold 2^32 - 1; the walk above stops at d = pods).  Plain f64 multiply / divide /
+ * add, in this order. */
+void ro_binom_cdf32(int maxp, double p, uint32_t* cdf) {
+  const int M1 = maxp + 1;
+  for (int i = 0; i < M1 * M1; ++i) cdf[i] = 0xffffffffu;
+  for (int n = 0; n <= maxp; ++n) {
+    uint32_t* row = cdf + (size_t)n * M1;
+    if (p >= 1.0) {
+      for (int j = 0; j < n; ++j) row[j] = 0;
+      continue;
+    }
+    if (p <= 0.0) continue;
+    const double q = 1.0 - p, r = p / q;
+    double pmf = 1.0, acc = 0.0;
+    for (int i = 0; i < n; ++i) pmf = pmf * q;
+    for (int j = 0; j < n; ++j) {
+      acc = acc + pmf;
+      double x = acc * 4294967296.0;
+      x = x + 0.5;
+      row[j] = x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
+      pmf = pmf * (double)(n - j);
+      pmf = pmf / (double)(j + 1);
+      pmf = pmf * r;
+    }
+  }
+}
+
 static void nodes_reset_lane(ro_env* e, int lane) {
   const rlks_env_cfg* cfg = &e->cfg;
   const int C = cfg->n_clouds, N = cfg->nodes_per_cluster;
@@ -204,19 +237,28 @@ static int nodes_step_lane(ro_env* e, int lane, int a, int t) {
   int32_t* used = e->used_cpu + (size_t)lane * C;
   uint32_t key[2] = {(uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32)};
   const uint32_t gid = (uint32_t)(cfg->env_offset + lane), ep = (uint32_t)e->episode[lane];
-  for (int c = 0; c < C; ++c) {
+  const int M1 = e->maxp + 1;
+  uint8_t* dirty = (uint8_t*)calloc((size_t)C * N, 1); /* nodes the step writes back */
+  for (int g0 = 0; g0 < C * N; g0 += 4) {
+    const int c = g0 / N;
+    int pods[4], any = 0;
+    for (int q = 0; q < 4; ++q) {
+      pods[q] = (e->cap_cpu[c] - fc[g0 + q]) / cfg->pod_cpu_m;
+      any |= pods[q] > 0;
+    }
+    if (!any) continue;
     uint32_t x[4];
-    uint32_t ctr[4] = {gid, ep, (uint32_t)t, ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)(c >> 1)};
+    uint32_t ctr[4] = {gid, ep, (uint32_t)t, ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)(g0 >> 2)};
     ro_philox4x32_10(ctr, key, x);
-    const uint32_t w0 = x[2 * (c & 1)], w1 = x[2 * (c & 1) + 1];
-    if (w0 < e->p_dep) {
-      const int n = (int)(((uint64_t)w1 * (uint64_t)N) >> 32);
-      const int g = c * N + n;
-      if (fc[g] < e->cap_cpu[c]) {
-        fc[g] += cfg->pod_cpu_m;
-        fm[g] += cfg->pod_mem_mi;
-        used[c] -= cfg->pod_cpu_m;
-      }
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t* row = e->cdf + (size_t)pods[q] * M1;
+      int d = 0;
+      while (d < pods[q] && x[q] >= row[d]) ++d;
+      fc[g0 + q] += d * cfg->pod_cpu_m;
+      fm[g0 + q] += d * cfg->pod_mem_mi;
+      used[c] -= d * cfg->pod_cpu_m;
+      e->counters[3] += d;
+      if (d) dirty[g0 + q] = 1;
     }
   }
   uint32_t x[4];
@@ -241,11 +283,14 @@ static int nodes_step_lane(ro_env* e, int lane, int a, int t) {
     if (n == N) { rejected = k - i; break; }
     ac[n] -= cfg->pod_cpu_m;
     am[n] -= cfg->pod_mem_mi;
+    dirty[(size_t)a * N + n] = 1;
     used[a] += cfg->pod_cpu_m;
     e->counters[1] += 1;
   }
   e->counters[0] += n;
   e->counters[2] += rejected;
+  for (int g = 0; g < C * N; ++g) e->counters[4] += dirty[g];
+  free(dirty);
   return rejected;
 }
 
@@ -264,7 +309,12 @@ int ro_env_enable_nodes(ro_env* e, const int32_t* cap_cpu, const int32_t* cap_me
     int mp = cap_cpu[c] / cfg->pod_cpu_m;
     if (cap_mem[c] / cfg->pod_mem_mi < mp) mp = cap_mem[c] / cfg->pod_mem_mi;
     e->init_max[c] = (int32_t)floor(cfg->init_occupancy * (double)mp);
+    if (e->init_max[c] > mp) e->init_max[c] = mp;
+    if (mp > e->maxp) e->maxp = mp;
   }
+  if (e->maxp > 64 || N % 8 != 0 || (long)C * N > 262144) return -1;
+  e->cdf = (uint32_t*)malloc((size_t)(e->maxp + 1) * (e->maxp + 1) * sizeof(uint32_t));
+  ro_binom_cdf32(e->maxp, cfg->depart_prob, e->cdf);
   e->n_trace = cfg->arrival_mode ? n_trace : 1;
   e->lam = (double*)malloc(e->n_trace * sizeof(double));
   e->enl = (double*)malloc(e->n_trace * sizeof(double));
@@ -272,8 +322,6 @@ int ro_env_enable_nodes(ro_env* e, const int32_t* cap_cpu, const int32_t* cap_me
     e->lam[i] = cfg->arrival_mode ? lam[i] : cfg->arrival_rate;
     e->enl[i] = exp(-e->lam[i]);
   }
-  const double pd = cfg->depart_prob * 4294967296.0;
-  e->p_dep = pd >= 4294967295.0 ? 0xffffffffu : (pd <= 0 ? 0u : (uint32_t)pd);
   e->free_cpu = (int32_t*)calloc(n * C * N, sizeof(int32_t));
   e->free_mem = (int32_t*)calloc(n * C * N, sizeof(int32_t));
   e->used_cpu = (int32_t*)calloc(n * C, sizeof(int32_t));
@@ -288,7 +336,7 @@ void ro_env_node_state(const ro_env* e, int32_t* free_cpu, int32_t* free_mem, in
   if (used_cpu) memcpy(used_cpu, e->used_cpu, n * e->cfg.n_clouds * sizeof(int32_t));
 }
 
-void ro_env_counters(const ro_env* e, int64_t* out3) { memcpy(out3, e->counters, sizeof(e->counters)); }
+void ro_env_counters(const ro_env* e, int64_t* out5) { memcpy(out5, e->counters, sizeof(e->counters)); }
 
 int ro_env_seed_lane(ro_env* e, int lane, const uint32_t* key, int keylen) {
   if (!e || lane < 0 || lane >= e->cfg.n_envs || keylen <= 0) return -1;
@@ -323,7 +371,7 @@ static void write_obs(ro_env* e, int lane, int t, float* obs) {
   for (int c = 0; c < C; ++c) obs[C + c] = (float)e->lat[(size_t)t * C + c];
   if (N > 0) {
     for (int c = 0; c < C; ++c)
-      obs[2 * C + c] = (float)((double)e->used_cpu[(size_t)lane * C + c] / ((double)N * (double)e->cap_cpu[c]));
+      obs[2 * C + c] = (float)e->used_cpu[(size_t)lane * C + c] / (float)(N * e->cap_cpu[c]);
   } else {
     for (int c = 0; c < C; ++c) obs[2 * C + c] = (float)noise_draw(e, lane, t, c);
   }

@@ -104,7 +104,7 @@ __global__ void k_env_step(EnvView v, const double* __restrict__ cost, const dou
                            double* __restrict__ rew64, float* __restrict__ rew32, uint8_t* __restrict__ term,
                            uint8_t* __restrict__ trunc, int32_t* __restrict__ step_out,
                            float* __restrict__ final_obs, int32_t* __restrict__ status) {
-  if (status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
+  if (status && status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
   extern __shared__ __attribute__((aligned(16))) double s_tab[];
   stage_tables(s_tab, cost, lat, v.T * v.C);
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
@@ -121,7 +121,234 @@ __global__ void k_env_step(EnvView v, const double* __restrict__ cost, const dou
     if (step_out) step_out[lane] = r.step;
   }
   const unsigned long long m = __ballot(over);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
+  if (status && (threadIdx.x & 63) == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
+}
+
+// ---------------------------------------------------------------- node-level step (c3 / c5)
+// One workgroup = 64 envs (one per lane) x W waves; wave w sweeps clusters w, w+W, ... of its 64
+// envs.  Per node: one 16-bit Philox draw -> departures ~ Binomial(pods, depart_prob) by the
+// LDS-resident inverse-CDF table; then, in the chosen cluster, first-fit placement of the
+// arriving pods; only changed nodes are written back.  The per-cluster used millicores meet in
+// LDS, wave 0 does the reward / step / episode bookkeeping, the auto-reset lanes re-draw their
+// occupancy, and the whole workgroup writes the 64 contiguous obs rows.  Same order and counters
+// as oracle/rlks_oracle.c:nodes_step_lane.
+constexpr int NODE_CHUNK = 8;
+
+__device__ __forceinline__ float node_obs(const EnvView& v, const double* __restrict__ cost,
+                                          const double* __restrict__ lat, const int32_t* s_used, int row,
+                                          int e, int j) {
+  const int C = v.C;
+  if (j < C) return (float)cost[row * C + j];
+  if (j < 2 * C) return (float)lat[row * C + j - C];
+  const int c = j - 2 * C;
+  return __fdiv_rn((float)s_used[c * 64 + e], (float)(v.nodes * v.cap[c]));
+}
+
+__global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __restrict__ cost,
+                                                    const double* __restrict__ lat,
+                                                    const int32_t* __restrict__ actions, float* __restrict__ obs,
+                                                    double* __restrict__ rew64, float* __restrict__ rew32,
+                                                    uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                    int32_t* __restrict__ step_out, float* __restrict__ final_obs,
+                                                    int32_t* __restrict__ status) {
+  if (status && status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int C = v.C, N = v.nodes, D = 3 * C, M1 = v.maxp + 1;
+  const int W = blockDim.x >> 6, l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint4* s_pre = (uint4*)smem;                             // [M1] first 4 CDF columns of each row
+  uint32_t* s_cdf = (uint32_t*)(s_pre + M1);               // [M1][M1]
+  int32_t* s_used = (int32_t*)(s_cdf + M1 * M1);           // [C][64]
+  int32_t* s_rej = s_used + C * 64;                        // [64]
+  int32_t* s_row = s_rej + 64;                             // [64] obs row, -1 = none
+  int32_t* s_frow = s_row + 64;                            // [64] final-obs row of auto-reset lanes, -1 = none
+  for (int i = threadIdx.x; i < M1 * M1; i += blockDim.x) s_cdf[i] = v.cdf[i];
+  for (int i = threadIdx.x; i < M1; i += blockDim.x) {
+    const uint32_t* r = v.cdf + (size_t)i * M1;
+    s_pre[i] = make_uint4(r[0], 1 < M1 ? r[1] : 0xffffffffu, 2 < M1 ? r[2] : 0xffffffffu,
+                          3 < M1 ? r[3] : 0xffffffffu);  // columns >= i hold 2^32-1; d is clamped to pods
+  }
+  const int env0 = blockIdx.x * 64, env = env0 + l;
+  const bool live = env < v.N;
+  int t = 0, ep = 0, a = -1;
+  if (live) { t = v.step[env]; ep = v.episode[env]; a = actions[env]; }
+  const bool act = live && t < v.T;  // iloc[t] in bounds: this lane steps
+  if (w == 0) s_rej[l] = 0;
+  __syncthreads();
+  const uint32_t gid = (uint32_t)(v.env_offset + env);
+  const int32_t pc = v.pod_cpu, pm = v.pod_mem;
+  int2* base = v.free + (size_t)blockIdx.x * (size_t)C * N * 64 + l;
+  unsigned long long n_checks = 0, n_placed = 0, n_rej = 0, n_dep = 0, n_wr = 0;
+  for (int c = w; c < C; c += W) {
+    int32_t used = 0;
+    if (act) {
+      const int32_t cc = v.cap[c];
+      int rem = (a == c) ? arrivals(v, gid, ep, t) : 0;
+      int passed = 0, placed = 0, departed = 0, written = 0;
+      int2* col = base + (size_t)c * N * 64;
+      int32_t sum_free = 0;
+      const int2* p = col;
+      for (int n0 = 0; n0 < N; n0 += NODE_CHUNK, p += NODE_CHUNK * 64) {
+        int2 f[NODE_CHUNK];
+        int pods[NODE_CHUNK];
+#pragma unroll
+        for (int q = 0; q < NODE_CHUNK; ++q) f[q] = p[q * 64];  // immediate offsets from one pointer
+        int any = 0;
+#pragma unroll
+        for (int q = 0; q < NODE_CHUNK; ++q) {
+          pods[q] = (int)(__umul24((uint32_t)(cc - f[q].x), v.pod_mag) >> v.pod_shift);
+          any |= pods[q];
+        }
+        int2* pw = col + (size_t)n0 * 64;
+        unsigned dep_mask = 0;  // nodes already written by a departure this chunk
+        if (any) {  // departures: every pod-slot leaves with depart_prob (4 nodes per Philox draw)
+#pragma unroll
+          for (int h = 0; h < NODE_CHUNK; h += 4) {
+            if (!(pods[h] | pods[h + 1] | pods[h + 2] | pods[h + 3])) continue;  // empty block draws nothing
+            const u32x4 x = philox4x32_10_mad(u32x4{gid, (uint32_t)ep, (uint32_t)t,
+                                                    ((uint32_t)RLKS_PURPOSE_DEPART << 16) |
+                                                        (uint32_t)((c * N + n0 + h) >> 2)},
+                                              v.k0, v.k1);
+            const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int q = h + j;
+              const uint32_t u = wd[j];
+              const uint4 pre = s_pre[pods[q]];
+              int d = (int)(u >= pre.x) + (int)(u >= pre.y) + (int)(u >= pre.z) + (int)(u >= pre.w);
+              d = min(d, pods[q]);
+              if (d == 4 && pods[q] > 4) {  // 4 or more pods left this node: continue the inverse-CDF walk
+                const uint32_t* row = s_cdf + pods[q] * M1;
+                while (d < pods[q] && u >= row[d]) ++d;
+              }
+              if (d) {
+                f[q].x += __umul24(d, pc);
+                f[q].y += __umul24(d, pm);
+                departed += d;
+                ++written;
+                dep_mask |= 1u << q;
+                pw[q * 64] = f[q];
+              }
+            }
+          }
+        }
+        if (rem > 0) {  // first fit: lowest node with room; a node passed over stays passed
+#pragma unroll
+          for (int q = 0; q < NODE_CHUNK; ++q) {
+            if (rem > 0) {
+              bool put = false;
+              while (rem > 0 && f[q].x >= pc && f[q].y >= pm) {
+                f[q].x -= pc;
+                f[q].y -= pm;
+                --rem;
+                ++placed;
+                put = true;
+              }
+              if (put) {
+                pw[q * 64] = f[q];
+                written += !((dep_mask >> q) & 1u);  // one write-back per node, as the oracle counts
+              }
+              if (rem > 0) ++passed;
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < NODE_CHUNK; ++q) sum_free += f[q].x;
+      }
+      used = N * cc - sum_free;
+      if (a == c) {
+        s_rej[l] = rem;
+        n_checks += passed + placed;
+        n_placed += placed;
+        n_rej += rem;
+      }
+      n_dep += departed;
+      n_wr += written;
+    }
+    s_used[c * 64 + l] = used;
+  }
+  if (v.counters) {
+    n_checks = wave_sum_u64(n_checks);
+    n_placed = wave_sum_u64(n_placed);
+    n_rej = wave_sum_u64(n_rej);
+    n_dep = wave_sum_u64(n_dep);
+    n_wr = wave_sum_u64(n_wr);
+    if (l == 0) {
+      if (n_checks) atomicAdd(&v.counters[0], n_checks);
+      if (n_placed) atomicAdd(&v.counters[1], n_placed);
+      if (n_rej) atomicAdd(&v.counters[2], n_rej);
+      if (n_dep) atomicAdd(&v.counters[3], n_dep);
+      if (n_wr) atomicAdd(&v.counters[4], n_wr);
+    }
+  }
+  __syncthreads();
+  bool over = false, reset = false;
+  if (w == 0) {  // step (:115-144): reward on row t, t += 1, done, episode bookkeeping
+    int row = -1, frow = -1;
+    if (live) {
+      if (!act) {  // iloc[t] out of bounds before any change
+        over = true;
+        rew64[env] = 0.0;
+        if (rew32) rew32[env] = 0.f;
+        term[env] = 0;
+        if (step_out) step_out[env] = t;
+      } else {
+        double r = __dmul_rn(v.scale, __dadd_rn(__dmul_rn(v.w_cost, cost[t * C + a]),
+                                                __dmul_rn(v.w_lat, lat[t * C + a])));
+        if (v.penalty != 0.0) r = __dsub_rn(r, __dmul_rn(v.penalty, (double)s_rej[l]));
+        const int t1 = t + 1;
+        v.step[env] = t1;
+        const bool done = t1 >= v.max_steps;
+        if (t1 >= v.T) {
+          over = true;
+        } else {
+          double ret = v.ep_ret[env] + r;
+          if (done) {
+            v.ret_sum[env] += ret;
+            v.ep_cnt[env] += 1;
+            ret = 0.0;
+          }
+          v.ep_ret[env] = ret;
+          row = t1;
+          if (done && v.autoreset) {
+            frow = t1;
+            row = 0;
+            reset = true;
+            v.step[env] = 0;
+            v.episode[env] = ep + 1;
+          }
+        }
+        rew64[env] = r;
+        if (rew32) rew32[env] = (float)r;
+        term[env] = (uint8_t)done;
+        if (step_out) step_out[env] = t1;
+      }
+      if (trunc) trunc[env] = 0;
+    }
+    s_row[l] = row;
+    s_frow[l] = frow;
+    const unsigned long long m = __ballot(over);
+    if (status && l == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
+  }
+  if (__syncthreads_or(reset)) {  // auto-reset lanes: final obs, then the next episode's occupancy
+    const int nrow = min(64, v.N - env0);
+    if (final_obs)
+      for (int i = threadIdx.x; i < nrow * D; i += blockDim.x) {
+        const int e = i / D, j = i - e * D;
+        if (s_frow[e] >= 0) final_obs[(size_t)env0 * D + i] = node_obs(v, cost, lat, s_used, s_frow[e], e, j);
+      }
+    __syncthreads();
+    if (live && s_frow[l] >= 0)
+      for (int c = w; c < C; c += W)
+        s_used[c * 64 + l] = nodes_reset_cluster(v, base + (size_t)c * N * 64, c, gid, ep + 1);
+    __syncthreads();
+  }
+  if (act)
+    for (int c = w; c < C; c += W) v.used_cpu[(size_t)c * v.N + env] = s_used[c * 64 + l];
+  const int nrow = min(64, v.N - env0);
+  for (int i = threadIdx.x; i < nrow * D; i += blockDim.x) {
+    const int e = i / D, j = i - e * D;
+    if (s_row[e] >= 0) obs[(size_t)env0 * D + i] = node_obs(v, cost, lat, s_used, s_row[e], e, j);
+  }
 }
 
 // TorchCategorical sample / argmax over A logits, then step
@@ -200,8 +427,9 @@ __global__ void k_node_transpose(EnvView v, int32_t* __restrict__ fc, int32_t* _
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // destination index
   if (i >= cn * v.N) return;
   const size_t lane = i / cn, g = i % cn;
-  if (fc) fc[i] = v.free_cpu[g * v.N + lane];
-  if (fm) fm[i] = v.free_mem[g * v.N + lane];
+  const int2 f = node_col(v, (int)lane)[g * 64];
+  if (fc) fc[i] = f.x;
+  if (fm) fm[i] = f.y;
 }
 
 __global__ void k_used_transpose(EnvView v, int32_t* __restrict__ used) {
@@ -229,6 +457,39 @@ __global__ void k_mt_draws(uint32_t* __restrict__ mt, double* __restrict__ out, 
 
 using namespace rlks;
 
+namespace {
+// Binomial(n, p) CDF for n = 0..maxp in units of 2^-32 (row n, column j = P(X <= j)), capped at
+// 2^32 - 1 and computed in f64 exactly as oracle/rlks_oracle.c:ro_binom_cdf32 does; columns j >= n
+// hold 2^32 - 1 (the departure walk stops at d = pods).
+std::vector<uint32_t> binom_cdf32(int maxp, double p) {
+  const int M1 = maxp + 1;
+  std::vector<uint32_t> cdf((size_t)M1 * M1, 0xffffffffu);
+  for (int n = 0; n <= maxp; ++n) {
+    uint32_t* row = cdf.data() + (size_t)n * M1;
+    if (p >= 1.0) {
+      for (int j = 0; j < n; ++j) row[j] = 0;
+      continue;
+    }
+    if (p <= 0.0) continue;
+    const double q = 1.0 - p;
+    const double r = p / q;
+    double pmf = 1.0;
+    for (int i = 0; i < n; ++i) pmf = pmf * q;
+    double acc = 0.0;
+    for (int j = 0; j < n; ++j) {
+      acc = acc + pmf;
+      double x = acc * 4294967296.0;
+      x = x + 0.5;
+      row[j] = x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
+      pmf = pmf * (double)(n - j);
+      pmf = pmf / (double)(j + 1);
+      pmf = pmf * r;
+    }
+  }
+  return cdf;
+}
+}  // namespace
+
 extern "C" {
 
 int rlks_env_create(const rlks_env_cfg* cfg, const double* cost, const double* lat, rlks_env** out) {
@@ -251,14 +512,22 @@ int rlks_env_create_ext(const rlks_env_cfg* cfg, const double* cost, const doubl
   const int C = cfg->n_clouds, NN = cfg->nodes_per_cluster;
   if (NN > 0) {
     RLKS_REQUIRE(node_cpu_m && node_mem_mi, RLKS_ERR_ARG, "rlks_env_create_ext: per-cluster capacities required");
-    RLKS_REQUIRE(NN % 4 == 0, RLKS_ERR_ARG, "rlks_env_create_ext: nodes_per_cluster must be a multiple of 4");
+    RLKS_REQUIRE(NN % 8 == 0, RLKS_ERR_ARG, "rlks_env_create_ext: nodes_per_cluster must be a multiple of 8");
+    RLKS_REQUIRE((long)C * NN <= 262144, RLKS_ERR_UNSUPPORTED,
+                 "rlks_env_create_ext: at most 262,144 nodes per env (16-bit Philox block index)");
+    RLKS_REQUIRE(C <= 1024, RLKS_ERR_UNSUPPORTED, "rlks_env_create_ext: at most 1,024 clusters");
+    RLKS_REQUIRE(cfg->depart_prob <= 1.0, RLKS_ERR_ARG, "rlks_env_create_ext: depart_prob must be <= 1");
     RLKS_REQUIRE(cfg->pod_cpu_m > 0 && cfg->pod_mem_mi > 0, RLKS_ERR_ARG, "rlks_env_create_ext: bad pod request");
     RLKS_REQUIRE(cfg->arrival_mode == 0 || (arrival_trace && n_trace > 0), RLKS_ERR_ARG,
                  "rlks_env_create_ext: bursty arrivals need a trace");
     RLKS_REQUIRE(cfg->arrival_rate >= 0 && cfg->depart_prob >= 0 && cfg->init_occupancy >= 0, RLKS_ERR_ARG,
                  "rlks_env_create_ext: rates must be non-negative");
-    for (int c = 0; c < C; ++c)
-      RLKS_REQUIRE(node_cpu_m[c] > 0 && node_mem_mi[c] > 0, RLKS_ERR_ARG, "rlks_env_create_ext: bad capacity");
+    for (int c = 0; c < C; ++c) {
+      RLKS_REQUIRE(node_cpu_m[c] > 0 && node_mem_mi[c] > 0 && node_cpu_m[c] < (1 << 22), RLKS_ERR_ARG,
+                   "rlks_env_create_ext: bad capacity");
+      RLKS_REQUIRE(std::min(node_cpu_m[c] / cfg->pod_cpu_m, node_mem_mi[c] / cfg->pod_mem_mi) <= 64,
+                   RLKS_ERR_UNSUPPORTED, "rlks_env_create_ext: at most 64 pods per node");
+    }
   }
   *out = nullptr;
   rlks_env* e = new (std::nothrow) rlks_env();
@@ -279,35 +548,37 @@ int rlks_env_create_ext(const rlks_env_cfg* cfg, const double* cost, const doubl
   alloc((void**)&e->d_ret_sum, N * sizeof(double));
   alloc((void**)&e->d_ep_cnt, N * sizeof(int32_t));
   alloc((void**)&e->d_status, 4 * sizeof(int32_t));
-  alloc((void**)&e->d_counters, 4 * sizeof(unsigned long long));
+  alloc((void**)&e->d_counters, 8 * sizeof(unsigned long long));
   if (cfg->noise_mode == RLKS_NOISE_MT19937) alloc((void**)&e->d_mt, (size_t)(MT_N + 1) * N * sizeof(uint32_t));
   if (err == hipSuccess) err = hipMemcpy(e->d_cost, cost, TC * sizeof(double), hipMemcpyHostToDevice);
   if (err == hipSuccess) err = hipMemcpy(e->d_lat, lat, TC * sizeof(double), hipMemcpyHostToDevice);
   if (NN > 0) {
     // host-side constants, computed exactly as oracle/rlks_oracle.c:ro_env_enable_nodes does
     std::vector<int32_t> cap(3 * C);
+    e->maxp = 0;
     for (int c = 0; c < C; ++c) {
       cap[c] = node_cpu_m[c];
       cap[C + c] = node_mem_mi[c];
       const int mp = std::min(node_cpu_m[c] / cfg->pod_cpu_m, node_mem_mi[c] / cfg->pod_mem_mi);
-      cap[2 * C + c] = (int32_t)std::floor(cfg->init_occupancy * (double)mp);
+      cap[2 * C + c] = std::min(mp, (int32_t)std::floor(cfg->init_occupancy * (double)mp));
+      e->maxp = std::max(e->maxp, mp);
     }
+    const std::vector<uint32_t> cdf = binom_cdf32(e->maxp, cfg->depart_prob);
     e->n_trace = cfg->arrival_mode ? n_trace : 1;
     std::vector<double> lam(2 * e->n_trace);
     for (int i = 0; i < e->n_trace; ++i) {
       lam[i] = cfg->arrival_mode ? arrival_trace[i] : cfg->arrival_rate;
       lam[e->n_trace + i] = std::exp(-lam[i]);
     }
-    const double pd = cfg->depart_prob * 4294967296.0;
-    e->p_dep = pd >= 4294967295.0 ? 0xffffffffu : (pd <= 0 ? 0u : (uint32_t)pd);
-    const size_t cells = (size_t)C * NN * N;
+    const size_t cells = (size_t)C * NN * cdiv((long)N, 64) * 64;  // wavefront-tiled, padded to 64 lanes
     alloc((void**)&e->d_cap, cap.size() * sizeof(int32_t));
     alloc((void**)&e->d_lam, lam.size() * sizeof(double));
-    alloc((void**)&e->d_free_cpu, cells * sizeof(int32_t));
-    alloc((void**)&e->d_free_mem, cells * sizeof(int32_t));
+    alloc((void**)&e->d_cdf, cdf.size() * sizeof(uint32_t));
+    alloc((void**)&e->d_free, cells * sizeof(int2));
     alloc((void**)&e->d_used_cpu, (size_t)C * N * sizeof(int32_t));
     if (err == hipSuccess) err = hipMemcpy(e->d_cap, cap.data(), cap.size() * sizeof(int32_t), hipMemcpyHostToDevice);
     if (err == hipSuccess) err = hipMemcpy(e->d_lam, lam.data(), lam.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(e->d_cdf, cdf.data(), cdf.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (err == hipSuccess) {
       hipLaunchKernelGGL(k_nodes_init, dim3(cdiv(N, ENV_BLOCK)), dim3(ENV_BLOCK), 0, 0, view(e));
       err = hipGetLastError();
@@ -336,8 +607,8 @@ int rlks_env_destroy(rlks_env* e) {
   if (e->d_mt) hipFree(e->d_mt);
   if (e->d_cap) hipFree(e->d_cap);
   if (e->d_lam) hipFree(e->d_lam);
-  if (e->d_free_cpu) hipFree(e->d_free_cpu);
-  if (e->d_free_mem) hipFree(e->d_free_mem);
+  if (e->d_cdf) hipFree(e->d_cdf);
+  if (e->d_free) hipFree(e->d_free);
   if (e->d_used_cpu) hipFree(e->d_used_cpu);
   delete e;
   return RLKS_OK;
@@ -372,14 +643,23 @@ int rlks_env_reset(rlks_env* e, const uint8_t* mask, float* obs, void* stream) {
 int rlks_env_step(rlks_env* e, const int32_t* actions, float* obs, double* rew64, float* rew32,
                   uint8_t* term, uint8_t* trunc, int32_t* step_out, float* final_obs, int32_t* status,
                   void* stream) {
-  RLKS_REQUIRE(e && actions && obs && rew64 && term && status, RLKS_ERR_ARG,
-               "rlks_env_step: null argument");
+  RLKS_REQUIRE(e && actions && obs && rew64 && term, RLKS_ERR_ARG, "rlks_env_step: null argument");
   hipStream_t s = (hipStream_t)stream;
   const unsigned grid = cdiv(e->cfg.n_envs, ENV_BLOCK);
-  RLKS_HIP(hipMemsetAsync(status, 0, 2 * sizeof(int32_t), s));
-  hipLaunchKernelGGL(k_validate, dim3(grid), dim3(ENV_BLOCK), 0, s, e->cfg.n_envs, e->cfg.n_clouds,
-                     actions, status);
-  RLKS_LAUNCHED();
+  if (status) {  // NULL: trusted actions (e.g. from the sampler), no validation / overrun report
+    RLKS_HIP(hipMemsetAsync(status, 0, 2 * sizeof(int32_t), s));
+    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(ENV_BLOCK), 0, s, e->cfg.n_envs, e->cfg.n_clouds,
+                       actions, status);
+    RLKS_LAUNCHED();
+  }
+  if (e->cfg.nodes_per_cluster > 0) {
+    const int C = e->cfg.n_clouds, W = std::min(C, 16), M1 = e->maxp + 1;
+    const size_t lds = (size_t)M1 * 16 + (size_t)M1 * M1 * sizeof(uint32_t) + ((size_t)C * 64 + 3 * 64) * sizeof(int32_t);
+    hipLaunchKernelGGL(k_node_step, dim3(cdiv(e->cfg.n_envs, 64)), dim3(64 * W), lds, s, view(e), e->d_cost,
+                       e->d_lat, actions, obs, rew64, rew32, term, trunc, step_out, final_obs, status);
+    RLKS_LAUNCHED();
+    return RLKS_OK;
+  }
   hipLaunchKernelGGL(k_env_step, dim3(grid), dim3(ENV_BLOCK), table_lds(e), s, view(e), e->d_cost,
                      e->d_lat, actions, obs, rew64, rew32, term, trunc, step_out, final_obs, status);
   RLKS_LAUNCHED();
@@ -391,6 +671,8 @@ int rlks_env_sample_step(rlks_env* e, const float* logits, int explore, int32_t*
   RLKS_REQUIRE(e && logits && actions && logp && obs_next && reward && done, RLKS_ERR_ARG,
                "rlks_env_sample_step: null argument");
   RLKS_REQUIRE(e->cfg.autoreset, RLKS_ERR_STATE, "rlks_env_sample_step: needs autoreset lanes");
+  RLKS_REQUIRE(e->cfg.nodes_per_cluster == 0, RLKS_ERR_UNSUPPORTED,
+               "rlks_env_sample_step: node-level envs step through rlks_env_step");
   hipLaunchKernelGGL(k_sample_step, dim3(cdiv(e->cfg.n_envs, ENV_BLOCK)), dim3(ENV_BLOCK), table_lds(e),
                      (hipStream_t)stream, view(e), e->d_cost, e->d_lat, logits, explore, actions, logp,
                      obs_next, reward, done);
@@ -433,10 +715,10 @@ int rlks_env_node_state(rlks_env* e, int32_t* free_cpu, int32_t* free_mem, int32
 int rlks_env_counters(rlks_env* e, int enable, unsigned long long* out_dev, void* stream) {
   RLKS_REQUIRE(e, RLKS_ERR_ARG, "rlks_env_counters: null env");
   hipStream_t s = (hipStream_t)stream;
-  if (out_dev) RLKS_HIP(hipMemcpyAsync(out_dev, e->d_counters, 3 * sizeof(unsigned long long),
+  if (out_dev) RLKS_HIP(hipMemcpyAsync(out_dev, e->d_counters, 5 * sizeof(unsigned long long),
                                        hipMemcpyDeviceToDevice, s));
   if (enable >= 0) {
-    if (enable && !e->counters_on) RLKS_HIP(hipMemsetAsync(e->d_counters, 0, 3 * sizeof(unsigned long long), s));
+    if (enable && !e->counters_on) RLKS_HIP(hipMemsetAsync(e->d_counters, 0, 5 * sizeof(unsigned long long), s));
     e->counters_on = enable;
   }
   return RLKS_OK;

@@ -30,11 +30,12 @@ struct rlks_env {
   int32_t* d_cap;       // [3][C]: node cpu (m), node mem (MiB), max initial pods per node
   double* d_lam;        // [2][n_trace]: arrival rate, exp(-rate)
   int n_trace;
-  uint32_t p_dep;       // depart_prob as a 32-bit threshold
-  int32_t* d_free_cpu;  // [C*N][n_envs]
-  int32_t* d_free_mem;  // [C*N][n_envs]
+  int maxp;             // most pods a node can hold (over all clusters)
+  uint32_t* d_cdf;      // [maxp+1][maxp+1] Binomial(n, depart_prob) CDF in 1/65536 units
+  int2* d_free;         // [ceil(n_envs/64)][C*N][64] {free millicores, free MiB}
   int32_t* d_used_cpu;  // [C][n_envs]
-  unsigned long long* d_counters;  // [3] nodes scanned, pods placed, pods rejected (opt-in)
+  unsigned long long* d_counters;  // [5] node checks, pods placed, pods rejected, pods departed,
+                                   // nodes written (opt-in)
   int counters_on;
 };
 
@@ -54,13 +55,14 @@ struct EnvView {
   int32_t* ep_cnt;
   uint32_t* mt;
   // node-level extension; nodes == 0 is the reference env
-  int nodes, pod_cpu, pod_mem, arrival_mode, n_trace;
-  uint32_t p_dep;
+  int nodes, pod_cpu, pod_mem, arrival_mode, n_trace, maxp;
+  uint32_t pod_mag;     // pods on a node = mul_u24(cap - free, pod_mag) >> pod_shift (exact: see view())
+  int pod_shift;
   double penalty;
   const int32_t* cap;   // [3][C]
   const double* lam;    // [2][n_trace]
-  int32_t* free_cpu;    // [C*N][n_envs]
-  int32_t* free_mem;
+  const uint32_t* cdf;  // [maxp+1][maxp+1]
+  int2* free;           // [ceil(n_envs/64)][C*N][64] {free millicores, free MiB}: one 8-byte load per node
   int32_t* used_cpu;    // [C][n_envs]
   unsigned long long* counters;  // null unless enabled
 };
@@ -75,9 +77,14 @@ inline EnvView view(const rlks_env* e) {
   v.step = e->d_step; v.episode = e->d_episode; v.ep_ret = e->d_ep_ret; v.ret_sum = e->d_ret_sum;
   v.ep_cnt = e->d_ep_cnt; v.mt = e->d_mt;
   v.nodes = e->cfg.nodes_per_cluster; v.pod_cpu = e->cfg.pod_cpu_m; v.pod_mem = e->cfg.pod_mem_mi;
-  v.arrival_mode = e->cfg.arrival_mode; v.n_trace = e->n_trace; v.p_dep = e->p_dep;
+  v.arrival_mode = e->cfg.arrival_mode; v.n_trace = e->n_trace; v.maxp = e->maxp;
+  // (cap - free) = pods * pod_cpu with pods <= 64 and cap < 2^22: with m = ceil(2^24 / pod_cpu),
+  // pods * pod_cpu * m / 2^24 = pods + pods * pod_cpu * delta / 2^24, delta < 1, and the error term
+  // stays below 1 for pod_cpu < 2^18; the 24-bit product stays below 2^32.  pod_cpu = 1: identity.
+  v.pod_shift = v.pod_cpu > 1 ? 24 : 0;
+  v.pod_mag = v.pod_cpu > 1 ? (uint32_t)((16777216u + (uint32_t)v.pod_cpu - 1u) / (uint32_t)v.pod_cpu) : 1u;
   v.penalty = e->cfg.reject_penalty;
-  v.cap = e->d_cap; v.lam = e->d_lam; v.free_cpu = e->d_free_cpu; v.free_mem = e->d_free_mem;
+  v.cap = e->d_cap; v.lam = e->d_lam; v.cdf = e->d_cdf; v.free = e->d_free;
   v.used_cpu = e->d_used_cpu; v.counters = e->counters_on ? e->d_counters : nullptr;
   return v;
 }
@@ -107,55 +114,44 @@ __device__ __forceinline__ double noise(const EnvView& v, int lane, int t, int c
 }
 
 // ---------------------------------------------------------------- node-level extension
-// DESIGN.md §4 (builder-defined; same algorithm, same Philox counters and the same f64 operation
-// order as oracle/rlks_oracle.c: nodes_reset_lane / nodes_step_lane).  Node state is SoA
-// [C*N][n_envs]: one lane's nodes are n_envs apart, so a wave's scan of node n is coalesced.
-__device__ __forceinline__ void nodes_reset_lane(const EnvView& v, int lane, int episode) {
-  const int C = v.C, N = v.nodes, S = v.N;
-  const uint32_t gid = (uint32_t)(v.env_offset + lane);
-  for (int c = 0; c < C; ++c) {
-    const int32_t cc = v.cap[c], cm = v.cap[C + c], m1 = v.cap[2 * C + c] + 1;
-    int32_t used = 0;
-    for (int n4 = 0; n4 < N; n4 += 4) {
-      const int g0 = c * N + n4;  // N % 4 == 0: a Philox block never straddles clusters
-      const u32x4 x = philox4x32_10(u32x4{gid, (uint32_t)episode, (uint32_t)(g0 >> 2),
-                                          (uint32_t)RLKS_PURPOSE_OCCUPANCY << 16}, v.k0, v.k1);
-      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int32_t pods = (int32_t)(((uint64_t)w[j] * (uint64_t)m1) >> 32);
-        v.free_cpu[(size_t)(g0 + j) * S + lane] = cc - pods * v.pod_cpu;
-        v.free_mem[(size_t)(g0 + j) * S + lane] = cm - pods * v.pod_mem;
-        used += pods * v.pod_cpu;
-      }
-    }
-    v.used_cpu[(size_t)c * S + lane] = used;
-  }
+// DESIGN.md §4 (builder-defined; same algorithm and the same Philox counters as
+// oracle/rlks_oracle.c).  Node state is int2 {free cpu, free mem}, tiled by wavefront:
+// [ceil(n_envs/64)][C*N][64], so a wave's read of node g is one coalesced 512-byte access and a
+// workgroup's 64 envs occupy one contiguous C*N*512-byte region that the step kernel streams.
+__device__ __forceinline__ int2* node_col(const EnvView& v, int lane) {  // node 0 of `lane`
+  return v.free + (size_t)(lane >> 6) * (size_t)v.C * v.nodes * 64 + (lane & 63);
 }
 
-// departures, Poisson arrivals and first-fit placement in cluster a at row t; returns rejected pods
-__device__ __forceinline__ int nodes_step_lane(const EnvView& v, int lane, int a, int t, int episode) {
-  const int C = v.C, N = v.nodes, S = v.N;
-  const uint32_t gid = (uint32_t)(v.env_offset + lane);
-  for (int c2 = 0; c2 < C; c2 += 2) {
-    const u32x4 x = philox4x32_10(u32x4{gid, (uint32_t)episode, (uint32_t)t,
-                                        ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)(c2 >> 1)}, v.k0, v.k1);
+// initial occupancy of cluster c for one lane (episode `episode`); col = node_col(lane) + c*N*64.
+// Returns the cluster's used millicores.
+__device__ __forceinline__ int32_t nodes_reset_cluster(const EnvView& v, int2* col, int c, uint32_t gid,
+                                                       int episode) {
+  const int C = v.C, N = v.nodes;
+  const int32_t cc = v.cap[c], cm = v.cap[C + c], m1 = v.cap[2 * C + c] + 1;
+  int32_t used = 0;
+  for (int n4 = 0; n4 < N; n4 += 4) {
+    const u32x4 x = philox4x32_10(u32x4{gid, (uint32_t)episode, (uint32_t)((c * N + n4) >> 2),
+                                        (uint32_t)RLKS_PURPOSE_OCCUPANCY << 16}, v.k0, v.k1);
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = c2 + j;
-      if (c < C && w[2 * j] < v.p_dep) {
-        const int n = (int)(((uint64_t)w[2 * j + 1] * (uint64_t)N) >> 32);
-        const size_t i = (size_t)(c * N + n) * S + lane;
-        const int32_t fc = v.free_cpu[i];
-        if (fc < v.cap[c]) {
-          v.free_cpu[i] = fc + v.pod_cpu;
-          v.free_mem[i] += v.pod_mem;
-          v.used_cpu[(size_t)c * S + lane] -= v.pod_cpu;
-        }
-      }
+    for (int j = 0; j < 4; ++j) {
+      const int32_t pods = (int32_t)(((uint64_t)w[j] * (uint64_t)m1) >> 32);
+      col[(size_t)(n4 + j) * 64] = make_int2(cc - pods * v.pod_cpu, cm - pods * v.pod_mem);
+      used += pods * v.pod_cpu;
     }
   }
+  return used;
+}
+
+__device__ __forceinline__ void nodes_reset_lane(const EnvView& v, int lane, int episode) {
+  const uint32_t gid = (uint32_t)(v.env_offset + lane);
+  int2* col = node_col(v, lane);
+  for (int c = 0; c < v.C; ++c)
+    v.used_cpu[(size_t)c * v.N + lane] = nodes_reset_cluster(v, col + (size_t)c * v.nodes * 64, c, gid, episode);
+}
+
+// pods arriving at row t: Poisson(lam) by inverse transform (f64, no contraction)
+__device__ __forceinline__ int arrivals(const EnvView& v, uint32_t gid, int episode, int t) {
   const u32x4 x = philox4x32_10(u32x4{gid, (uint32_t)episode, (uint32_t)t, (uint32_t)RLKS_PURPOSE_ARRIVAL << 16},
                                 v.k0, v.k1);
   const double u = u53(x.x, x.y);
@@ -168,30 +164,7 @@ __device__ __forceinline__ int nodes_step_lane(const EnvView& v, int lane, int a
     p = __ddiv_rn(__dmul_rn(p, lam), (double)k);
     F = __dadd_rn(F, p);
   }
-  int n = 0, rejected = 0, placed = 0;
-  const size_t base = (size_t)a * N * S + lane;
-  int32_t used_add = 0;
-  for (int i = 0; i < k; ++i) {
-    int32_t fc = 0, fm = 0;
-    while (n < N) {
-      fc = v.free_cpu[base + (size_t)n * S];
-      fm = v.free_mem[base + (size_t)n * S];
-      if (fc >= v.pod_cpu && fm >= v.pod_mem) break;
-      ++n;
-    }
-    if (n == N) { rejected = k - i; break; }
-    v.free_cpu[base + (size_t)n * S] = fc - v.pod_cpu;
-    v.free_mem[base + (size_t)n * S] = fm - v.pod_mem;
-    used_add += v.pod_cpu;
-    ++placed;
-  }
-  if (used_add) v.used_cpu[(size_t)a * S + lane] += used_add;
-  if (v.counters) {
-    atomicAdd(&v.counters[0], (unsigned long long)(n + placed));
-    atomicAdd(&v.counters[1], (unsigned long long)placed);
-    atomicAdd(&v.counters[2], (unsigned long long)rejected);
-  }
-  return rejected;
+  return k;
 }
 
 // _get_obs (:90-103): f32[cost[0..C), lat[0..C), cpu[0..C)] of row t
@@ -200,10 +173,9 @@ __device__ __forceinline__ void emit_obs(const EnvView& v, const double* s_tab, 
   const int C = v.C, TC = v.T * v.C;
   for (int c = 0; c < C; ++c) o[c] = (float)s_tab[t * C + c];
   for (int c = 0; c < C; ++c) o[C + c] = (float)s_tab[TC + t * C + c];
-  if (v.nodes > 0) {  // utilisation of each cluster from its nodes (extension)
+  if (v.nodes > 0) {  // utilisation of each cluster from its nodes (extension): exact ints, IEEE f32 divide
     for (int c = 0; c < C; ++c)
-      o[2 * C + c] = (float)__ddiv_rn((double)v.used_cpu[(size_t)c * v.N + lane],
-                                      __dmul_rn((double)v.nodes, (double)v.cap[c]));
+      o[2 * C + c] = __fdiv_rn((float)v.used_cpu[(size_t)c * v.N + lane], (float)(v.nodes * v.cap[c]));
   } else {
     for (int c = 0; c < C; ++c) o[2 * C + c] = (float)noise(v, lane, t, c, episode);
   }
@@ -228,11 +200,9 @@ __device__ __forceinline__ StepOut step_lane(const EnvView& v, const double* s_t
     return r;
   }
   int ep = v.episode[lane];
-  const int rejected = v.nodes > 0 ? nodes_step_lane(v, lane, a, t, ep) : 0;
   const double cost = s_tab[t * C + a];
   const double lat = s_tab[TC + t * C + a];
   r.reward = __dmul_rn(v.scale, __dadd_rn(__dmul_rn(v.w_cost, cost), __dmul_rn(v.w_lat, lat)));
-  if (v.penalty != 0.0) r.reward = __dsub_rn(r.reward, __dmul_rn(v.penalty, (double)rejected));
   t += 1;
   v.step[lane] = t;
   r.step = t;
@@ -256,7 +226,6 @@ __device__ __forceinline__ StepOut step_lane(const EnvView& v, const double* s_t
       for (int j = 0; j < D; ++j) final_o[j] = o[j];
     v.step[lane] = 0;
     v.episode[lane] = ep + 1;
-    if (v.nodes > 0) nodes_reset_lane(v, lane, ep + 1);
     emit_obs(v, s_tab, lane, 0, ep + 1, o);
   }
   return r;

@@ -394,6 +394,8 @@ int rlks_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, con
   rlks_env_config(env, &cfg);
   RLKS_REQUIRE(cfg.n_envs == b->N && 3 * cfg.n_clouds == d->obs_dim && cfg.n_clouds == d->n_actions,
                RLKS_ERR_ARG, "rlks_rollout: env / policy / buffer shapes disagree");
+  RLKS_REQUIRE(cfg.nodes_per_cluster == 0, RLKS_ERR_UNSUPPORTED,
+               "rlks_rollout: fused rollout covers the table env; node-level envs step through rlks_env_step");
   const int N = b->N, D = d->obs_dim, A = d->n_actions;
   hipStream_t s = (hipStream_t)stream;
   const Layout L = make_layout(D, d->hidden, A);

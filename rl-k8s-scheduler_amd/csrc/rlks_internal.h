@@ -48,6 +48,25 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1
   return c;
 }
 
+// Same function with each 32x32->64 product as one v_mad_u64_u32 (the compiler splits it into
+// v_mul_lo_u32 + v_mul_hi_u32); bit-identical, measured 14% faster (tools/micro/philox_rate.hip).
+__device__ __forceinline__ uint64_t mad_u64_u32(uint32_t a, uint32_t b) {
+  uint64_t r, carry;
+  asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(carry) : "v"(a), "s"(b));
+  (void)carry;
+  return r;
+}
+
+__device__ __forceinline__ u32x4 philox4x32_10_mad(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint64_t p0 = mad_u64_u32(c.x, 0xD2511F53u), p1 = mad_u64_u32(c.z, 0xCD9E8D57u);
+    c = u32x4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
+  }
+  return c;
+}
+
 // 53-bit uniform double in [0,1): CPython genrand_res53 construction (a>>5, b>>6)
 __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
   return __dmul_rn(__dadd_rn(__dmul_rn((double)(a >> 5), 67108864.0), (double)(b >> 6)),
@@ -93,6 +112,11 @@ __device__ __forceinline__ double mt_random(uint32_t* __restrict__ mt, int strid
 
 // ----------------------------------------------------------------------------- wave helpers
 __device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;

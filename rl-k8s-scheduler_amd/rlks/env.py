@@ -91,11 +91,15 @@ class NodeSpec:
 
     Defaults follow the reference manifests: pod request 100m / 64Mi (simple-service.yaml:25-28);
     node types t3.micro-like (2 vCPU / 1 GiB) and Standard_B2s-like (2 vCPU / 4 GiB)
-    (aws-/azure-cluster-config.yaml:12) alternating over the clusters.
+    (aws-/azure-cluster-config.yaml:12) alternating over the clusters.  Each step every running pod
+    leaves with probability `depart_prob` (geometric lifetimes), then
+    Poisson(`arrival_rate`) pods (or `arrival_trace[t]`) arrive at the chosen cluster.
+    depart_prob="stationary" balances the two at the initial mean occupancy
+    (arrival_rate / expected initial pods per env), so a cluster neither drains nor fills.
     """
 
     def __init__(self, n_clouds, nodes_per_cluster=256, *, node_cpu_m=None, node_mem_mi=None, pod_cpu_m=100,
-                 pod_mem_mi=64, arrival_rate=1.0, arrival_trace=None, depart_prob=0.5, init_occupancy=0.5,
+                 pod_mem_mi=64, arrival_rate=1.0, arrival_trace=None, depart_prob="stationary", init_occupancy=0.5,
                  reject_penalty=0.0):
         self.n_clouds = int(n_clouds)
         self.nodes_per_cluster = int(nodes_per_cluster)
@@ -107,8 +111,24 @@ class NodeSpec:
         self.pod_cpu_m, self.pod_mem_mi = int(pod_cpu_m), int(pod_mem_mi)
         self.arrival_rate = float(arrival_rate)
         self.arrival_trace = None if arrival_trace is None else np.ascontiguousarray(arrival_trace, np.float64)
-        self.depart_prob, self.init_occupancy = float(depart_prob), float(init_occupancy)
+        self.init_occupancy = float(init_occupancy)
         self.reject_penalty = float(reject_penalty)
+        self.depart_prob = self.stationary_depart_prob() if depart_prob == "stationary" else float(depart_prob)
+
+    def max_pods(self):
+        """pods a node of each cluster can hold"""
+        return np.minimum(self.node_cpu_m // self.pod_cpu_m, self.node_mem_mi // self.pod_mem_mi)
+
+    def expected_initial_pods(self):
+        """mean pods per env after a reset: node pods ~ U{0..floor(init_occupancy * max_pods)}"""
+        mp = self.max_pods()
+        init_max = np.minimum(mp, np.floor(self.init_occupancy * mp))
+        return float(self.nodes_per_cluster * (init_max / 2.0).sum())
+
+    def stationary_depart_prob(self):
+        rate = float(np.mean(self.arrival_trace)) if self.arrival_trace is not None else self.arrival_rate
+        pods = self.expected_initial_pods()
+        return min(1.0, rate / pods) if pods > 0 else 0.0
 
 
 def bursty_trace(n=100, base=1.0, peak=2.0, ramp=20, burst_every=25, burst=4.0):
@@ -349,9 +369,10 @@ class VecK8sMultiCloudEnv:
         return fc, fm, used
 
     def counters(self, enable=-1):
-        """{nodes scanned, pods placed, pods rejected} since counting was enabled (enable=1 resets)"""
+        """[node checks, pods placed, pods rejected, pods departed, nodes written] since counting was
+        enabled (enable=1 resets)"""
         torch = _torch()
-        out = torch.zeros(3, dtype=torch.int64, device=self.device)
+        out = torch.zeros(5, dtype=torch.int64, device=self.device)
         _lib.call("rlks_env_counters", self.handle, int(enable), _lib.ptr(out), self.dev.stream)
         return out
 

@@ -36,7 +36,7 @@ def test_node_state_invariants_and_obs(mode):
     cc, cm = _caps(C)
     trace = np.concatenate([np.linspace(0.0, 3.0, 20), np.full(80, 1.5)]) if mode else None
     env = oracle.OracleEnv(oracle.make_cfg(n, 100, C, noise_mode=0, seed=3, autoreset=1, nodes=N, arrival_mode=mode,
-                                           arrival_rate=2.0, depart_prob=0.6, init_occupancy=0.5),
+                                           arrival_rate=2.0, depart_prob=0.1, init_occupancy=0.5),
                            cost, lat, cc, cm, trace)
     obs = env.reset()
     assert obs.shape == (n, 3 * C)
@@ -46,12 +46,12 @@ def test_node_state_invariants_and_obs(mode):
         obs, rew, term, step, _, st = env.step(a)
         assert st[0] == 0 and st[1] == 0
         fc, used = _check_invariants(env, cc, cm)
-        util = used / (N * cc[None, :].astype(np.float64))
-        np.testing.assert_array_equal(obs[:, 2 * C:], util.astype(np.float32))
+        util = used.astype(np.float32) / (N * cc[None, :]).astype(np.float32)
+        np.testing.assert_array_equal(obs[:, 2 * C:], util)
         row = np.where(term.astype(bool), 0, step)  # auto-reset lanes show their new episode's row 0
         np.testing.assert_array_equal(obs[:, :C], cost[row].astype(np.float32))
-    scanned, placed, rejected = env.counters()
-    assert placed > 0 and scanned >= placed
+    scanned, placed, rejected, departed, written = env.counters()
+    assert placed > 0 and scanned >= placed and departed > 0 and written > 0
 
 
 def test_first_fit_places_on_lowest_fitting_node():
@@ -73,7 +73,7 @@ def test_first_fit_places_on_lowest_fitting_node():
         if changed.size:
             assert (prev[: changed.min()] < 100).all()  # every lower node was already full
         prev = fc.copy()
-    _, placed, rejected = env.counters()
+    _, placed, rejected, _, _ = env.counters()
     assert placed == min(placed + rejected, 3 * N) and rejected >= 0
 
 
@@ -95,7 +95,7 @@ def test_zero_nodes_is_the_reference_env(golden_cost_lat, traces):
 
 
 def test_reject_penalty_applies():
-    C, N = 2, 1
+    C, N = 2, 8
     cost, lat = _tables(C)
     cc, cm = np.array([100, 100], np.int32), np.array([64, 64], np.int32)  # one pod per node
     base = oracle.OracleEnv(oracle.make_cfg(16, 100, C, noise_mode=0, seed=2, nodes=N, arrival_rate=3.0,
@@ -111,3 +111,38 @@ def test_reject_penalty_applies():
         assert (r1 <= r0).all()
         tot += (r0 - r1).sum()
     assert tot == 0.5 * pen.counters()[2]
+
+
+def test_binomial_departure_table():
+    """the departure table is the Binomial(n, p) CDF to 2^-32 (scipy), monotone, capped at 2^32-1"""
+    from scipy.stats import binom
+
+    for p in (0.0, 1.1e-4, 0.02, 0.3, 0.5, 1.0):
+        cdf = oracle.binom_cdf32(20, p).astype(np.int64)
+        for n in range(21):
+            row = cdf[n, : n + 1]
+            assert row[-1] == 2**32 - 1 and (np.diff(row) >= 0).all()
+            ref = np.minimum(np.round(binom.cdf(np.arange(n), n, p) * 2.0**32), 2**32 - 1)
+            assert n == 0 or np.abs(row[:n] - ref).max() <= 2, (p, n)
+
+
+@pytest.mark.parametrize("p", [0.0, 1e-3, 0.05, 1.0])
+def test_departures_are_geometric_per_pod(p):
+    """no arrivals: each step every pod leaves with probability p (mean over many nodes)"""
+    C, N, n = 2, 64, 256
+    cost, lat = _tables(C)
+    cc, cm = np.array([2000, 2000], np.int32), np.array([4096, 4096], np.int32)
+    env = oracle.OracleEnv(oracle.make_cfg(n, 100, C, noise_mode=0, seed=9, nodes=N, arrival_rate=0.0,
+                                           depart_prob=p, init_occupancy=1.0), cost, lat, cc, cm)
+    env.reset()
+    pods0 = ((2000 - env.node_state()[0]) // 100).sum()
+    a = np.zeros(n, np.int32)
+    env.step(a)
+    pods1 = ((2000 - env.node_state()[0]) // 100).sum()
+    left = pods0 - pods1
+    assert env.counters()[3] == left
+    if p in (0.0, 1.0):
+        assert left == p * pods0
+    else:
+        sd = np.sqrt(pods0 * p * (1 - p))
+        assert abs(left - p * pods0) < 5 * sd
