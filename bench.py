@@ -32,6 +32,10 @@ sys.path.insert(0, str(ROOT / "rl-k8s-scheduler_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 dense peak (MI355X_MICROARCH.md)
+F16_MFMA_PEAK_TFLOPS = 2500.0  # dense fp16/bf16 MFMA peak (MI355X_MICROARCH.md)
+# split-fp16: every fp32-accurate product is three f16 MFMA products, so the ceiling for the
+# algorithmic (fp32) FLOPs is a third of the f16 peak
+SF16_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 
 # algorithmic work per row of each SGD-step kernel (D = 6, H = 256, A = 2, both nets)
 D_, H_, A_ = 6, 256, 2
@@ -41,6 +45,11 @@ FLOPS_PER_ROW = {
     "k_fwd_head_vf": 2 * (D_ * H_ + H_ * H_ + H_) + 4 * H_,
     "k_dw2": 2 * 2 * H_ * H_,                       # dW2 = dZ2^T H1, both nets
     "k_dh1": 2 * 2 * H_ * H_ + 2 * 2 * D_ * H_,     # dH1 = dZ2 W2 and dW1 = dZ1^T X, both nets
+    # split-fp16 kernels (sgd_sf16.hip), algorithmic fp32 FLOPs per row:
+    # F1 per net = forward + head backward + dH1 = dZ2 W2 + dW1 = dZ1^T X
+    "k_sf_fwdbwd_pi": 2 * (D_ * H_ + H_ * H_ + H_ * A_) + 4 * H_ * A_ + 2 * H_ * H_ + 2 * D_ * H_,
+    "k_sf_fwdbwd_vf": 2 * (D_ * H_ + H_ * H_ + H_) + 4 * H_ + 2 * H_ * H_ + 2 * D_ * H_,
+    "k_sf_dw2": 2 * 2 * H_ * H_,                    # dW2 = dZ2^T H1, both nets
 }
 ENV_BYTES_PER_STEP = 4 + 8 + 24 + 4 + 1  # action, step r/w, obs, reward, done
 GAE_BYTES_PER_STEP = 17                  # r, V, done in; A, vtarg out
@@ -57,6 +66,7 @@ def parse():
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--precision", default="auto", choices=("auto", "sf16", "fp32"), help="SGD-step matrix arithmetic")
     return ap.parse_args()
 
 
@@ -86,15 +96,27 @@ def kernel_timing(algo, torch, reps=20):
 
     _lib.call("rlks_ppo_gather", desc, C.byref(algo.bufs), 1, 0, 0, algo.mb, algo.dyn.data_ptr(),
               algo.mbuf.data_ptr(), s.cuda_stream)
-    for name, mask in (("k_fwd_head_pi", _lib.RLKS_PHASE_FWD_PI), ("k_fwd_head_vf", _lib.RLKS_PHASE_FWD_VF),
-                       ("k_dw2", _lib.RLKS_PHASE_DW2), ("k_dh1", _lib.RLKS_PHASE_DH1),
-                       ("k_reduce", _lib.RLKS_PHASE_REDUCE)):
+    if algo.precision == "sf16":
+        phase(_lib.RLKS_PHASE_ALL)()  # weight splits + dZ2 in place for the per-phase timings
+        phases = (("k_sf_prep", _lib.RLKS_PHASE_PREP), ("k_sf_fwdbwd_pi", _lib.RLKS_PHASE_FWD_PI),
+                  ("k_sf_fwdbwd_vf", _lib.RLKS_PHASE_FWD_VF), ("k_sf_dw2", _lib.RLKS_PHASE_DW2),
+                  ("k_reduce", _lib.RLKS_PHASE_REDUCE))
+        peak, peak_name = SF16_PEAK_TFLOPS, "frac_sf16_mfma"
+    else:
+        phases = (("k_fwd_head_pi", _lib.RLKS_PHASE_FWD_PI), ("k_fwd_head_vf", _lib.RLKS_PHASE_FWD_VF),
+                  ("k_dw2", _lib.RLKS_PHASE_DW2), ("k_dh1", _lib.RLKS_PHASE_DH1), ("k_reduce", _lib.RLKS_PHASE_REDUCE))
+        peak, peak_name = FP32_MFMA_PEAK_TFLOPS, "frac_fp32_mfma"
+    for name, mask in phases:
         ms = timed(phase(mask))
         rec = {"ms": ms}
         if name in FLOPS_PER_ROW:
             tf = FLOPS_PER_ROW[name] * algo.mb / (ms * 1e-3) / 1e12
-            rec.update({"tflops": tf, "frac_fp32_mfma": tf / FP32_MFMA_PEAK_TFLOPS})
+            rec.update({"tflops": tf, peak_name: tf / peak, "frac_fp32_mfma_peak": tf / FP32_MFMA_PEAK_TFLOPS})
         out[name] = rec
+    ms = timed(lambda: _lib.call("rlks_ppo_grad", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(),
+                                 algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None,
+                                 algo.ws.data_ptr(), algo.ws.numel(), s.cuda_stream))
+    out["sgd_grad_total"] = {"ms": ms}
     b = algo.buf
     N, T = algo.N, algo.T
     ms = timed(lambda: _lib.call("rlks_env_sample_step", algo.env.handle, b["logits"].data_ptr(), 1,
@@ -227,7 +249,7 @@ def main():
 
     cfg = (PPOConfig().environment("K8sMultiCloudEnv").framework("torch")
            .training(train_batch_size=args.envs * args.rollout * world, sgd_minibatch_size=args.minibatch * world,
-                     num_sgd_iter=args.epochs, lr=3e-4, gamma=0.99)
+                     num_sgd_iter=args.epochs, lr=3e-4, gamma=0.99, sgd_precision=args.precision)
            .debugging(seed=42))
     cfg.num_envs = args.envs
     cfg.rollout_fragment_length = args.rollout
@@ -266,11 +288,15 @@ def main():
         if kernels:
             # the dominant kernel as rocprofv3 --stats ranks them: largest share of GPU time (each
             # runs once per SGD step, so: the longest launch)
-            dom = max(("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1"), key=lambda k: kernels[k]["ms"])
+            cands = [k for k in kernels if k in FLOPS_PER_ROW]
+            dom = max(cands, key=lambda k: kernels[k]["ms"])
             k = kernels[dom]
-            roofline = {"bound": "mfma", "kernel": dom, "achieved": k["tflops"], "peak": FP32_MFMA_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": k["tflops"] / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                        "flop_per_launch": FLOPS_PER_ROW[dom] * algo.mb, "avg_launch_ms": k["ms"]}
+            peak = SF16_PEAK_TFLOPS if algo.precision == "sf16" else FP32_MFMA_PEAK_TFLOPS
+            roofline = {"bound": "mfma", "kernel": dom, "achieved": k["tflops"], "peak": peak,
+                        "unit": "TFLOP/s", "frac": k["tflops"] / peak, "traffic": None,
+                        "flop_per_launch": FLOPS_PER_ROW[dom] * algo.mb, "avg_launch_ms": k["ms"],
+                        "peak_basis": ("split-fp16: 2.5 PF dense f16 MFMA / 3 products per fp32-accurate FLOP"
+                                       if algo.precision == "sf16" else "fp32 MFMA dense peak")}
             pmc = pmc_traffic()
             if pmc and dom in pmc:
                 roofline["traffic"] = pmc[dom]["hbm_bytes_per_launch"]
@@ -288,11 +314,11 @@ def main():
             "metric": "env-steps/sec (node), batched rollout+policy update, 1/2/4/8 GPUs; %HBM BW",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32", "data": "synthetic (env-generated rollouts, random-init FCNet)",
+            "dtype": "fp32" if algo.precision == "fp32" else "fp32 (split-fp16 MFMA, fp32-accurate)", "data": "synthetic (env-generated rollouts, random-init FCNet)",
             "config": {"workload": "c2: 4,096 envs/GPU x 2-cloud table, T=128 rollout + GAE + PPO update "
                                    "(10 epochs x 8 minibatches of 65,536 rows/GPU, FCNet [256,256] tanh)",
                        "envs_per_gpu": args.envs, "rollout_steps": args.rollout, "minibatch_per_gpu": algo.mb,
-                       "epochs": args.epochs, "global_batch": algo.samples * world,
+                       "epochs": args.epochs, "global_batch": algo.samples * world, "sgd_precision": algo.precision,
                        "parallelism": f"dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "finite": finite,
         }

@@ -180,6 +180,7 @@ int rlks_ppo_grad(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, cons
 #define RLKS_PHASE_ALL 15
 #define RLKS_PHASE_FWD_PI 16 /* F1 of the policy net only (profiling) */
 #define RLKS_PHASE_FWD_VF 32 /* F1 of the value net only (profiling) */
+#define RLKS_PHASE_PREP 64   /* split-fp16: weight split/permute (implied by RLKS_PHASE_FWD) */
 int rlks_ppo_grad_phases(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
                          const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
                          void* workspace_dev, int64_t workspace_bytes, int phases, void* stream);

@@ -62,8 +62,17 @@ typedef struct rlks_mlp_desc {
   int32_t obs_dim;   /* D  (reference: 6) */
   int32_t hidden;    /* H  (reference: fcnet_hiddens [256, 256]) */
   int32_t n_actions; /* A  (reference: 2) */
-  int32_t reserved;
+  int32_t precision; /* RLKS_PRECISION_*: how the SGD step's matrix products are computed */
 } rlks_mlp_desc;
+
+/* SGD-step matrix arithmetic.  Both meet the 1e-5 relative gradient bar against the fp64 oracle:
+ * FP32 runs v_mfma_f32_32x32x2_f32 (bitwise an fmaf chain); SF16 splits every operand into two
+ * scaled fp16 halves and accumulates three v_mfma_f32_32x32x16_f16 products in fp32 (error
+ * <= ~2^-21 per product, measured below the fp32 chain's) at 16x the fp32 matrix rate. */
+enum {
+  RLKS_PRECISION_FP32 = 0,
+  RLKS_PRECISION_SF16 = 1
+};
 
 /* PPO loss coefficients that stay fixed for a run (RLlib PPOConfig names and defaults) */
 typedef struct rlks_ppo_coeffs {

@@ -46,6 +46,30 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return ax < 0.6f ? small : __builtin_copysignf(big, x);
 }
 
+// reduce 16 per-lane values (register r <-> accumulator row) over the 32 lanes of a half-wave;
+// afterwards lane l holds the total of register ((l >> 1) & 15) (lanes l and l^1 agree)
+__device__ __forceinline__ float half_wave_reduce16(const float (&v)[16], int l) {
+  float v8[8], v4[4], v2[2];
+  {
+    const bool b = (l >> 4) & 1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v8[j] = (b ? v[j + 8] : v[j]) + __shfl_xor(b ? v[j] : v[j + 8], 16, 64);
+  }
+  {
+    const bool b = (l >> 3) & 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v4[j] = (b ? v8[j + 4] : v8[j]) + __shfl_xor(b ? v8[j] : v8[j + 4], 8, 64);
+  }
+  {
+    const bool b = (l >> 2) & 1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) v2[j] = (b ? v4[j + 2] : v4[j]) + __shfl_xor(b ? v4[j] : v4[j + 2], 4, 64);
+  }
+  const bool b = (l >> 1) & 1;
+  float v1 = (b ? v2[1] : v2[0]) + __shfl_xor(b ? v2[0] : v2[1], 2, 64);
+  return v1 + __shfl_xor(v1, 1, 64);
+}
+
 // ----------------------------------------------------------------------------- layout
 struct Layout {
   int64_t off[RLKS_N_TENSORS];

@@ -7,7 +7,7 @@
 // from /root/reference: the restated semantics are pinned against oracle/oracle.py.
 #include <cmath>
 
-#include "mlp_common.h"
+#include "sgd_sf16.h"
 
 namespace rlks {
 
@@ -220,12 +220,65 @@ static Ws ws_layout(int D, int A, int M, char* base) {
   return w;
 }
 
+// split-fp16 path: pre-split weights, dZ2^T, per-F1-block and per-F2-split partials
+struct SfWs {
+  SfNetW w[2];
+  SfNet n[2];
+  double* stat64;
+  int64_t bytes;
+  int blocks, splits, tiles_per_split;
+};
+
+static SfWs sf_ws_layout(int D, int A, int M, char* base) {
+  SfWs w{};
+  const int KD = sf_kd(D), tiles = M / 32;
+  w.blocks = M / 256;
+  w.splits = 1;
+  while (w.splits * 2 <= 128 && tiles % (w.splits * 2) == 0) w.splits *= 2;
+  w.tiles_per_split = tiles / w.splits;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    char* p = base ? base + o : nullptr;
+    o += (bytes + 255) / 256 * 256;
+    return p;
+  };
+  for (int net = 0; net < 2; ++net) {
+    const int An = net == 0 ? A : 1;
+    SfNetW& W = w.w[net];
+    SfNet& n = w.n[net];
+    W.w1h = (_Float16*)take(2LL * HID * KD);
+    W.w1l = (_Float16*)take(2LL * HID * KD);
+    W.w2ph = (_Float16*)take(2LL * HID * HID);
+    W.w2pl = (_Float16*)take(2LL * HID * HID);
+    W.w2th = (_Float16*)take(2LL * HID * HID);
+    W.w2tl = (_Float16*)take(2LL * HID * HID);
+    W.sc = (float*)take(4 * 8);
+    W.pmax = (float*)take(4 * 32);
+    W.dzmax = (unsigned*)take(4);
+    n.w1h = W.w1h; n.w1l = W.w1l; n.w2ph = W.w2ph; n.w2pl = W.w2pl; n.w2th = W.w2th; n.w2tl = W.w2tl;
+    n.sc = W.sc; n.dzmax = W.dzmax;
+    n.dz2t = (float*)take(4LL * M * HID);
+    n.part_w1 = (float*)take(4LL * w.blocks * HID * D);
+    n.part_b1 = (float*)take(4LL * w.blocks * HID);
+    n.part_w3 = (float*)take(4LL * tiles * An * HID);
+    n.part_b3 = (float*)take(4LL * tiles * An);
+    n.part_stat = (float*)take(4LL * tiles * 4);
+    n.part_w2 = (float*)take(4LL * w.splits * HID * HID);
+    n.part_b2 = (float*)take(4LL * w.splits * HID);
+  }
+  w.stat64 = (double*)take(8 * 8);
+  w.bytes = o;
+  return w;
+}
+
 static int check_desc(const rlks_mlp_desc* d) {
   RLKS_REQUIRE(d, RLKS_ERR_ARG, "null mlp desc");
   RLKS_REQUIRE(d->obs_dim > 0 && d->obs_dim <= DMAX, RLKS_ERR_UNSUPPORTED, "obs_dim must be in [1, 32]");
   RLKS_REQUIRE(d->n_actions == 2 || d->n_actions == 4 || d->n_actions == 8, RLKS_ERR_UNSUPPORTED,
                "n_actions must be 2, 4 or 8");
   RLKS_REQUIRE(d->hidden == HID, RLKS_ERR_UNSUPPORTED, "fused MLP kernels are built for hidden = 256");
+  RLKS_REQUIRE(d->precision == RLKS_PRECISION_FP32 || d->precision == RLKS_PRECISION_SF16, RLKS_ERR_ARG,
+               "unknown precision");
   return RLKS_OK;
 }
 
@@ -288,9 +341,73 @@ int rlks_ppo_gather(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, uint64_t
 
 int rlks_ppo_workspace_bytes(const rlks_mlp_desc* d, int rows, int64_t* bytes) {
   if (int rc = check_desc(d)) return rc;
+  if (d->precision == RLKS_PRECISION_SF16) {
+    RLKS_REQUIRE(bytes && rows > 0 && rows % 256 == 0, RLKS_ERR_ARG,
+                 "rlks_ppo_workspace_bytes: split-fp16 rows must be a positive multiple of 256");
+    *bytes = sf_ws_layout(d->obs_dim, d->n_actions, rows, nullptr).bytes;
+    return RLKS_OK;
+  }
   RLKS_REQUIRE(bytes && rows > 0 && rows % GB == 0, RLKS_ERR_ARG,
                "rlks_ppo_workspace_bytes: rows must be a positive multiple of 128");
   *bytes = ws_layout(d->obs_dim, d->n_actions, rows, nullptr).bytes;
+  return RLKS_OK;
+}
+
+static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
+                   const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes, int phases,
+                   hipStream_t s) {
+  RLKS_REQUIRE(M > 0 && M % 256 == 0, RLKS_ERR_ARG, "rlks_ppo_grad: split-fp16 rows must be a positive multiple of 256");
+  const int D = d->obs_dim, A = d->n_actions, H = HID;
+  const SfWs w = sf_ws_layout(D, A, M, (char*)workspace);
+  RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_ppo_grad: workspace too small");
+  const Layout L = make_layout(D, H, A);
+  const bool f_pi = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_PI), f_vf = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_VF);
+  if (phases & (RLKS_PHASE_FWD | RLKS_PHASE_PREP)) {
+    SfPrepArgs pa{};
+    pa.D = D;
+    pa.KD = sf_kd(D);
+    for (int net = 0; net < 2; ++net) {
+      pa.n[net] = w.w[net];
+      const NetPtrs P = net_ptrs_host(params, L, net);
+      pa.n[net].w1 = P.w1; pa.n[net].b1 = P.b1; pa.n[net].w2 = P.w2;
+    }
+    if (int rc = launch_sf_prep(pa, s)) return rc;
+  }
+  SfArgs a{};
+  a.x = mb; a.x_stride = mb_stride(D, A); a.M = M; a.D = D; a.A_pi = A;
+  a.tiles_per_split = w.tiles_per_split; a.co = *co; a.dyn = dyn;
+  for (int net = 0; net < 2; ++net) {
+    a.n[net] = w.n[net];
+    const NetPtrs P = net_ptrs_host(params, L, net);
+    a.n[net].b2 = P.b2; a.n[net].w3 = P.w3; a.n[net].b3 = P.b3;
+  }
+  // F1 (forward, loss, dZ2, dH1 -> dW1 / db1, dW3 / db3) per net; F2 (dW2, db2) for both
+  if (f_pi)
+    if (int rc = launch_sf_f1(a, 0, A, s)) return rc;
+  if (f_vf)
+    if (int rc = launch_sf_f1(a, 1, A, s)) return rc;
+  if (phases & RLKS_PHASE_DW2)
+    if (int rc = launch_sf_dw2(a, w.splits, s)) return rc;
+  if (!(phases & RLKS_PHASE_REDUCE)) return RLKS_OK;
+  Reducer R;
+  for (int net = 0; net < 2; ++net) {
+    const int An = net == 0 ? A : 1;
+    const int64_t* o = L.off + 6 * net;
+    const SfNet& n = w.n[net];
+    R.add(n.part_w1, grad + o[0], nullptr, (int64_t)H * D, w.blocks, H * D);
+    R.add(n.part_b1, grad + o[1], nullptr, H, w.blocks, H);
+    R.add(n.part_w2, grad + o[2], nullptr, (int64_t)H * H, w.splits, H * H);
+    R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
+    R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, M / 32, An * H);
+    R.add(n.part_b3, grad + o[5], nullptr, An, M / 32, An);
+    if (stats) R.add(n.part_stat, nullptr, w.stat64 + 4 * net, 4, M / 32, 4);
+  }
+  hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
+  RLKS_LAUNCHED();
+  if (stats) {
+    hipLaunchKernelGGL(k_stats_finish, dim3(1), dim3(64), 0, s, stats, w.stat64, w.stat64 + 4, M);
+    RLKS_LAUNCHED();
+  }
   return RLKS_OK;
 }
 
@@ -298,6 +415,10 @@ int rlks_ppo_grad_phases(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, cons
                          const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes,
                          int phases, void* stream) {
   if (int rc = check_desc(d)) return rc;
+  if (d->precision == RLKS_PRECISION_SF16) {
+    RLKS_REQUIRE(co && params && dyn && mb && grad && workspace, RLKS_ERR_ARG, "rlks_ppo_grad: null argument");
+    return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, phases, (hipStream_t)stream);
+  }
   RLKS_REQUIRE(co && params && dyn && mb && grad && workspace, RLKS_ERR_ARG, "rlks_ppo_grad: null argument");
   RLKS_REQUIRE(M > 0 && M % GB == 0, RLKS_ERR_ARG, "rlks_ppo_grad: rows must be a positive multiple of 128");
   const int D = d->obs_dim, A = d->n_actions, H = HID;

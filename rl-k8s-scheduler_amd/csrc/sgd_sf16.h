@@ -1,0 +1,45 @@
+// sgd_sf16.h — argument blocks and launchers of the split-fp16 SGD-step kernels (sgd_sf16.hip).
+#pragma once
+
+#include "mlp_common.h"
+
+namespace rlks {
+
+struct SfNetW {
+  const float *w1, *b1, *w2;
+  _Float16 *w1h, *w1l, *w2ph, *w2pl, *w2th, *w2tl;
+  float* sc;          // [8]: s_w1, 1/s_w1, s_w2, 1/s_w2, e_w1, e_w2
+  float* pmax;        // [32] per-block max |w| (16 over W2, 16 over W1a)
+  unsigned* dzmax;    // zeroed here (F1 atomicMax)
+};
+struct SfPrepArgs {
+  SfNetW n[2];
+  int D, KD;
+};
+
+struct SfNet {
+  const float *b2, *w3, *b3;
+  const _Float16 *w1h, *w1l, *w2ph, *w2pl, *w2th, *w2tl;
+  const float* sc;
+  unsigned* dzmax;
+  float* dz2t;  // [M/32][HID][32]
+  float *part_w1, *part_b1;                 // [F1 blocks][...]
+  float *part_w3, *part_b3, *part_stat;     // [tiles of 32 rows][...]
+  float *part_w2, *part_b2;                                   // [splits][...]
+};
+struct SfArgs {
+  SfNet n[2];
+  const float* x;
+  int x_stride, M, D, A_pi;
+  int tiles_per_split;
+  rlks_ppo_coeffs co;
+  const float* dyn;
+};
+
+size_t sf_f1_lds_bytes(int A_, int NG);
+int sf_kd(int D);
+int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
+int launch_sf_f1(const SfArgs& a, int net, int A, hipStream_t s);  // needs M % 256 == 0
+int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
+
+}  // namespace rlks

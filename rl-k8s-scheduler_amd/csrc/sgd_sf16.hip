@@ -1,0 +1,730 @@
+// sgd_sf16.hip — the PPO SGD step (K4) on split-fp16 MFMA: fp32-accurate products at 16x the
+// fp32 matrix rate.
+//
+// Every GEMM operand x is carried as a pair of fp16 values (hi, lo) of x * 2^e, with 2^e a power
+// of two chosen from max|x| so that the scaled values sit in [2^14, 2^15): hi = fp16(x 2^e),
+// lo = fp16(x 2^e - hi), |x 2^e - hi - lo| <= 2^-22 |x 2^e|.  A product a.b is accumulated by three
+// v_mfma_f32_32x32x16_f16 (lo.hi + hi.lo + hi.hi, fp32 accumulate); the dropped lo.lo term is
+// <= 2^-22 |a b|.  Measured on MI355X (tools/micro/sf16_layout.hip, K = 256): 1.9e-7 relative
+// error vs fp64, against 2.8e-7 for an fp32 fmaf chain.  Three f16 MFMAs cost 96 cycles per
+// 32x32x16 block, where the same work on v_mfma_f32_32x32x2_f32 takes 512.
+//
+// Orientation.  An MFMA accumulator tile X (columns on lanes, rows in registers) is the next
+// MFMA's B operand without data movement when the next product sums over X's rows (Y = A X), or
+// its A operand (Z = X^T B); the other operand is then read in X's row order perm(s, h, j)
+// (cdna_hip_programming.md §3).  Weights are pre-split by k_sf_prep into those orders, so:
+//   F1 (k_sf_fwdbwd, one wave per 32-row tile, hidden units in registers, rows on lanes)
+//     Z1^T = W1a Xa^T          Xa = [X | 1]: b1 folded into W1a's column D
+//     Z2^T = W2 H1^T           B = H1^T straight from the tanh'd accumulator
+//     H2^T, head (in-register sums over hidden units), PPO loss -> dlogits, dZ2^T
+//     dW3 (half-wave reduce), db3, stats; dZ2^T -> HBM for F2; per-tile max|dZ2| -> atomicMax
+//     dH1 = dZ2 W2             A = dZ2^T accumulator (transposes to rows-in-registers)
+//     Z1 = Xa W1a^T, dZ1 = dH1 (1 - H1^2)
+//     dW1a^T = Xa^T dZ1        B = dZ1 accumulator; row D of dW1a is db1
+//   F2 (k_sf_dw2): dW2 = dZ2^T H1 over the rows, H1 recomputed (rows in registers) as the B
+//     operand, dZ2^T tiles staged through LDS pre-split with the global max|dZ2| scale; db2 from
+//     the same loads.  Row splits write fp32 partials, summed in a fixed order by k_reduce.
+//
+// Reference semantics: RLlib FCNet [256, 256] tanh, vf_share_layers=False, PPO loss as in
+// mlp_fwd.hip (train_ppo.py:9-31; RLlib third-party).
+#include <cmath>
+
+#include "sgd_sf16.h"
+
+namespace rlks {
+
+using h8 = __attribute__((ext_vector_type(8))) _Float16;
+using h4 = __attribute__((ext_vector_type(4))) _Float16;
+
+constexpr int SF_W = 8;             // waves per F1 / F2 workgroup
+constexpr int SF_ROWS = 32 * SF_W;  // minibatch rows per F1 workgroup
+constexpr int SF_CH = 8192;         // halves per staged chunk (per hi / lo array)
+constexpr float SF_H1_SCALE = 16384.f;  // tanh outputs (|h| < 1) scaled by 2^14
+
+__device__ __forceinline__ int sf_perm(int s, int h, int j) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
+
+__device__ __forceinline__ f32x16 mma(h8 a, h8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+// (ah + al)(bh + bl) - al bl, small terms first
+__device__ __forceinline__ f32x16 mma3(h8 ah, h8 al, h8 bh, h8 bl, f32x16 c) {
+  c = mma(al, bh, c);
+  c = mma(ah, bl, c);
+  return mma(ah, bh, c);
+}
+
+__device__ __forceinline__ void split1(float x, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+// elements [o, o + 8) of v, times s
+template <int N>
+__device__ __forceinline__ void split8(const float (&v)[N], int o, float s, h8& hi, h8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    _Float16 a, b;
+    split1(v[o + j] * s, a, b);
+    hi[j] = a;
+    lo[j] = b;
+  }
+}
+__device__ __forceinline__ void split16(const f32x16& v, int o, float s, h8& hi, h8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    _Float16 a, b;
+    split1(v[o + j] * s, a, b);
+    hi[j] = a;
+    lo[j] = b;
+  }
+}
+
+// exponent e with mx 2^e in [2^14, 2^15); 0 for mx = 0 / non-finite
+__device__ __forceinline__ int sf_exp(float mx) {
+  if (!(mx > 0.f) || !(mx <= 3.4e38f)) return 0;
+  int e;
+  (void)frexpf(mx, &e);
+  return min(max(15 - e, -120), 120);
+}
+__device__ __forceinline__ float pow2(int e) { return ldexpf(1.f, e); }
+
+// 1 - 2 / (exp(2x) + 1): 5 VALU ops (2 transcendental); absolute error ~1e-7, which is what the
+// split products see (|h| < 1 carried at a fixed 2^14 scale)
+__device__ __forceinline__ float tanh_abs(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.885390081777927f);
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ----------------------------------------------------------------------------- weight prep
+// W1a = [W1 | b1] -> w1h/w1l [HID][KD]; W2 -> w2p (A operand of Z2^T = W2 H1^T: row n, k in perm
+// order per 32-block) and w2t (B operand of dH1 = dZ2 W2: row k, n in perm order per 32-block),
+// each with its own power-of-two scale from max |w|.
+// pass 1: per-block max |w| (16 blocks over W2, 16 over W1a) -> pmax[net][32]
+__global__ __launch_bounds__(256) void k_sf_wmax(SfPrepArgs g) {
+  __shared__ float red[256];
+  const SfNetW& N = g.n[blockIdx.x];
+  const int b = blockIdx.y, tid = threadIdx.x, D = g.D;
+  float mx = 0.f;
+  if (b < 16) {
+    for (int e = b * 4096 + tid; e < (b + 1) * 4096; e += 256) mx = fmaxf(mx, fabsf(N.w2[e]));
+  } else {
+    const int n = HID * (D + 1), per = (n + 15) / 16, e0 = (b - 16) * per, e1 = min(n, e0 + per);
+    for (int e = e0 + tid; e < e1; e += 256) {
+      const int k = e / (D + 1), d = e - k * (D + 1);
+      mx = fmaxf(mx, fabsf(d < D ? N.w1[k * D + d] : N.b1[k]));
+    }
+  }
+  red[tid] = mx;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
+    __syncthreads();
+  }
+  if (tid == 0) N.pmax[b] = red[0];
+}
+
+// pass 2: grid (2 nets, 64 blocks) x 256 threads, 4 elements of W2 (both orders) per thread and
+// the W1a split in the first blocks
+__global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
+  const SfNetW& N = g.n[blockIdx.x];
+  const int D = g.D, KD = g.KD, tid = threadIdx.x;
+  float m2 = 0.f, m1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    m2 = fmaxf(m2, N.pmax[i]);
+    m1 = fmaxf(m1, N.pmax[16 + i]);
+  }
+  const int e1 = sf_exp(m1), e2 = sf_exp(m2);
+  const float s1 = pow2(e1), s2 = pow2(e2);
+  const int base = blockIdx.y * 1024;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = base + j * 256 + tid;
+    const int row = i >> 8, c = i & 255, blk = c >> 5, rem = c & 31;
+    const int src = 32 * blk + sf_perm(rem >> 4, (rem >> 3) & 1, rem & 7);
+    _Float16 a, b;
+    split1(N.w2[row * HID + src] * s2, a, b);  // w2p[n = row][k perm]
+    N.w2ph[i] = a;
+    N.w2pl[i] = b;
+    split1(N.w2[src * HID + row] * s2, a, b);  // w2t[k = row][n perm]
+    N.w2th[i] = a;
+    N.w2tl[i] = b;
+    if (i < HID * KD) {
+      const int k = i / KD, d = i - k * KD;
+      const float v = d < D ? N.w1[k * D + d] : (d == D ? N.b1[k] : 0.f);
+      split1(v * s1, a, b);
+      N.w1h[i] = a;
+      N.w1l[i] = b;
+    }
+  }
+  if (blockIdx.y == 0 && tid == 0) {
+    N.sc[0] = s1; N.sc[1] = 1.f / s1; N.sc[4] = (float)e1;
+    N.sc[2] = s2; N.sc[3] = 1.f / s2; N.sc[5] = (float)e2;
+    *N.dzmax = 0u;
+  }
+}
+
+// ----------------------------------------------------------------------------- F1
+// Weight chunks staged by LDS-DMA (global_load_lds_dwordx4: each lane's 16 bytes land at
+// base + 16 * lane, so the swizzle is applied on the global side).  Chunk c < 8: w2p columns
+// [32c, 32c+32) of all 256 rows (Z2 loop); c >= 8: w2t rows [32(c-8), +32) (dH1 loop).  A chunk
+// is 2 x 1024 slots of 16 B (hi, lo); wave w issues slot blocks 4w .. 4w+3 of 64.
+__device__ __forceinline__ void chunk_dma(const SfNet& N, _Float16* buf, int c, int w, int l) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = 4 * w + i, arr = blk >> 4, sig = (blk & 15) * 64 + l;
+    const _Float16* src;
+    if (c < 8) {
+      const int n = sig >> 2, pc = (sig & 3) ^ ((n >> 2) & 3);
+      src = (arr ? N.w2pl : N.w2ph) + n * HID + 32 * c + 8 * pc;
+    } else {
+      const int k = sig >> 5, pc = (sig & 31) ^ (k & 15);
+      src = (arr ? N.w2tl : N.w2th) + (32 * (c - 8) + k) * HID + 8 * pc;
+    }
+    _Float16* dst = buf + arr * SF_CH + (blk & 15) * 64 * 8;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int A_, int NET, int KD, int NG>
+__global__ __launch_bounds__(512) void k_sf_fwdbwd(SfArgs g) {
+  constexpr int KS = KD / 16;   // k-steps of the first layer
+  // NG: accumulator row groups (8 rows each) holding the rows d <= D of dW1a^T.  NG = 1 (D < 8,
+  // the reference's 2-cloud obs) accumulates dW1a^T in LDS; wider obs keep it in registers.
+  constexpr bool DW1_LDS = NG == 1;
+  const SfNet& N = g.n[NET];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  _Float16* sCh = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][SF_CH]  (64 KB)
+  float* sB2 = lds + 2 * SF_CH;                      // [HID]
+  float* sW3 = sB2 + HID;                            // [A_][HID]
+  float* sDW = sW3 + A_ * HID;                       // DW1_LDS: [SF_W][HID k][8 d]  (64 KB)
+
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int D = g.D, stride = g.x_stride;
+  const int tile = blockIdx.x * SF_W + w, row0 = tile * 32;
+
+  chunk_dma(N, sCh, 0, w, l);
+  for (int i = tid; i < HID; i += 512) sB2[i] = N.b2[i];
+  for (int i = tid; i < A_ * HID; i += 512) sW3[i] = N.w3[i];
+
+  // ---- this wave's rows: Xa = [X | 1 | 0] fragments, lane row m = r, d = 16ks + 8h + j
+  float xv[KS * 8];
+  const float* xr = g.x + (size_t)(row0 + r) * stride;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 16 * ks + 8 * h + j;
+      xv[ks * 8 + j] = d < D ? xr[d] : (d == D ? 1.f : 0.f);
+    }
+  float xm = 0.f;
+#pragma unroll
+  for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
+  const int ex = sf_exp(wave_max(xm));
+  const float sx = pow2(ex);
+  h8 xh[KS], xl[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) split8(xv, ks * 8, sx, xh[ks], xl[ks]);
+  const float inv_w1 = N.sc[1], inv_w2 = N.sc[3];
+  const int e_w2 = (int)N.sc[5];
+  const float inv_z1 = inv_w1 / sx;  // Z1 accumulators carry s_x s_w1
+
+  // W1a fragments (row / column k = 32 kt + r), prefetched one k-tile ahead
+  h8 wh[KS], wl[KS], nwh[KS], nwl[KS];
+  auto w1_load = [&](int kt, h8 (&dh)[KS], h8 (&dl_)[KS]) {
+    const int k = 32 * kt + r;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      dh[ks] = *reinterpret_cast<const h8*>(N.w1h + k * KD + 16 * ks + 8 * h);
+      dl_[ks] = *reinterpret_cast<const h8*>(N.w1l + k * KD + 16 * ks + 8 * h);
+    }
+  };
+  w1_load(0, wh, wl);
+  vm_drain();
+  __syncthreads();
+
+  // ---- Z2^T = W2 H1^T over 8 k-tiles; H1^T tile kt recomputed from Xa just before its use
+  f32x16 acc[8];
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
+  for (int c = 0; c < 8; ++c) {
+    const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
+    chunk_dma(N, sCh + ((c + 1) & 1) * 2 * SF_CH, c + 1, w, l);
+    w1_load((c + 1) & 7, nwh, nwl);
+    h8 bh[2], bl[2];
+    {
+      f32x16 z;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) z = mma3(wh[ks], wl[ks], xh[ks], xl[ks], z);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
+      split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
+      split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      const int n = 32 * nt + r;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int off = n * 32 + 8 * ((2 * s + h) ^ ((n >> 2) & 3));
+        const h8 ah = *reinterpret_cast<const h8*>(buf + off);
+        const h8 al = *reinterpret_cast<const h8*>(buf + SF_CH + off);
+        acc[nt] = mma3(ah, al, bh[s], bl[s], acc[nt]);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) { wh[ks] = nwh[ks]; wl[ks] = nwl[ks]; }
+    vm_drain();
+    __syncthreads();
+  }
+
+  // ---- H2^T = tanh(Z2^T + b2), head out[a] = b3 + sum_n W3[a][n] H2[n]
+  const float inv_z2 = inv_w2 / SF_H1_SCALE;
+  float out[A_];
+#pragma unroll
+  for (int a = 0; a < A_; ++a) out[a] = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int n0 = 32 * nt + 8 * gq + 4 * h;
+      const float4 bb = *reinterpret_cast<const float4*>(sB2 + n0);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+      float wv[A_][4];
+#pragma unroll
+      for (int a = 0; a < A_; ++a) {
+        const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
+        wv[a][0] = t.x; wv[a][1] = t.y; wv[a][2] = t.z; wv[a][3] = t.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = 4 * gq + i;
+        const float h2 = tanh_abs(fmaf(acc[nt][q], inv_z2, bv[i]));
+        acc[nt][q] = h2;
+#pragma unroll
+        for (int a = 0; a < A_; ++a) out[a] = fmaf(h2, wv[a][i], out[a]);
+      }
+    }
+#pragma unroll
+  for (int a = 0; a < A_; ++a) out[a] += __shfl_xor(out[a], 32, 64) + N.b3[a];
+
+  // ---- PPO loss for row m = row0 + r (both half-waves compute it; stats from h = 0)
+  float dl[A_];
+  float st_pl = 0.f, st_vf = 0.f, st_kl = 0.f, st_ent = 0.f;
+  {
+    const float* rec = g.x + (size_t)(row0 + r) * stride;
+    const float inv_count = g.dyn[RLKS_DYN_INV_COUNT];
+    const int Ap = g.A_pi;
+    if (NET == 0) {
+      const float* lo = rec + D;
+      const float adv = (rec[D + Ap] - g.dyn[RLKS_DYN_ADV_MEAN]) * g.dyn[RLKS_DYN_ADV_INVSTD];
+      const float logp_old = rec[D + Ap + 2];
+      const int act = (int)rec[D + Ap + 3];
+      float mx = out[0], mo = lo[0];
+#pragma unroll
+      for (int a = 1; a < A_; ++a) { mx = fmaxf(mx, out[a]); mo = fmaxf(mo, lo[a]); }
+      float se = 0.f, so = 0.f;
+#pragma unroll
+      for (int a = 0; a < A_; ++a) { se += expf(out[a] - mx); so += expf(lo[a] - mo); }
+      const float lse = mx + logf(se), lso = mo + logf(so);
+      float p[A_], lp[A_], po[A_];
+      float kl = 0.f, ent = 0.f, lpa = 0.f;
+#pragma unroll
+      for (int a = 0; a < A_; ++a) {
+        lp[a] = out[a] - lse;
+        p[a] = expf(lp[a]);
+        const float lpo = lo[a] - lso;
+        po[a] = expf(lpo);
+        kl += po[a] * (lpo - lp[a]);
+        ent -= p[a] * lp[a];
+        lpa = (a == act) ? lp[a] : lpa;
+      }
+      const float ratio = expf(lpa - logp_old);
+      const float lo_c = 1.f - g.co.clip_param, hi_c = 1.f + g.co.clip_param;
+      const float rc = fminf(fmaxf(ratio, lo_c), hi_c);
+      const float s1 = adv * ratio, s2 = adv * rc;
+      // torch.min backward splits ties evenly; torch.clamp passes the gradient on [lo, hi]
+      const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+      const float inr = (ratio >= lo_c && ratio <= hi_c) ? 1.f : 0.f;
+      const float dr = -adv * (w1 + (1.f - w1) * inr) * ratio;
+      const float klc = g.dyn[RLKS_DYN_KL_COEFF];
+#pragma unroll
+      for (int a = 0; a < A_; ++a) {
+        float d = dr * ((a == act ? 1.f : 0.f) - p[a]);
+        d += klc * (p[a] - po[a]);
+        d += g.co.entropy_coeff * p[a] * (lp[a] + ent);
+        dl[a] = d * inv_count;
+      }
+      st_pl = -fminf(s1, s2);
+      st_kl = kl;
+      st_ent = ent;
+    } else {
+      const float diff = out[0] - rec[D + Ap + 1];
+      const float sq = diff * diff;
+      st_vf = fminf(sq, g.co.vf_clip_param);
+      dl[0] = (sq <= g.co.vf_clip_param) ? g.co.vf_loss_coeff * 2.f * diff * inv_count : 0.f;
+    }
+  }
+
+  // ---- per-tile partials straight to HBM: dW3[a][n] = sum_m dl[m][a] H2[m][n] (half-wave
+  // reduce), db3, loss stats
+#pragma unroll
+  for (int a = 0; a < A_; ++a)
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = dl[a] * acc[nt][q];
+      const float t = half_wave_reduce16(v, l);
+      if ((l & 1) == 0) N.part_w3[((size_t)tile * A_ + a) * HID + 32 * nt + acc_row((l >> 1) & 15, l)] = t;
+    }
+  {
+    float sv[A_ + 4];
+#pragma unroll
+    for (int a = 0; a < A_; ++a) sv[a] = h ? 0.f : dl[a];
+    sv[A_] = h ? 0.f : st_pl; sv[A_ + 1] = h ? 0.f : st_vf; sv[A_ + 2] = h ? 0.f : st_kl; sv[A_ + 3] = h ? 0.f : st_ent;
+#pragma unroll
+    for (int i = 0; i < A_ + 4; ++i) {
+      const float t = wave_sum(sv[i]);
+      if (l == 0) {
+        if (i < A_) N.part_b3[(size_t)tile * A_ + i] = t;
+        else N.part_stat[(size_t)tile * 4 + i - A_] = t;
+      }
+    }
+  }
+
+  // ---- dZ2^T = (dl W3) (1 - H2^2): to HBM (F2), tile max |dZ2| (this wave's split + F2's scale)
+  float dmx = 0.f;
+  {
+    float* dst = N.dz2t + (size_t)tile * HID * 32 + r;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int n0 = 32 * nt + 8 * gq + 4 * h;
+        float wv[A_][4];
+#pragma unroll
+        for (int a = 0; a < A_; ++a) {
+          const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
+          wv[a][0] = t.x; wv[a][1] = t.y; wv[a][2] = t.z; wv[a][3] = t.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = 4 * gq + i;
+          float gsum = 0.f;
+#pragma unroll
+          for (int a = 0; a < A_; ++a) gsum = fmaf(dl[a], wv[a][i], gsum);
+          const float h2 = acc[nt][q];
+          const float dz = gsum * (1.f - h2 * h2);
+          acc[nt][q] = dz;
+          dmx = fmaxf(dmx, fabsf(dz));
+          dst[(size_t)(n0 + i) * 32] = dz;
+        }
+      }
+  }
+  dmx = wave_max(dmx);
+  if (l == 0) atomicMax(N.dzmax, __float_as_uint(dmx));
+  const int edz = sf_exp(dmx);
+  h8 dzh[8][2], dzl[8][2];
+  {
+    const float sdz = pow2(edz);
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      split16(acc[nt], 0, sdz, dzh[nt][0], dzl[nt][0]);
+      split16(acc[nt], 8, sdz, dzh[nt][1], dzl[nt][1]);
+    }
+  }
+  // Xa^T fragments of dW1a^T = Xa^T dZ1: lane row d = r, m = perm(s, h, j)
+  h8 xth[2], xtl[2];
+  {
+    float t[16];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = sf_perm(s, h, j);
+        t[s * 8 + j] = r < D ? g.x[(size_t)(row0 + m) * stride + r] : (r == D ? 1.f : 0.f);
+      }
+    split8(t, 0, sx, xth[0], xtl[0]);
+    split8(t, 8, sx, xth[1], xtl[1]);
+  }
+
+  // ---- dH1 = dZ2 W2 per 32-column k-tile; dZ1 = dH1 (1 - H1^2); dW1a^T = Xa^T dZ1
+  // dZ1 enters the split at 2^(e_dz + e_w2 - 23): |dH1 2^(e_dz + e_w2)| <= 256 2^15 2^15
+  float dw1[DW1_LDS ? 1 : 8][4 * NG];
+  const float sz1 = pow2(-23);
+  const float u1 = pow2(23 - ex - edz - e_w2);
+  for (int c = 8; c < 16; ++c) {
+    const int kt = c - 8;
+    const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
+    if (c + 1 < 16) chunk_dma(N, sCh + ((c + 1) & 1) * 2 * SF_CH, c + 1, w, l);
+    if (c + 1 < 16) w1_load(kt + 1, nwh, nwl);
+    f32x16 d;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[q] = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int off = r * HID + 8 * ((4 * nt + 2 * s + h) ^ (r & 15));
+        const h8 bh = *reinterpret_cast<const h8*>(buf + off);
+        const h8 bl = *reinterpret_cast<const h8*>(buf + SF_CH + off);
+        d = mma3(dzh[nt][s], dzl[nt][s], bh, bl, d);
+      }
+    {
+      f32x16 z;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) z = mma3(xh[ks], xl[ks], wh[ks], wl[ks], z);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float h1 = tanh_abs(z[q] * inv_z1);
+        d[q] = d[q] * (1.f - h1 * h1);
+      }
+    }
+    h8 zh[2], zl[2];
+    split16(d, 0, sz1, zh[0], zl[0]);
+    split16(d, 8, sz1, zh[1], zl[1]);
+    f32x16 wacc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) wacc[q] = 0.f;
+    wacc = mma3(xth[0], xtl[0], zh[0], zl[0], wacc);
+    wacc = mma3(xth[1], xtl[1], zh[1], zl[1], wacc);
+    if constexpr (DW1_LDS) {
+      // rows d = 4h + 0..3 of column k: one 16-byte store into this wave's [k][8] slot
+      float4 v = {wacc[0] * u1, wacc[1] * u1, wacc[2] * u1, wacc[3] * u1};
+      *reinterpret_cast<float4*>(sDW + (w * HID + 32 * kt + r) * 8 + 4 * h) = v;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4 * NG; ++q) dw1[kt][q] = wacc[q] * u1;
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) { wh[ks] = nwh[ks]; wl[ks] = nwl[ks]; }
+    vm_drain();
+    __syncthreads();
+  }
+
+  // ---- workgroup epilogue: fixed-order sums of dW1a^T over the 8 waves -> per-block partials
+  const int blk = blockIdx.x;
+  if constexpr (DW1_LDS) {
+    const int nd = D + 1;
+    for (int e = tid; e < HID * nd; e += 512) {
+      const int k = e / nd, d = e - k * nd;
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < SF_W; ++ww) s += sDW[(ww * HID + k) * 8 + d];
+      if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
+      else N.part_b1[(size_t)blk * HID + k] = s;
+    }
+  } else {
+    float* sP = reinterpret_cast<float*>(sCh);  // [SF_W][HID][8] per pass of 8 rows
+    for (int d0 = 0; d0 <= D; d0 += 8) {
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+        for (int q = 0; q < 4 * NG; ++q) {
+          const int d = acc_row(q, l);
+          if (d >= d0 && d < d0 + 8 && d <= D) sP[(w * HID + 32 * kt + r) * 8 + (d - d0)] = dw1[kt][q];
+        }
+      __syncthreads();
+      const int nd = min(8, D + 1 - d0);
+      for (int e = tid; e < HID * nd; e += 512) {
+        const int k = e / nd, dd = e - k * nd, d = d0 + dd;
+        float s = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < SF_W; ++ww) s += sP[(ww * HID + k) * 8 + dd];
+        if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
+        else N.part_b1[(size_t)blk * HID + k] = s;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- F2
+// grid (splits, 2 nets), 512 threads; wave w owns dW2 columns k = 32w + r, all 256 rows n.
+template <int KD>
+__global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
+  constexpr int KS = KD / 16;
+  const int net = blockIdx.y;
+  const SfNet& N = g.n[net];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  _Float16* sA = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][HID n][32 m perm]
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int D = g.D, stride = g.x_stride;
+  const int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
+
+  const float mxg = __uint_as_float(*N.dzmax);
+  const int eg = sf_exp(mxg);
+  const float sg = pow2(eg);
+  const float unscale = 1.f / (sg * SF_H1_SCALE);
+  const float inv_w1 = N.sc[1];
+
+  h8 wh[KS], wl[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    wh[ks] = *reinterpret_cast<const h8*>(N.w1h + (32 * w + r) * KD + 16 * ks + 8 * h);
+    wl[ks] = *reinterpret_cast<const h8*>(N.w1l + (32 * w + r) * KD + 16 * ks + 8 * h);
+  }
+
+  float4 pv[4];
+  float db2[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      pv[i] = *reinterpret_cast<const float4*>(N.dz2t + (size_t)t * HID * 32 + (size_t)(tid + 512 * i) * 4);
+  };
+  auto store = [&](int buf) {
+    _Float16* b = sA + buf * 2 * SF_CH;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = tid + 512 * i, n = f >> 3, c = f & 7;
+      const float4 v = pv[i];
+      db2[i] += (v.x + v.y) + (v.z + v.w);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      h4 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        _Float16 a, bb;
+        split1(vv[j] * sg, a, bb);
+        hi[j] = a;
+        lo[j] = bb;
+      }
+      const int pc = 2 * (c >> 2) + (c & 1);
+      const int off = n * 32 + 8 * (pc ^ ((n >> 2) & 3)) + 4 * ((c >> 1) & 1);
+      *reinterpret_cast<h4*>(b + off) = hi;
+      *reinterpret_cast<h4*>(b + SF_CH + off) = lo;
+    }
+  };
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
+
+  load(t0);
+  store(0);
+  if (t0 + 1 < t1) load(t0 + 1);
+  __syncthreads();
+  for (int t = t0; t < t1; ++t) {
+    const int buf = (t - t0) & 1;
+    // H1 tile (rows m in registers, columns k = 32w + r on lanes) as the B operand
+    h8 bh[2], bl[2];
+    {
+      float xv[KS * 8];
+      const float* xr = g.x + (size_t)(t * 32 + r) * stride;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int d = 16 * ks + 8 * h + j;
+          xv[ks * 8 + j] = d < D ? xr[d] : (d == D ? 1.f : 0.f);
+        }
+      float xm = 0.f;
+#pragma unroll
+      for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
+      const float sx = pow2(sf_exp(wave_max(xm)));
+      f32x16 z;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        h8 a, b;
+        split8(xv, ks * 8, sx, a, b);
+        z = mma3(a, b, wh[ks], wl[ks], z);
+      }
+      const float inv_z1 = inv_w1 / sx;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
+      split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
+      split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
+    }
+    const _Float16* b = sA + buf * 2 * SF_CH;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      const int n = 32 * nt + r;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int off = n * 32 + 8 * ((2 * s + h) ^ ((n >> 2) & 3));
+        const h8 ah = *reinterpret_cast<const h8*>(b + off);
+        const h8 al = *reinterpret_cast<const h8*>(b + SF_CH + off);
+        acc[nt] = mma3(ah, al, bh[s], bl[s], acc[nt]);
+      }
+    }
+    if (t + 1 < t1) store(buf ^ 1);
+    if (t + 2 < t1) load(t + 2);
+    __syncthreads();
+  }
+  float* out = N.part_w2 + (size_t)blockIdx.x * HID * HID;
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) out[(size_t)(32 * nt + acc_row(q, l)) * HID + 32 * w + r] = acc[nt][q] * unscale;
+  // db2: the 8 threads tid & ~7 .. | 7 hold row n = (tid + 512 i) >> 3
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v = db2[i];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    if ((tid & 7) == 0) N.part_b2[(size_t)blockIdx.x * HID + ((tid + 512 * i) >> 3)] = v;
+  }
+}
+
+// ----------------------------------------------------------------------------- launchers
+size_t sf_f1_lds_bytes(int A_, int NG) {
+  return (size_t)2 * 2 * SF_CH * sizeof(_Float16) + (size_t)(HID + A_ * HID + (NG == 1 ? SF_W * HID * 8 : 0)) * sizeof(float);
+}
+
+int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_sf_wmax, dim3(2, 32), dim3(256), 0, s, a);
+  RLKS_LAUNCHED();
+  hipLaunchKernelGGL(k_sf_split, dim3(2, 64), dim3(256), 0, s, a);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+template <int A_, int KD, int NG>
+static int launch_f1_net(const SfArgs& a, int net, hipStream_t s) {
+  const dim3 grid(a.M / SF_ROWS);
+  if (net == 0) hipLaunchKernelGGL((k_sf_fwdbwd<A_, 0, KD, NG>), grid, dim3(512), sf_f1_lds_bytes(A_, NG), s, a);
+  else hipLaunchKernelGGL((k_sf_fwdbwd<1, 1, KD, NG>), grid, dim3(512), sf_f1_lds_bytes(1, NG), s, a);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+// obs_dim = 3 x clusters: C = 2, 4, 8 -> D = 6, 12, 24 (D + 1 <= 8, 16, 32)
+int sf_kd(int D) { return D + 1 <= 16 ? 16 : 32; }
+
+int launch_sf_f1(const SfArgs& a, int net, int A, hipStream_t s) {
+  RLKS_REQUIRE(a.M % SF_ROWS == 0, RLKS_ERR_ARG, "split-fp16 SGD step: rows must be a multiple of 256");
+  RLKS_REQUIRE(a.D == 3 * A, RLKS_ERR_UNSUPPORTED, "split-fp16 SGD step expects obs_dim = 3 x n_actions");
+  switch (A) {
+    case 2: return launch_f1_net<2, 16, 1>(a, net, s);
+    case 4: return launch_f1_net<4, 16, 2>(a, net, s);
+    case 8: return launch_f1_net<8, 32, 4>(a, net, s);
+    default: return fail(RLKS_ERR_UNSUPPORTED, "split-fp16 head is built for 2, 4 or 8 actions");
+  }
+}
+
+int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {
+  const size_t lds = (size_t)2 * 2 * SF_CH * sizeof(_Float16);
+  if (sf_kd(a.D) == 16) hipLaunchKernelGGL(k_sf_dw2<16>, dim3(splits, 2), dim3(512), lds, s, a);
+  else hipLaunchKernelGGL(k_sf_dw2<32>, dim3(splits, 2), dim3(512), lds, s, a);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+}  // namespace rlks

@@ -21,7 +21,8 @@ RLKS_DYN_SIZE = 8
 RLKS_DYN_ADV_MEAN, RLKS_DYN_ADV_INVSTD, RLKS_DYN_KL_COEFF, RLKS_DYN_INV_COUNT = 0, 1, 2, 3
 RLKS_STAT_SIZE = 8
 RLKS_PHASE_FWD, RLKS_PHASE_DW2, RLKS_PHASE_DH1, RLKS_PHASE_REDUCE, RLKS_PHASE_ALL = 1, 2, 4, 8, 15
-RLKS_PHASE_FWD_PI, RLKS_PHASE_FWD_VF = 16, 32
+RLKS_PHASE_FWD_PI, RLKS_PHASE_FWD_VF, RLKS_PHASE_PREP = 16, 32, 64
+RLKS_PRECISION_FP32, RLKS_PRECISION_SF16 = 0, 1
 RLKS_STAT_POLICY_LOSS, RLKS_STAT_VF_LOSS, RLKS_STAT_KL, RLKS_STAT_ENTROPY, RLKS_STAT_ROWS = 0, 1, 2, 3, 4
 
 
@@ -40,7 +41,7 @@ class EnvCfg(C.Structure):
 
 
 class MlpDesc(C.Structure):
-    _fields_ = [("obs_dim", C.c_int32), ("hidden", C.c_int32), ("n_actions", C.c_int32), ("reserved", C.c_int32)]
+    _fields_ = [("obs_dim", C.c_int32), ("hidden", C.c_int32), ("n_actions", C.c_int32), ("precision", C.c_int32)]
 
 
 class PpoCoeffs(C.Structure):

@@ -74,6 +74,10 @@ class PPOConfig:
         self.table = None
         self.adam_betas = (0.9, 0.999)
         self.adam_eps = 1e-8
+        # SGD-step matrix arithmetic (include/rlks_types.h RLKS_PRECISION_*): "sf16" = split-fp16
+        # MFMA (fp32-accurate, 16x the fp32 matrix rate; minibatch rows per rank % 256 == 0),
+        # "fp32" = fp32 MFMA; "auto" = sf16 where the minibatch allows it
+        self.sgd_precision = "auto"
 
     # ---- builder methods (names as in RLlib)
     def environment(self, env=None, env_config=None, **kw):
@@ -198,6 +202,13 @@ class PPO:
             self.env = DeviceEnv(make_cfg(self.N, table, noise=cfg.noise, seed=seed, autoreset=True,
                                           env_offset=ddp.lane_range(self.N, self.rank)[0]), table, self.device)
             self.params = PolicyParams(self.D, self.H, self.A, device=self.device, seed=seed)
+            prec = cfg.sgd_precision
+            if prec == "auto":
+                prec = "sf16" if self.mb % 256 == 0 else "fp32"
+            if prec not in ("sf16", "fp32") or (prec == "sf16" and self.mb % 256):
+                raise ValueError(f"sgd_precision {cfg.sgd_precision!r} with {self.mb} minibatch rows per rank")
+            self.precision = prec
+            self.params.desc.precision = _lib.RLKS_PRECISION_SF16 if prec == "sf16" else _lib.RLKS_PRECISION_FP32
             P = self.params.padded
             f32 = dict(dtype=torch.float32, device=self.device)
             self.adam_m = torch.zeros(P, **f32)

@@ -126,17 +126,21 @@ def _minibatch(rows, rng, D=6, A=2, p=None, d=None):
     return mb
 
 
-@pytest.mark.parametrize("rows", [256, 4096])
-def test_ppo_grad_matches_oracle(rows):
+@pytest.mark.parametrize("rows,A,precision", [(256, 2, 0), (4096, 2, 0), (256, 2, 1), (4096, 2, 1), (65536, 2, 1),
+                                              (512, 4, 1), (512, 8, 1)])
+def test_ppo_grad_matches_oracle(rows, A, precision):
+    """precision 0: fp32 MFMA kernels; 1: split-fp16 MFMA kernels (sgd_sf16.hip) — same 1e-5 bar"""
     from rlks import _lib
 
     d = _dev()
-    p = _params(d, seed=rows)
+    D = 3 * A
+    p = _params(d, seed=rows + A, D=D, A=A)
+    p.desc.precision = precision
     rng = np.random.default_rng(rows)
-    mb = _minibatch(rows, rng, p=p, d=d)
+    mb = _minibatch(rows, rng, D=D, A=A, p=p, d=d)
     # value targets near the current values so that some rows are inside / outside vf_clip
-    _, vv = p.forward(torch.from_numpy(mb[:, :6].copy()).to(d))
-    mb[:, 9] = vv.cpu().numpy() + rng.standard_normal(rows).astype(np.float32) * 4
+    _, vv = p.forward(torch.from_numpy(mb[:, :D].copy()).to(d))
+    mb[:, D + A + 1] = vv.cpu().numpy() + rng.standard_normal(rows).astype(np.float32) * 4
     adv_mean, adv_invstd, klc = 0.3, 0.7, 0.2
     dyn = torch.tensor([adv_mean, adv_invstd, klc, 1.0 / rows, 0, 0, 0, 0], dtype=torch.float32, device=d)
     co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.01)
@@ -149,7 +153,7 @@ def test_ppo_grad_matches_oracle(rows):
     _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
               rows, grad.data_ptr(), stats.data_ptr(), ws.data_ptr(), ws.numel(), None)
     g = grad.cpu().numpy()
-    eg, est = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, 6, 256, 2, mb, entropy_coeff=0.01,
+    eg, est = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, 256, A, mb, entropy_coeff=0.01,
                                    kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd)
     from rlks.policy import TENSOR_NAMES
 
