@@ -47,27 +47,28 @@ __device__ __forceinline__ float fast_tanh(float x) {
 }
 
 // reduce 16 per-lane values (register r <-> accumulator row) over the 32 lanes of a half-wave;
-// afterwards lane l holds the total of register ((l >> 1) & 15) (lanes l and l^1 agree)
+// afterwards lane l holds the total of register ((l >> 1) & 15) (lanes l and l^1 agree).
+// Reduce-scatter without LDS: v_permlane16_swap pairs rows 0/1 (and 2/3) of the wave, then
+// DPP row_ror:8, row_half_mirror and two quad_perms finish within each row of 16 lanes
+// (38 VALU, no ds_bpermute round trips).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
 __device__ __forceinline__ float half_wave_reduce16(const float (&v)[16], int l) {
-  float v8[8], v4[4], v2[2];
-  {
-    const bool b = (l >> 4) & 1;
+  float u[8], w[4], x[2];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v8[j] = (b ? v[j + 8] : v[j]) + __shfl_xor(b ? v[j] : v[j + 8], 16, 64);
+  for (int i = 0; i < 8; ++i) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
+    u[i] = __uint_as_float(p[0]) + __uint_as_float(p[1]);  // even rows: v[i], odd rows: v[i + 8]
   }
-  {
-    const bool b = (l >> 3) & 1;
+  const bool b3 = (l >> 3) & 1, b2 = (l >> 2) & 1, b1 = (l >> 1) & 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v4[j] = (b ? v8[j + 4] : v8[j]) + __shfl_xor(b ? v8[j] : v8[j + 4], 8, 64);
-  }
-  {
-    const bool b = (l >> 2) & 1;
+  for (int i = 0; i < 4; ++i) w[i] = (b3 ? u[i + 4] : u[i]) + dpp<0x128>(b3 ? u[i] : u[i + 4]);  // row_ror:8
 #pragma unroll
-    for (int j = 0; j < 2; ++j) v2[j] = (b ? v4[j + 2] : v4[j]) + __shfl_xor(b ? v4[j] : v4[j + 2], 4, 64);
-  }
-  const bool b = (l >> 1) & 1;
-  float v1 = (b ? v2[1] : v2[0]) + __shfl_xor(b ? v2[0] : v2[1], 2, 64);
-  return v1 + __shfl_xor(v1, 1, 64);
+  for (int i = 0; i < 2; ++i) x[i] = (b2 ? w[i + 2] : w[i]) + dpp<0x141>(b2 ? w[i] : w[i + 2]);  // half_mirror
+  const float y = (b1 ? x[1] : x[0]) + dpp<0x4E>(b1 ? x[0] : x[1]);                             // quad [2,3,0,1]
+  return y + dpp<0xB1>(y);                                                                         // quad [1,0,3,2]
 }
 
 // ----------------------------------------------------------------------------- layout

@@ -13,40 +13,59 @@ namespace rlks {
 
 // ----------------------------------------------------------------------------- reduce
 // out[i] = sum_p part[p * pstride + i] (i < len, p < P) in a fixed order with f64 accumulation.
-// A block = OPB outputs x G partial-groups (OPB * G = 256); G is chosen per task so that every
-// thread sums about 16 partials, so narrow tasks (b3, stats) do not leave a serial tail.
+// A block = 256 threads = OPB output vectors x G partial-groups; a vector is 4 consecutive outputs
+// (one 16-byte load per partial) when the task's length and stride allow it, else 1.  G is chosen
+// per task so that every thread sums about 16 partials.
 struct RedTask {
   const float* part;
   float* out;        // float output ...
   double* out64;     // ... or double output (stats)
   int64_t pstride;
-  int P, len, G;
+  int P, len, G, V;
   int blk0;
 };
-constexpr int MAX_TASKS = 16;
+constexpr int MAX_TASKS = 20;
 struct RedArgs {
   RedTask t[MAX_TASKS];
   int ntasks;
+  double* stats;     // optional: stats[4] = rows, stats[5..7] = 0 (the sums come from tasks)
+  double rows;
 };
 
 __global__ __launch_bounds__(256) void k_reduce(RedArgs g) {
-  __shared__ double sh[256];
+  __shared__ double sh[4][256];
   int ti = 0;
   while (ti + 1 < g.ntasks && (int)blockIdx.x >= g.t[ti + 1].blk0) ++ti;
   const RedTask T = g.t[ti];
   const int opb = 256 / T.G;
   const int o = threadIdx.x % opb, grp = threadIdx.x / opb;
-  const int i = ((int)blockIdx.x - T.blk0) * opb + o;
-  double s = 0.0;
-  if (i < T.len)
-    for (int p = grp; p < T.P; p += T.G) s += (double)T.part[(int64_t)p * T.pstride + i];
-  sh[threadIdx.x] = s;
+  const int iv = ((int)blockIdx.x - T.blk0) * opb + o;  // output vector
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  if (T.V == 4) {
+    if (4 * iv < T.len)
+      for (int p = grp; p < T.P; p += T.G) {
+        const float4 v = *reinterpret_cast<const float4*>(T.part + (int64_t)p * T.pstride + 4 * iv);
+        s[0] += (double)v.x; s[1] += (double)v.y; s[2] += (double)v.z; s[3] += (double)v.w;
+      }
+  } else if (iv < T.len) {
+    for (int p = grp; p < T.P; p += T.G) s[0] += (double)T.part[(int64_t)p * T.pstride + iv];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sh[j][threadIdx.x] = s[j];
   __syncthreads();
-  if (grp == 0 && i < T.len) {
-    double t = 0.0;
-    for (int j = 0; j < T.G; ++j) t += sh[j * opb + o];
-    if (T.out64) T.out64[i] = t;
-    else T.out[i] = (float)t;
+  if (grp == 0) {
+    for (int j = 0; j < T.V; ++j) {
+      const int i = T.V * iv + j;
+      if (i >= T.len) break;
+      double t = 0.0;
+      for (int q = 0; q < T.G; ++q) t += sh[j][q * opb + o];
+      if (T.out64) T.out64[i] = t;
+      else T.out[i] = (float)t;
+    }
+  }
+  if (g.stats && blockIdx.x == 0 && threadIdx.x == 0) {
+    g.stats[RLKS_STAT_ROWS] = g.rows;
+    g.stats[5] = g.stats[6] = g.stats[7] = 0.0;
   }
 }
 
@@ -57,12 +76,15 @@ struct Reducer {
     RedTask& t = a.t[a.ntasks++];
     int G = 1;
     while (G < 256 && G * 16 < P) G *= 2;
+    const bool vec = len % 4 == 0 && pstride % 4 == 0 && ((uintptr_t)part & 15) == 0;
     t.part = part; t.out = out; t.out64 = out64; t.pstride = pstride; t.P = P; t.len = len; t.G = G;
+    t.V = vec ? 4 : 1;
     t.blk0 = blocks;
-    blocks += (int)cdiv(len, 256 / G);
+    blocks += (int)cdiv(cdiv(len, t.V), 256 / G);
   }
 };
 
+// fp32 path: per-net stat sums -> RLKS_STAT_* layout
 __global__ void k_stats_finish(double* __restrict__ st, const double* __restrict__ s_pi,
                                const double* __restrict__ s_vf, int rows) {
   if (threadIdx.x) return;
@@ -232,7 +254,7 @@ struct SfWs {
 static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   SfWs w{};
   const int KD = sf_kd(D), tiles = M / 32;
-  w.blocks = M / 256;
+  w.blocks = M / 128;  // F1 workgroups of 4 x 32 rows
   w.splits = 1;
   while (w.splits * 2 <= 128 && tiles % (w.splits * 2) == 0) w.splits *= 2;
   w.tiles_per_split = tiles / w.splits;
@@ -382,10 +404,8 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     a.n[net].b2 = P.b2; a.n[net].w3 = P.w3; a.n[net].b3 = P.b3;
   }
   // F1 (forward, loss, dZ2, dH1 -> dW1 / db1, dW3 / db3) per net; F2 (dW2, db2) for both
-  if (f_pi)
-    if (int rc = launch_sf_f1(a, 0, A, s)) return rc;
-  if (f_vf)
-    if (int rc = launch_sf_f1(a, 1, A, s)) return rc;
+  if (f_pi || f_vf)
+    if (int rc = launch_sf_f1(a, f_pi ? 0 : 1, (f_pi && f_vf) ? 2 : 1, A, s)) return rc;
   if (phases & RLKS_PHASE_DW2)
     if (int rc = launch_sf_dw2(a, w.splits, s)) return rc;
   if (!(phases & RLKS_PHASE_REDUCE)) return RLKS_OK;
@@ -400,14 +420,18 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
     R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, M / 32, An * H);
     R.add(n.part_b3, grad + o[5], nullptr, An, M / 32, An);
-    if (stats) R.add(n.part_stat, nullptr, w.stat64 + 4 * net, 4, M / 32, 4);
+  }
+  if (stats) {  // per-tile columns [policy loss, vf loss, kl, entropy] -> RLKS_STAT_* directly
+    const int tiles = M / 32;
+    R.add(w.n[0].part_stat + 0, nullptr, stats + RLKS_STAT_POLICY_LOSS, 4, tiles, 1);
+    R.add(w.n[1].part_stat + 1, nullptr, stats + RLKS_STAT_VF_LOSS, 4, tiles, 1);
+    R.add(w.n[0].part_stat + 2, nullptr, stats + RLKS_STAT_KL, 4, tiles, 1);
+    R.add(w.n[0].part_stat + 3, nullptr, stats + RLKS_STAT_ENTROPY, 4, tiles, 1);
+    R.a.stats = stats;
+    R.a.rows = (double)M;
   }
   hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
   RLKS_LAUNCHED();
-  if (stats) {
-    hipLaunchKernelGGL(k_stats_finish, dim3(1), dim3(64), 0, s, stats, w.stat64, w.stat64 + 4, M);
-    RLKS_LAUNCHED();
-  }
   return RLKS_OK;
 }
 

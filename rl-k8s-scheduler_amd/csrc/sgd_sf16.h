@@ -32,14 +32,15 @@ struct SfArgs {
   const float* x;
   int x_stride, M, D, A_pi;
   int tiles_per_split;
+  int net0;  // F1: first net of the grid (blockIdx.y + net0)
   rlks_ppo_coeffs co;
   const float* dyn;
 };
 
-size_t sf_f1_lds_bytes(int A_, int NG);
+size_t sf_f1_lds_bytes(int A_, int NG, int KD, int W);
 int sf_kd(int D);
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
-int launch_sf_f1(const SfArgs& a, int net, int A, hipStream_t s);  // needs M % 256 == 0
+int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s);  // needs M % 256 == 0
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
 
 }  // namespace rlks

@@ -36,8 +36,9 @@ namespace rlks {
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
 
-constexpr int SF_W = 8;             // waves per F1 / F2 workgroup
-constexpr int SF_ROWS = 32 * SF_W;  // minibatch rows per F1 workgroup
+constexpr int SF_W = 8;             // waves per F2 workgroup
+constexpr int SF_F1_W = 4;          // waves per F1 workgroup (one per SIMD)
+constexpr int SF_ROWS = 256;        // minibatch rows must be a multiple of this
 constexpr int SF_CH = 8192;         // halves per staged chunk (per hi / lo array)
 constexpr float SF_H1_SCALE = 16384.f;  // tanh outputs (|h| < 1) scaled by 2^14
 
@@ -92,6 +93,17 @@ __device__ __forceinline__ float pow2(int e) { return ldexpf(1.f, e); }
 __device__ __forceinline__ float tanh_abs(float x) {
   const float e = __builtin_amdgcn_exp2f(x * 2.885390081777927f);
   return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
+
+// interleave the scheduling region: NM x (1 MFMA, NV VALU) (cdna_hip_programming.md T19); an
+// MFMA leaves 24 of its 32 issue cycles for independent vector work of the same wave
+template <int NM, int NV>
+__device__ __forceinline__ void sched_interleave() {
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+  }
 }
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -173,11 +185,12 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
 // Weight chunks staged by LDS-DMA (global_load_lds_dwordx4: each lane's 16 bytes land at
 // base + 16 * lane, so the swizzle is applied on the global side).  Chunk c < 8: w2p columns
 // [32c, 32c+32) of all 256 rows (Z2 loop); c >= 8: w2t rows [32(c-8), +32) (dH1 loop).  A chunk
-// is 2 x 1024 slots of 16 B (hi, lo); wave w issues slot blocks 4w .. 4w+3 of 64.
+// is 2 x 1024 slots of 16 B (hi, lo) = 32 blocks of 64; wave w of W issues blocks (32/W) w + i.
+template <int W>
 __device__ __forceinline__ void chunk_dma(const SfNet& N, _Float16* buf, int c, int w, int l) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = 4 * w + i, arr = blk >> 4, sig = (blk & 15) * 64 + l;
+  for (int i = 0; i < 32 / W; ++i) {
+    const int blk = (32 / W) * w + i, arr = blk >> 4, sig = (blk & 15) * 64 + l;
     const _Float16* src;
     if (c < 8) {
       const int n = sig >> 2, pc = (sig & 3) ^ ((n >> 2) & 3);
@@ -192,8 +205,21 @@ __device__ __forceinline__ void chunk_dma(const SfNet& N, _Float16* buf, int c, 
 }
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-template <int A_, int NET, int KD, int NG>
-__global__ __launch_bounds__(512) void k_sf_fwdbwd(SfArgs g) {
+#ifdef RLKS_STAMPS
+// diagnostic build only (tools/stamps.sh): per-wave phase clocks of F1, [net][tile][phase]
+__device__ unsigned long long g_sf_stamps[2][4096][8];
+#define SF_STAMP(i) \
+  if (l == 0 && tile < 4096) g_sf_stamps[NET][tile][i] = __builtin_amdgcn_s_memtime()
+#else
+#define SF_STAMP(i)
+#endif
+
+// W waves per workgroup, one 32-row tile each; one wave per SIMD (waves_per_eu 1) so that every
+// wave has the full 512-register file: dZ2^T stays split in registers through the dH1 loop and
+// the LDS fragments of the next MFMA step are in flight during the current one.
+template <int A_, int NET, int KD, int NG, int W>
+__device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
+  constexpr int NTHR = 64 * W;
   constexpr int KS = KD / 16;   // k-steps of the first layer
   // NG: accumulator row groups (8 rows each) holding the rows d <= D of dW1a^T.  NG = 1 (D < 8,
   // the reference's 2-cloud obs) accumulates dW1a^T in LDS; wider obs keep it in registers.
@@ -203,15 +229,18 @@ __global__ __launch_bounds__(512) void k_sf_fwdbwd(SfArgs g) {
   _Float16* sCh = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][SF_CH]  (64 KB)
   float* sB2 = lds + 2 * SF_CH;                      // [HID]
   float* sW3 = sB2 + HID;                            // [A_][HID]
-  float* sDW = sW3 + A_ * HID;                       // DW1_LDS: [SF_W][HID k][8 d]  (64 KB)
+  _Float16* sW1 = reinterpret_cast<_Float16*>(sW3 + A_ * HID);  // [2 hi/lo][HID k][KD] (swizzled)
+  h8* sXT = reinterpret_cast<h8*>(sW1 + 2 * HID * KD);          // [W][2 s][2 hi/lo][64 lanes]
+  float* sDW = reinterpret_cast<float*>(sXT + W * 4 * 64);   // DW1_LDS: [2][W][32 k][8 d]
 
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int D = g.D, stride = g.x_stride;
-  const int tile = blockIdx.x * SF_W + w, row0 = tile * 32;
+  const int tile = blockIdx.x * W + w, row0 = tile * 32;
+  SF_STAMP(0);
 
-  chunk_dma(N, sCh, 0, w, l);
-  for (int i = tid; i < HID; i += 512) sB2[i] = N.b2[i];
-  for (int i = tid; i < A_ * HID; i += 512) sW3[i] = N.w3[i];
+  chunk_dma<W>(N, sCh, 0, w, l);
+  for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i];
+  for (int i = tid; i < A_ * HID; i += NTHR) sW3[i] = N.w3[i];
 
   // ---- this wave's rows: Xa = [X | 1 | 0] fragments, lane row m = r, d = 16ks + 8h + j
   float xv[KS * 8];
@@ -235,19 +264,26 @@ __global__ __launch_bounds__(512) void k_sf_fwdbwd(SfArgs g) {
   const int e_w2 = (int)N.sc[5];
   const float inv_z1 = inv_w1 / sx;  // Z1 accumulators carry s_x s_w1
 
-  // W1a fragments (row / column k = 32 kt + r), prefetched one k-tile ahead
-  h8 wh[KS], wl[KS], nwh[KS], nwl[KS];
-  auto w1_load = [&](int kt, h8 (&dh)[KS], h8 (&dl_)[KS]) {
+  // W1a (hi, lo) in LDS: row k of KD halves, 16-byte pieces XOR-swizzled by (k >> 3) so that the
+  // fragment reads of 16 consecutive rows are conflict-free
+  for (int p = tid; p < 2 * HID * KD / 8; p += NTHR) {
+    const int arr = p / (HID * KD / 8), q = p - arr * (HID * KD / 8), k = q / (KD / 8), pc = q - k * (KD / 8);
+    const uint4 v = *reinterpret_cast<const uint4*>((arr ? N.w1l : N.w1h) + k * KD + 8 * pc);
+    *reinterpret_cast<uint4*>(sW1 + arr * HID * KD + k * KD + 8 * (pc ^ ((k >> 3) & 1))) = v;
+  }
+  h8 wh[KS], wl[KS];
+  auto w1_frag = [&](int kt) {
     const int k = 32 * kt + r;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      dh[ks] = *reinterpret_cast<const h8*>(N.w1h + k * KD + 16 * ks + 8 * h);
-      dl_[ks] = *reinterpret_cast<const h8*>(N.w1l + k * KD + 16 * ks + 8 * h);
+      const int off = k * KD + 8 * ((2 * ks + h) ^ ((k >> 3) & 1));
+      wh[ks] = *reinterpret_cast<const h8*>(sW1 + off);
+      wl[ks] = *reinterpret_cast<const h8*>(sW1 + HID * KD + off);
     }
   };
-  w1_load(0, wh, wl);
   vm_drain();
   __syncthreads();
+  SF_STAMP(1);
 
   // ---- Z2^T = W2 H1^T over 8 k-tiles; H1^T tile kt recomputed from Xa just before its use
   f32x16 acc[8];
@@ -255,39 +291,65 @@ __global__ __launch_bounds__(512) void k_sf_fwdbwd(SfArgs g) {
   for (int nt = 0; nt < 8; ++nt)
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
+  // H1^T tile kt (rows k = 32 kt + perm) as split B fragments; software-pipelined one k-tile
+  // ahead so that its MFMA + tanh + split overlap the current tile's 48 MFMAs
+  auto h1t_tile = [&](int kt, h8 (&bh)[2], h8 (&bl)[2]) {
+    w1_frag(kt);
+    f32x16 z;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) z = mma3(wh[ks], wl[ks], xh[ks], xl[ks], z);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
+    split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
+    split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
+  };
+  h8 bh[2], bl[2];
+  h1t_tile(0, bh, bl);
   for (int c = 0; c < 8; ++c) {
     const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
-    chunk_dma(N, sCh + ((c + 1) & 1) * 2 * SF_CH, c + 1, w, l);
-    w1_load((c + 1) & 7, nwh, nwl);
-    h8 bh[2], bl[2];
-    {
-      f32x16 z;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) z[q] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) z = mma3(wh[ks], wl[ks], xh[ks], xl[ks], z);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
-      split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
-      split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
-    }
+    chunk_dma<W>(N, sCh + ((c + 1) & 1) * 2 * SF_CH, c + 1, w, l);
+    h8 fa[8][2][2];
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
       const int n = 32 * nt + r;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int off = n * 32 + 8 * ((2 * s + h) ^ ((n >> 2) & 3));
-        const h8 ah = *reinterpret_cast<const h8*>(buf + off);
-        const h8 al = *reinterpret_cast<const h8*>(buf + SF_CH + off);
-        acc[nt] = mma3(ah, al, bh[s], bl[s], acc[nt]);
+        fa[nt][s][0] = *reinterpret_cast<const h8*>(buf + off);
+        fa[nt][s][1] = *reinterpret_cast<const h8*>(buf + SF_CH + off);
       }
     }
+    h8 nbh[2], nbl[2];
+    h1t_tile(c + 1 < 8 ? c + 1 : 7, nbh, nbl);  // next tile's H1 (branch-free: the last is discarded)
+    // consecutive MFMAs on independent accumulators
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) { wh[ks] = nwh[ks]; wl[ks] = nwl[ks]; }
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) acc[nt] = mma(fa[nt][s][1], bh[s], acc[nt]);
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) acc[nt] = mma(fa[nt][s][0], bl[s], acc[nt]);
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) acc[nt] = mma(fa[nt][s][0], bh[s], acc[nt]);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) { bh[s] = nbh[s]; bl[s] = nbl[s]; }
     vm_drain();
     __syncthreads();
   }
 
+  SF_STAMP(2);
+  // Xa^T values for dW1a^T = Xa^T dZ1 (lane row d = r, m = perm(s, h, j)), loaded before the
+  // head so that their latency hides behind it; split after dZ2
+  float xtv[16];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = sf_perm(s, h, j);
+      xtv[s * 8 + j] = r < D ? g.x[(size_t)(row0 + m) * stride + r] : (r == D ? 1.f : 0.f);
+    }
   // ---- H2^T = tanh(Z2^T + b2), head out[a] = b3 + sum_n W3[a][n] H2[n]
   const float inv_z2 = inv_w2 / SF_H1_SCALE;
   float out[A_];
@@ -376,6 +438,7 @@ __global__ __launch_bounds__(512) void k_sf_fwdbwd(SfArgs g) {
     }
   }
 
+  SF_STAMP(3);
   // ---- per-tile partials straight to HBM: dW3[a][n] = sum_m dl[m][a] H2[m][n] (half-wave
   // reduce), db3, loss stats
 #pragma unroll
@@ -403,6 +466,7 @@ __global__ __launch_bounds__(512) void k_sf_fwdbwd(SfArgs g) {
     }
   }
 
+  SF_STAMP(4);
   // ---- dZ2^T = (dl W3) (1 - H2^2): to HBM (F2), tile max |dZ2| (this wave's split + F2's scale)
   float dmx = 0.f;
   {
@@ -444,91 +508,136 @@ __global__ __launch_bounds__(512) void k_sf_fwdbwd(SfArgs g) {
       split16(acc[nt], 8, sdz, dzh[nt][1], dzl[nt][1]);
     }
   }
-  // Xa^T fragments of dW1a^T = Xa^T dZ1: lane row d = r, m = perm(s, h, j)
-  h8 xth[2], xtl[2];
   {
-    float t[16];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = sf_perm(s, h, j);
-        t[s * 8 + j] = r < D ? g.x[(size_t)(row0 + m) * stride + r] : (r == D ? 1.f : 0.f);
-      }
-    split8(t, 0, sx, xth[0], xtl[0]);
-    split8(t, 8, sx, xth[1], xtl[1]);
+    h8 a, b;
+    split8(xtv, 0, sx, a, b);
+    sXT[(w * 4 + 0) * 64 + l] = a;
+    sXT[(w * 4 + 1) * 64 + l] = b;
+    split8(xtv, 8, sx, a, b);
+    sXT[(w * 4 + 2) * 64 + l] = a;
+    sXT[(w * 4 + 3) * 64 + l] = b;
   }
-
+  SF_STAMP(5);
   // ---- dH1 = dZ2 W2 per 32-column k-tile; dZ1 = dH1 (1 - H1^2); dW1a^T = Xa^T dZ1
   // dZ1 enters the split at 2^(e_dz + e_w2 - 23): |dH1 2^(e_dz + e_w2)| <= 256 2^15 2^15
   float dw1[DW1_LDS ? 1 : 8][4 * NG];
+  const int blk = blockIdx.x;
+  auto dw1_flush = [&](int kt) {  // thread tid < 32 (D + 1): element (k = 32 kt + tid / (D+1), d)
+    const int nd = D + 1, kk = tid / nd, d = tid - kk * nd, k = 32 * kt + kk;
+    float s = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) s += sDW[(((kt & 1) * W + ww) * 32 + kk) * 8 + d];
+    if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
+    else N.part_b1[(size_t)blk * HID + k] = s;
+  };
   const float sz1 = pow2(-23);
   const float u1 = pow2(23 - ex - edz - e_w2);
+  // derivative (1 - H1^2) of k-tile kt, rows m in registers (Z1 = Xa W1a^T)
+  auto h1_der = [&](int kt, f32x16& der) {
+    w1_frag(kt);
+    f32x16 z;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) z = mma3(xh[ks], xl[ks], wh[ks], wl[ks], z);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float h1 = tanh_abs(z[q] * inv_z1);
+      der[q] = 1.f - h1 * h1;
+    }
+  };
+  // dZ1 = dH1 (1 - H1^2) -> split -> dW1a^T = Xa^T dZ1 of k-tile kt (issued one iteration late so
+  // that it overlaps the next tile's MFMAs)
+  auto dw1_tile = [&](int kt, const f32x16& dh, const f32x16& der) {
+    f32x16 dz;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dz[q] = dh[q] * der[q];
+    h8 zh[2], zl[2];
+    split16(dz, 0, sz1, zh[0], zl[0]);
+    split16(dz, 8, sz1, zh[1], zl[1]);
+    f32x16 wacc, wacc2;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { wacc[q] = 0.f; wacc2[q] = 0.f; }
+    const h8 x0h = sXT[(w * 4 + 0) * 64 + l], x0l = sXT[(w * 4 + 1) * 64 + l];
+    const h8 x1h = sXT[(w * 4 + 2) * 64 + l], x1l = sXT[(w * 4 + 3) * 64 + l];
+    wacc = mma(x0l, zh[0], wacc);
+    wacc2 = mma(x1l, zh[1], wacc2);
+    wacc = mma(x0h, zl[0], wacc);
+    wacc2 = mma(x1h, zl[1], wacc2);
+    wacc = mma(x0h, zh[0], wacc);
+    wacc2 = mma(x1h, zh[1], wacc2);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) wacc[q] += wacc2[q];
+    if constexpr (DW1_LDS) {
+      // rows d = 4h + 0..3 of column k: one 16-byte store into this wave's slot of k-tile kt
+      float4 v = {wacc[0] * u1, wacc[1] * u1, wacc[2] * u1, wacc[3] * u1};
+      *reinterpret_cast<float4*>(sDW + (((kt & 1) * W + w) * 32 + r) * 8 + 4 * h) = v;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4 * NG; ++q) dw1[kt][q] = wacc[q] * u1;
+    }
+  };
+  f32x16 der, dprev, derprev;
+  h1_der(0, der);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) { dprev[q] = 0.f; derprev[q] = 0.f; }
   for (int c = 8; c < 16; ++c) {
     const int kt = c - 8;
     const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
-    if (c + 1 < 16) chunk_dma(N, sCh + ((c + 1) & 1) * 2 * SF_CH, c + 1, w, l);
-    if (c + 1 < 16) w1_load(kt + 1, nwh, nwl);
-    f32x16 d;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) d[q] = 0.f;
+    // branch-free body: at c = 15 chunk 15 is re-fetched into the idle buffer
+    chunk_dma<W>(N, sCh + ((c + 1) & 1) * 2 * SF_CH, c + 1 < 16 ? c + 1 : 15, w, l);
+    h8 fb[8][2][2];
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int off = r * HID + 8 * ((4 * nt + 2 * s + h) ^ (r & 15));
-        const h8 bh = *reinterpret_cast<const h8*>(buf + off);
-        const h8 bl = *reinterpret_cast<const h8*>(buf + SF_CH + off);
-        d = mma3(dzh[nt][s], dzl[nt][s], bh, bl, d);
+        fb[nt][s][0] = *reinterpret_cast<const h8*>(buf + off);
+        fb[nt][s][1] = *reinterpret_cast<const h8*>(buf + SF_CH + off);
       }
-    {
-      f32x16 z;
+    // four independent accumulation chains (n-tile mod 4), MFMAs interleaved across them
+    f32x16 dc[4];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) z[q] = 0.f;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) z = mma3(xh[ks], xl[ks], wh[ks], wl[ks], z);
+      for (int q = 0; q < 16; ++q) dc[i][q] = 0.f;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float h1 = tanh_abs(z[q] * inv_z1);
-        d[q] = d[q] * (1.f - h1 * h1);
+    for (int g2 = 0; g2 < 2; ++g2)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dc[i] = mma(dzl[4 * g2 + i][s], fb[4 * g2 + i][s][0], dc[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dc[i] = mma(dzh[4 * g2 + i][s], fb[4 * g2 + i][s][1], dc[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dc[i] = mma(dzh[4 * g2 + i][s], fb[4 * g2 + i][s][0], dc[i]);
       }
+    f32x16 nder;
+    h1_der(kt + 1 < 8 ? kt + 1 : 7, nder);
+    // tail of k-tile kt - 1; at kt = 0 it runs on zeros into slot 1, rewritten before its flush
+    dw1_tile((kt + 7) & 7, dprev, derprev);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      dprev[q] = (dc[0][q] + dc[1][q]) + (dc[2][q] + dc[3][q]);
+      derprev[q] = der[q];
+      der[q] = nder[q];
     }
-    h8 zh[2], zl[2];
-    split16(d, 0, sz1, zh[0], zl[0]);
-    split16(d, 8, sz1, zh[1], zl[1]);
-    f32x16 wacc;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) wacc[q] = 0.f;
-    wacc = mma3(xth[0], xtl[0], zh[0], zl[0], wacc);
-    wacc = mma3(xth[1], xtl[1], zh[1], zl[1], wacc);
-    if constexpr (DW1_LDS) {
-      // rows d = 4h + 0..3 of column k: one 16-byte store into this wave's [k][8] slot
-      float4 v = {wacc[0] * u1, wacc[1] * u1, wacc[2] * u1, wacc[3] * u1};
-      *reinterpret_cast<float4*>(sDW + (w * HID + 32 * kt + r) * 8 + 4 * h) = v;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4 * NG; ++q) dw1[kt][q] = wacc[q] * u1;
-    }
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) { wh[ks] = nwh[ks]; wl[ks] = nwl[ks]; }
+    if constexpr (DW1_LDS)
+      if (kt > 1 && tid < 32 * (D + 1)) dw1_flush(kt - 2);
     vm_drain();
     __syncthreads();
   }
-
-  // ---- workgroup epilogue: fixed-order sums of dW1a^T over the 8 waves -> per-block partials
-  const int blk = blockIdx.x;
+  dw1_tile(7, dprev, derprev);
   if constexpr (DW1_LDS) {
-    const int nd = D + 1;
-    for (int e = tid; e < HID * nd; e += 512) {
-      const int k = e / nd, d = e - k * nd;
-      float s = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < SF_W; ++ww) s += sDW[(ww * HID + k) * 8 + d];
-      if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
-      else N.part_b1[(size_t)blk * HID + k] = s;
-    }
+    if (tid < 32 * (D + 1)) dw1_flush(6);
+    __syncthreads();
+  }
+  SF_STAMP(6);
+  // ---- workgroup epilogue: fixed-order sums of dW1a^T over the 8 waves -> per-block partials
+  if constexpr (DW1_LDS) {
+    if (tid < 32 * (D + 1)) dw1_flush(7);
   } else {
-    float* sP = reinterpret_cast<float*>(sCh);  // [SF_W][HID][8] per pass of 8 rows
+    float* sP = reinterpret_cast<float*>(sCh);  // [W][HID][8] per pass of 8 rows
     for (int d0 = 0; d0 <= D; d0 += 8) {
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt)
@@ -539,17 +648,26 @@ __global__ __launch_bounds__(512) void k_sf_fwdbwd(SfArgs g) {
         }
       __syncthreads();
       const int nd = min(8, D + 1 - d0);
-      for (int e = tid; e < HID * nd; e += 512) {
+      for (int e = tid; e < HID * nd; e += NTHR) {
         const int k = e / nd, dd = e - k * nd, d = d0 + dd;
         float s = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < SF_W; ++ww) s += sP[(ww * HID + k) * 8 + dd];
+        for (int ww = 0; ww < W; ++ww) s += sP[(ww * HID + k) * 8 + dd];
         if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
         else N.part_b1[(size_t)blk * HID + k] = s;
       }
       __syncthreads();
     }
   }
+  SF_STAMP(7);
+}
+
+// both nets in one grid (blockIdx.y + net0): the hardware backfills CUs across the two nets
+// instead of draining between two launches
+template <int A_, int KD, int NG, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_sf_fwdbwd(SfArgs g) {
+  if (blockIdx.y + g.net0 == 0) sf_fwdbwd_body<A_, 0, KD, NG, W>(g);
+  else sf_fwdbwd_body<1, 1, KD, NG, W>(g);
 }
 
 // ----------------------------------------------------------------------------- F2
@@ -684,8 +802,16 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
 }
 
 // ----------------------------------------------------------------------------- launchers
-size_t sf_f1_lds_bytes(int A_, int NG) {
-  return (size_t)2 * 2 * SF_CH * sizeof(_Float16) + (size_t)(HID + A_ * HID + (NG == 1 ? SF_W * HID * 8 : 0)) * sizeof(float);
+#ifdef RLKS_STAMPS
+extern "C" int rlks_dbg_sf_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sf_stamps), sizeof(g_sf_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
+
+size_t sf_f1_lds_bytes(int A_, int NG, int KD, int W) {
+  return (size_t)2 * 2 * SF_CH * sizeof(_Float16) + (size_t)(HID + A_ * HID) * sizeof(float) +
+         (size_t)2 * HID * KD * sizeof(_Float16) + (size_t)W * 4 * 64 * 16 +
+         (NG == 1 ? (size_t)2 * W * 32 * 8 * sizeof(float) : 0);
 }
 
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
@@ -697,10 +823,11 @@ int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
 }
 
 template <int A_, int KD, int NG>
-static int launch_f1_net(const SfArgs& a, int net, hipStream_t s) {
-  const dim3 grid(a.M / SF_ROWS);
-  if (net == 0) hipLaunchKernelGGL((k_sf_fwdbwd<A_, 0, KD, NG>), grid, dim3(512), sf_f1_lds_bytes(A_, NG), s, a);
-  else hipLaunchKernelGGL((k_sf_fwdbwd<1, 1, KD, NG>), grid, dim3(512), sf_f1_lds_bytes(1, NG), s, a);
+static int launch_f1_net(SfArgs a, int net0, int nets, hipStream_t s) {
+  constexpr int W = SF_F1_W;
+  a.net0 = net0;
+  const dim3 grid(a.M / (32 * W), nets);
+  hipLaunchKernelGGL((k_sf_fwdbwd<A_, KD, NG, W>), grid, dim3(64 * W), sf_f1_lds_bytes(A_, NG, KD, W), s, a);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }
@@ -708,13 +835,13 @@ static int launch_f1_net(const SfArgs& a, int net, hipStream_t s) {
 // obs_dim = 3 x clusters: C = 2, 4, 8 -> D = 6, 12, 24 (D + 1 <= 8, 16, 32)
 int sf_kd(int D) { return D + 1 <= 16 ? 16 : 32; }
 
-int launch_sf_f1(const SfArgs& a, int net, int A, hipStream_t s) {
+int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s) {
   RLKS_REQUIRE(a.M % SF_ROWS == 0, RLKS_ERR_ARG, "split-fp16 SGD step: rows must be a multiple of 256");
   RLKS_REQUIRE(a.D == 3 * A, RLKS_ERR_UNSUPPORTED, "split-fp16 SGD step expects obs_dim = 3 x n_actions");
   switch (A) {
-    case 2: return launch_f1_net<2, 16, 1>(a, net, s);
-    case 4: return launch_f1_net<4, 16, 2>(a, net, s);
-    case 8: return launch_f1_net<8, 32, 4>(a, net, s);
+    case 2: return launch_f1_net<2, 16, 1>(a, net0, nets, s);
+    case 4: return launch_f1_net<4, 16, 2>(a, net0, nets, s);
+    case 8: return launch_f1_net<8, 32, 4>(a, net0, nets, s);
     default: return fail(RLKS_ERR_UNSUPPORTED, "split-fp16 head is built for 2, 4 or 8 actions");
   }
 }

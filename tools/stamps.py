@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Phase timing of the split-fp16 F1 kernel from in-kernel s_memtime stamps (diagnostic build).
+
+  make -C rl-k8s-scheduler_amd/csrc stamps
+  RLKS_LIB=rl-k8s-scheduler_amd/rlks/librlks_stamps.so python tools/stamps.py
+
+Runs a few c2-sized SGD-step gradients (65,536 rows), then prints, per net, the median over waves
+of each phase's shader cycles (the stamps are taken by lane 0 of every wave after the phase)."""
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "rl-k8s-scheduler_amd"))
+PHASES = ["prologue", "Z2 loop", "head+loss", "dW3/stats", "dZ2 store+split", "dH1 loop", "epilogue"]
+
+
+def main():
+    import torch
+    from rlks import _lib
+    from rlks.policy import PolicyParams
+
+    assert "stamps" in os.environ.get("RLKS_LIB", ""), "set RLKS_LIB to librlks_stamps.so"
+    d = torch.device("cuda", 0)
+    rows = 65536
+    p = PolicyParams(6, 256, 2, device=d, seed=1)
+    p.desc.precision = _lib.RLKS_PRECISION_SF16
+    rng = np.random.default_rng(0)
+    mb = np.zeros((rows, 12), np.float32)
+    mb[:, :6] = rng.random((rows, 6))
+    mb[:, 6:8] = rng.standard_normal((rows, 2))
+    mb[:, 8] = rng.standard_normal(rows)
+    mb[:, 9] = rng.standard_normal(rows)
+    mb[:, 11] = rng.integers(0, 2, rows)
+    mb[:, 10] = -0.7
+    dyn = torch.tensor([0, 1, 0.2, 1.0 / rows, 0, 0, 0, 0], dtype=torch.float32, device=d)
+    co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.0)
+    wsb = C.c_int64()
+    _lib.call("rlks_ppo_workspace_bytes", C.byref(p.desc), rows, C.byref(wsb))
+    ws = torch.empty(wsb.value, dtype=torch.uint8, device=d)
+    grad = torch.zeros(p.padded, device=d)
+    mbt = torch.from_numpy(mb).to(d)
+    for _ in range(5):
+        _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
+                  rows, grad.data_ptr(), None, ws.data_ptr(), ws.numel(), None)
+    torch.cuda.synchronize()
+    st = np.zeros((2, 4096, 8), np.uint64)
+    assert _lib.lib().rlks_dbg_sf_stamps(st.ctypes.data_as(C.c_void_p)) == 0
+    tiles = rows // 32
+    for net in range(2):
+        s = st[net, :tiles].astype(np.int64)
+        dt = np.diff(s, axis=1)
+        tot = s[:, 7] - s[:, 0]
+        start = s[:, 0] - s[:, 0].min()
+        print(f"net {net}: wave lifetime median {np.median(tot):.0f} cyc, start spread {start.max():.0f} cyc")
+        for i, name in enumerate(PHASES):
+            print(f"  {name:18s} median {np.median(dt[:, i]):8.0f}  p90 {np.percentile(dt[:, i], 90):8.0f}"
+                  f"  share {np.median(dt[:, i]) / np.median(tot):.2f}")
+
+
+if __name__ == "__main__":
+    main()
