@@ -47,8 +47,9 @@ FLOPS_PER_ROW = {
     "k_dh1": 2 * 2 * H_ * H_ + 2 * 2 * D_ * H_,     # dH1 = dZ2 W2 and dW1 = dZ1^T X, both nets
     # split-fp16 kernels (sgd_sf16.hip), algorithmic fp32 FLOPs per row:
     # F1 per net = forward + head backward + dH1 = dZ2 W2 + dW1 = dZ1^T X
-    "k_sf_fwdbwd_pi": 2 * (D_ * H_ + H_ * H_ + H_ * A_) + 4 * H_ * A_ + 2 * H_ * H_ + 2 * D_ * H_,
-    "k_sf_fwdbwd_vf": 2 * (D_ * H_ + H_ * H_ + H_) + 4 * H_ + 2 * H_ * H_ + 2 * D_ * H_,
+    # (one launch covers both nets: forward + head backward + dH1 = dZ2 W2 + dW1 = dZ1^T X)
+    "k_sf_fwdbwd": (2 * (D_ * H_ + H_ * H_ + H_ * A_) + 4 * H_ * A_ + 2 * H_ * H_ + 2 * D_ * H_)
+                   + (2 * (D_ * H_ + H_ * H_ + H_) + 4 * H_ + 2 * H_ * H_ + 2 * D_ * H_),
     "k_sf_dw2": 2 * 2 * H_ * H_,                    # dW2 = dZ2^T H1, both nets
 }
 ENV_BYTES_PER_STEP = 4 + 8 + 24 + 4 + 1  # action, step r/w, obs, reward, done
@@ -98,9 +99,9 @@ def kernel_timing(algo, torch, reps=20):
               algo.mbuf.data_ptr(), s.cuda_stream)
     if algo.precision == "sf16":
         phase(_lib.RLKS_PHASE_ALL)()  # weight splits + dZ2 in place for the per-phase timings
-        phases = (("k_sf_prep", _lib.RLKS_PHASE_PREP), ("k_sf_fwdbwd_pi", _lib.RLKS_PHASE_FWD_PI),
-                  ("k_sf_fwdbwd_vf", _lib.RLKS_PHASE_FWD_VF), ("k_sf_dw2", _lib.RLKS_PHASE_DW2),
-                  ("k_reduce", _lib.RLKS_PHASE_REDUCE))
+        phases = (("k_sf_prep", _lib.RLKS_PHASE_PREP),
+                  ("k_sf_fwdbwd", _lib.RLKS_PHASE_FWD_PI | _lib.RLKS_PHASE_FWD_VF),
+                  ("k_sf_dw2", _lib.RLKS_PHASE_DW2), ("k_reduce", _lib.RLKS_PHASE_REDUCE))
         peak, peak_name = SF16_PEAK_TFLOPS, "frac_sf16_mfma"
     else:
         phases = (("k_fwd_head_pi", _lib.RLKS_PHASE_FWD_PI), ("k_fwd_head_vf", _lib.RLKS_PHASE_FWD_VF),
