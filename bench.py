@@ -130,8 +130,8 @@ def kernel_timing(algo, torch, reps=20):
                                  s.cuda_stream))
     gbs = GAE_BYTES_PER_STEP * N * T / (ms * 1e-3) / 1e9
     out["k_gae"] = {"ms": ms, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
-    ms = timed(lambda: _lib.call("rlks_rollout", algo.env.handle, desc, algo.params.flat.data_ptr(),
-                                 C.byref(algo.bufs), 1, s.cuda_stream), n=3)
+    ms = timed(lambda: _lib.call("rlks_rollout_ws", algo.env.handle, desc, algo.params.flat.data_ptr(),
+                                 C.byref(algo.bufs), 1, algo.ws.data_ptr(), algo.ws.numel(), s.cuda_stream), n=3)
     # T fused (pi forward + sample + env step) launches + one batched value pass over (T+1) N rows
     flops = (T * N + (T + 1) * N) * 269824 / 2
     out["rollout"] = {"ms": ms, "env_steps_per_s": T * N / (ms * 1e-3), "tflops": flops / (ms * 1e-3) / 1e12}

@@ -154,6 +154,13 @@ typedef struct rlks_rollout_bufs {
  * V(obs[T]).  obs[0] must hold the current observations. */
 int rlks_rollout(rlks_env* env, const rlks_mlp_desc* desc, const float* params_dev,
                  const rlks_rollout_bufs* bufs, int explore, void* stream);
+/* Same rollout; with desc->precision == RLKS_PRECISION_SF16 it runs the split-fp16 step kernel
+ * (both nets' forward + sample + env step per launch, values written per step, V(obs[T]) last)
+ * with the split weights in `workspace` (an rlks_ppo_workspace_bytes-sized buffer: the SGD step's
+ * workspace can be shared).  Other precisions fall through to rlks_rollout. */
+int rlks_rollout_ws(rlks_env* env, const rlks_mlp_desc* desc, const float* params_dev,
+                    const rlks_rollout_bufs* bufs, int explore, void* workspace, int64_t ws_bytes,
+                    void* stream);
 
 /* Minibatch rows per packed record: [obs D | logits_old A | adv | vtarg | logp_old | action] */
 int rlks_minibatch_stride(const rlks_mlp_desc* desc);

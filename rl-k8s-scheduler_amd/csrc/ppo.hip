@@ -247,7 +247,7 @@ struct SfWs {
   SfNetW w[2];
   SfNet n[2];
   double* stat64;
-  int64_t bytes;
+  int64_t bytes, weight_bytes;
   int blocks, splits, tiles_per_split;
 };
 
@@ -257,15 +257,15 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   w.blocks = M / 128;  // F1 workgroups of 4 x 32 rows
   w.splits = 1;
   while (w.splits * 2 <= 128 && tiles % (w.splits * 2) == 0) w.splits *= 2;
-  w.tiles_per_split = tiles / w.splits;
+  w.tiles_per_split = tiles > 0 ? tiles / w.splits : 0;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
     char* p = base ? base + o : nullptr;
     o += (bytes + 255) / 256 * 256;
     return p;
   };
+  // split weights of both nets first: their offsets do not depend on M (the rollout shares them)
   for (int net = 0; net < 2; ++net) {
-    const int An = net == 0 ? A : 1;
     SfNetW& W = w.w[net];
     SfNet& n = w.n[net];
     W.w1h = (_Float16*)take(2LL * HID * KD);
@@ -274,11 +274,18 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     W.w2pl = (_Float16*)take(2LL * HID * HID);
     W.w2th = (_Float16*)take(2LL * HID * HID);
     W.w2tl = (_Float16*)take(2LL * HID * HID);
+    W.w2rh = (_Float16*)take(2LL * HID * HID);
+    W.w2rl = (_Float16*)take(2LL * HID * HID);
     W.sc = (float*)take(4 * 8);
     W.pmax = (float*)take(4 * 32);
     W.dzmax = (unsigned*)take(4);
     n.w1h = W.w1h; n.w1l = W.w1l; n.w2ph = W.w2ph; n.w2pl = W.w2pl; n.w2th = W.w2th; n.w2tl = W.w2tl;
     n.sc = W.sc; n.dzmax = W.dzmax;
+  }
+  w.weight_bytes = o;
+  for (int net = 0; net < 2; ++net) {
+    const int An = net == 0 ? A : 1;
+    SfNet& n = w.n[net];
     n.dz2t = (float*)take(4LL * M * HID);
     n.part_w1 = (float*)take(4LL * w.blocks * HID * D);
     n.part_b1 = (float*)take(4LL * w.blocks * HID);
@@ -291,6 +298,20 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   w.stat64 = (double*)take(8 * 8);
   w.bytes = o;
   return w;
+}
+
+static int sf_prep(const rlks_mlp_desc* d, const SfWs& w, const float* params, hipStream_t s) {
+  const int D = d->obs_dim;
+  const Layout L = make_layout(D, HID, d->n_actions);
+  SfPrepArgs pa{};
+  pa.D = D;
+  pa.KD = sf_kd(D);
+  for (int net = 0; net < 2; ++net) {
+    pa.n[net] = w.w[net];
+    const NetPtrs P = net_ptrs_host(params, L, net);
+    pa.n[net].w1 = P.w1; pa.n[net].b1 = P.b1; pa.n[net].w2 = P.w2;
+  }
+  return launch_sf_prep(pa, s);
 }
 
 static int check_desc(const rlks_mlp_desc* d) {
@@ -384,17 +405,8 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
   RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_ppo_grad: workspace too small");
   const Layout L = make_layout(D, H, A);
   const bool f_pi = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_PI), f_vf = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_VF);
-  if (phases & (RLKS_PHASE_FWD | RLKS_PHASE_PREP)) {
-    SfPrepArgs pa{};
-    pa.D = D;
-    pa.KD = sf_kd(D);
-    for (int net = 0; net < 2; ++net) {
-      pa.n[net] = w.w[net];
-      const NetPtrs P = net_ptrs_host(params, L, net);
-      pa.n[net].w1 = P.w1; pa.n[net].b1 = P.b1; pa.n[net].w2 = P.w2;
-    }
-    if (int rc = launch_sf_prep(pa, s)) return rc;
-  }
+  if (phases & (RLKS_PHASE_FWD | RLKS_PHASE_PREP))
+    if (int rc = sf_prep(d, w, params, s)) return rc;
   SfArgs a{};
   a.x = mb; a.x_stride = mb_stride(D, A); a.M = M; a.D = D; a.A_pi = A;
   a.tiles_per_split = w.tiles_per_split; a.co = *co; a.dyn = dyn;
@@ -564,6 +576,42 @@ int rlks_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, con
   v.P = net_ptrs_host(params, L, 1);
   v.x = b->obs; v.x_stride = D; v.M = (b->T + 1) * N; v.D = D; v.A_pi = A; v.out = b->values;
   return launch_fwd_head(v, 1, A, FWD_ONLY, s);
+}
+
+int rlks_rollout_ws(rlks_env* env, const rlks_mlp_desc* d, const float* params, const rlks_rollout_bufs* b,
+                    int explore, void* workspace, int64_t ws_bytes, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  if (d->precision != RLKS_PRECISION_SF16) return rlks_rollout(env, d, params, b, explore, stream);
+  RLKS_REQUIRE(env && params && b && b->T > 0 && b->N > 0 && workspace, RLKS_ERR_ARG, "rlks_rollout_ws: bad argument");
+  rlks_env_cfg cfg;
+  rlks_env_config(env, &cfg);
+  RLKS_REQUIRE(cfg.n_envs == b->N && 3 * cfg.n_clouds == d->obs_dim && cfg.n_clouds == d->n_actions,
+               RLKS_ERR_ARG, "rlks_rollout_ws: env / policy / buffer shapes disagree");
+  RLKS_REQUIRE(cfg.nodes_per_cluster == 0, RLKS_ERR_UNSUPPORTED,
+               "rlks_rollout_ws: fused rollout covers the table env; node-level envs step through rlks_env_step");
+  const int N = b->N, D = d->obs_dim, A = d->n_actions;
+  const SfWs w = sf_ws_layout(D, A, 0, (char*)workspace);
+  RLKS_REQUIRE(ws_bytes >= w.weight_bytes, RLKS_ERR_ARG, "rlks_rollout_ws: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  if (int rc = sf_prep(d, w, params, s)) return rc;
+  const Layout L = make_layout(D, HID, A);
+  SfRollArgs a{};
+  for (int net = 0; net < 2; ++net) {
+    const NetPtrs P = net_ptrs_host(params, L, net);
+    a.n[net] = SfRollNet{w.w[net].w1h, w.w[net].w1l, w.w[net].w2rh, w.w[net].w2rl, P.b2, P.w3, P.b3, w.w[net].sc};
+  }
+  a.M = N; a.D = D; a.A = A; a.T = b->T;
+  a.env = view(env); a.tab_cost = env->d_cost; a.tab_lat = env->d_lat; a.explore = explore;
+  // one launch: per step both nets' forward of obs[t] (logits[t], values[t]), sample, env step ->
+  // obs[t + 1]; step T writes the bootstrap V(obs[T])
+  a.x = b->obs;
+  a.logits = b->logits;
+  a.values = b->values;
+  a.logp = b->logp;
+  a.actions = b->actions;
+  a.rewards = b->rewards;
+  a.dones = b->dones;
+  return launch_sf_roll(a, FWD_ROLLOUT, s);
 }
 
 }  // extern "C"

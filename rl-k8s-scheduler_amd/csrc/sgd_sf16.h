@@ -8,6 +8,7 @@ namespace rlks {
 struct SfNetW {
   const float *w1, *b1, *w2;
   _Float16 *w1h, *w1l, *w2ph, *w2pl, *w2th, *w2tl;
+  _Float16 *w2rh, *w2rl;  // rollout: w2p in wave-fragment order [q 4][kt 8][s 2][i 2][64 lanes][8]
   float* sc;          // [8]: s_w1, 1/s_w1, s_w2, 1/s_w2, e_w1, e_w2
   float* pmax;        // [32] per-block max |w| (16 over W2, 16 over W1a)
   unsigned* dzmax;    // zeroed here (F1 atomicMax)
@@ -36,6 +37,31 @@ struct SfArgs {
   rlks_ppo_coeffs co;
   const float* dyn;
 };
+
+// rollout step on split-fp16 (rollout_sf16.hip): both nets' forward + sample + env step
+struct SfRollNet {
+  const _Float16 *w1h, *w1l, *w2rh, *w2rl;
+  const float *b2, *w3, *b3;
+  const float* sc;
+};
+struct SfRollArgs {
+  SfRollNet n[2];
+  float* x;        // FWD_ONLY: [M][D] observations; FWD_ROLLOUT: obs [T+1][M][D] (obs[0] read)
+  int M, D, A, T;  // T: rollout steps (FWD_ROLLOUT); buffers below are time-major [T(+1)][M]
+  float* logits;   // [(T)][M][A] or null
+  float* values;   // [(T+1)][M] or null
+  // FWD_ROLLOUT: sample, step the env lane m = row m
+  EnvView env;
+  const double* tab_cost;
+  const double* tab_lat;
+  int explore;
+  float* obs_next;
+  float* logp;
+  int32_t* actions;
+  float* rewards;
+  uint8_t* dones;
+};
+int launch_sf_roll(const SfRollArgs& a, int mode, hipStream_t s);
 
 size_t sf_f1_lds_bytes(int A_, int NG, int KD, int W);
 int sf_kd(int D);

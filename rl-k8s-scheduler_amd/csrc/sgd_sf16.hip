@@ -166,6 +166,16 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
     split1(N.w2[src * HID + row] * s2, a, b);  // w2t[k = row][n perm]
     N.w2th[i] = a;
     N.w2tl[i] = b;
+    if (N.w2rh) {  // rollout copy: i = ((((q 8 + kt) 2 + s) 2 + ii) 64 + lane) 8 + j -> w2p[n][32kt+16s+8h+j]
+      const int j = i & 7, lane = (i >> 3) & 63, ii = (i >> 9) & 1, ss = (i >> 10) & 1, kt = (i >> 11) & 7,
+                q = i >> 14;
+      const int n = 32 * (2 * q + ii) + (lane & 31), kk = 32 * kt + 16 * ss + 8 * (lane >> 5) + j;
+      const int src2 = 32 * kt + sf_perm(ss, lane >> 5, j);
+      (void)kk;
+      split1(N.w2[n * HID + src2] * s2, a, b);
+      N.w2rh[i] = a;
+      N.w2rl[i] = b;
+    }
     if (i < HID * KD) {
       const int k = i / KD, d = i - k * KD;
       const float v = d < D ? N.w1[k * D + d] : (d == D ? N.b1[k] : 0.f);

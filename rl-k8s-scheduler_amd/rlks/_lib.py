@@ -85,6 +85,7 @@ SIGNATURES = {
     "rlks_mlp_layout": [C.POINTER(MlpDesc), C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64)],
     "rlks_policy_forward": [C.POINTER(MlpDesc), _P, _P, _I, _P, _P, _P],
     "rlks_rollout": [_P, C.POINTER(MlpDesc), _P, C.POINTER(RolloutBufs), _I, _P],
+    "rlks_rollout_ws": [_P, C.POINTER(MlpDesc), _P, C.POINTER(RolloutBufs), _I, _P, _I64, _P],
     "rlks_minibatch_stride": [C.POINTER(MlpDesc)],
     "rlks_ppo_gather": [C.POINTER(MlpDesc), C.POINTER(RolloutBufs), C.c_uint64, _I, _I64, _I, _P, _P, _P],
     "rlks_ppo_workspace_bytes": [C.POINTER(MlpDesc), _I, C.POINTER(_I64)],

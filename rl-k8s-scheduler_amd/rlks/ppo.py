@@ -259,8 +259,10 @@ class PPO:
     def rollout(self, explore=True):
         s = self.stream
         b = self.buf
-        _lib.call("rlks_rollout", self.env.handle, C.byref(self.params.desc), _lib.ptr(self.params.flat),
-                  C.byref(self.bufs), int(explore), s)
+        # sf16: one split-fp16 launch per step computes both nets (values included) and steps the
+        # env; the split weights live in the SGD workspace
+        _lib.call("rlks_rollout_ws", self.env.handle, C.byref(self.params.desc), _lib.ptr(self.params.flat),
+                  C.byref(self.bufs), int(explore), _lib.ptr(self.ws), self.ws.numel(), s)
 
     def advantages(self):
         s = self.stream

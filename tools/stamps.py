@@ -18,7 +18,33 @@ sys.path.insert(0, str(ROOT / "rl-k8s-scheduler_amd"))
 PHASES = ["prologue", "Z2 loop", "head+loss", "dW3/stats", "dZ2 store+split", "dH1 loop", "epilogue"]
 
 
+def roll():
+    """phase clocks of the split-fp16 rollout step kernel (k_sf_roll), c2 shapes"""
+    import torch
+    from rlks import _lib
+    from rlks.ppo import PPO, PPOConfig
+
+    cfg = PPOConfig().training(train_batch_size=4096 * 128, sgd_minibatch_size=65536, num_sgd_iter=1)
+    cfg.num_envs = 4096
+    cfg.rollout_fragment_length = 128
+    algo = PPO(config=cfg, device=torch.device("cuda", 0))
+    for _ in range(3):
+        algo.rollout()
+    torch.cuda.synchronize()
+    st = np.zeros((256, 2, 8), np.uint64)
+    assert _lib.lib().rlks_dbg_roll_stamps(st.ctypes.data_as(C.c_void_p)) == 0
+    s = st[:128].astype(np.int64)
+    names = ["X split", "phase 1 (H1^T) + barrier", "phase 2 (Z2^T)", "phase 3 + barrier", "sample + env step"]
+    for wv, who in ((0, "wave 0 (pi)"), (1, "wave 4 (vf)")):
+        dt = np.diff(s[:, wv, :6], axis=1)
+        print(f"{who}:")
+        for i, n in enumerate(names[: 5 if wv == 0 else 4]):
+            print(f"  {n:26s} median {np.median(dt[:, i]):7.0f} cyc")
+
+
 def main():
+    if "--roll" in sys.argv:
+        return roll()
     import torch
     from rlks import _lib
     from rlks.policy import PolicyParams
