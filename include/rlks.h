@@ -154,6 +154,14 @@ typedef struct rlks_rollout_bufs {
  * V(obs[T]).  obs[0] must hold the current observations. */
 int rlks_rollout(rlks_env* env, const rlks_mlp_desc* desc, const float* params_dev,
                  const rlks_rollout_bufs* bufs, int explore, void* stream);
+/* Policy / value forward with a workspace (rlks_ppo_workspace_bytes for >= n rows): required for
+ * the generic-width path (RLKS_PRECISION_WIDE or shapes outside the fused kernels). */
+int rlks_policy_forward_ws(const rlks_mlp_desc* desc, const float* params_dev, const float* obs_dev, int n,
+                           float* logits_dev, float* values_dev, void* workspace, int64_t ws_bytes, void* stream);
+/* Generic split-fp16 GEMM of the wide-MLP path (config c5); see rlks_gemm_desc. */
+int rlks_gemm_sf16(const rlks_gemm_desc* desc, void* stream);
+/* atomicMax of max |x| over x[rows][cols] (row stride ld) into *slot (caller zeroes the slot). */
+int rlks_absmax(const float* x, int rows, int cols, int ld, uint32_t* slot, void* stream);
 /* Same rollout; with desc->precision == RLKS_PRECISION_SF16 it runs the split-fp16 step kernel
  * (both nets' forward + sample + env step per launch, values written per step, V(obs[T]) last)
  * with the split weights in `workspace` (an rlks_ppo_workspace_bytes-sized buffer: the SGD step's

@@ -71,8 +71,31 @@ typedef struct rlks_mlp_desc {
  * <= ~2^-21 per product, measured below the fp32 chain's) at 16x the fp32 matrix rate. */
 enum {
   RLKS_PRECISION_FP32 = 0,
-  RLKS_PRECISION_SF16 = 1
+  RLKS_PRECISION_SF16 = 1,
+  RLKS_PRECISION_WIDE = 2  /* generic split-fp16 GEMM path (wide_mlp.hip): any width, node envs;
+                              chosen automatically when the fused 256-unit kernels do not fit */
 };
+
+/* One split-fp16 GEMM (fp32 in / fp32 out, fp32-accurate): C = epi(op(A) op(B)), op = transpose
+ * when trans_*; operand scales come from max|x| slots (uint bits of a non-negative float). */
+enum {
+  RLKS_GEMM_STORE = 0,     /* C = acc */
+  RLKS_GEMM_TANH_BIAS = 1, /* C = tanh(acc + bias[n]) */
+  RLKS_GEMM_BIAS = 2,      /* C = acc + bias[n] */
+  RLKS_GEMM_DTANH = 3      /* C = acc * (1 - aux[m][n]^2) */
+};
+typedef struct rlks_gemm_desc {
+  const float* a;
+  const float* b;
+  float* c;
+  const float* bias;
+  const float* aux;
+  int32_t m, n, k, lda, ldb, ldc, ldaux;
+  int32_t trans_a, trans_b, epilogue, accumulate, reserved;
+  const uint32_t* a_max;
+  const uint32_t* b_max;
+  uint32_t* c_max;         /* optional (NULL): atomicMax of |C| */
+} rlks_gemm_desc;
 
 /* PPO loss coefficients that stay fixed for a run (RLlib PPOConfig names and defaults) */
 typedef struct rlks_ppo_coeffs {

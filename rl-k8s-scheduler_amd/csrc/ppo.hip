@@ -8,6 +8,7 @@
 #include <cmath>
 
 #include "sgd_sf16.h"
+#include "wide_mlp.h"
 
 namespace rlks {
 
@@ -314,14 +315,20 @@ static int sf_prep(const rlks_mlp_desc* d, const SfWs& w, const float* params, h
   return launch_sf_prep(pa, s);
 }
 
+static bool is_wide(const rlks_mlp_desc* d) { return d->precision == RLKS_PRECISION_WIDE || wide_needed(d); }
+
+// the fused kernels (mlp_fwd / mlp_bwd / sgd_sf16 / rollout_sf16) cover hidden 256, obs < 32 and
+// 2 / 4 / 8 actions; everything else runs on the generic-width path (wide_mlp.hip)
 static int check_desc(const rlks_mlp_desc* d) {
   RLKS_REQUIRE(d, RLKS_ERR_ARG, "null mlp desc");
-  RLKS_REQUIRE(d->obs_dim > 0 && d->obs_dim <= DMAX, RLKS_ERR_UNSUPPORTED, "obs_dim must be in [1, 32]");
-  RLKS_REQUIRE(d->n_actions == 2 || d->n_actions == 4 || d->n_actions == 8, RLKS_ERR_UNSUPPORTED,
-               "n_actions must be 2, 4 or 8");
-  RLKS_REQUIRE(d->hidden == HID, RLKS_ERR_UNSUPPORTED, "fused MLP kernels are built for hidden = 256");
-  RLKS_REQUIRE(d->precision == RLKS_PRECISION_FP32 || d->precision == RLKS_PRECISION_SF16, RLKS_ERR_ARG,
-               "unknown precision");
+  RLKS_REQUIRE(d->precision == RLKS_PRECISION_FP32 || d->precision == RLKS_PRECISION_SF16 ||
+                   d->precision == RLKS_PRECISION_WIDE, RLKS_ERR_ARG, "unknown precision");
+  RLKS_REQUIRE(d->obs_dim > 0 && d->hidden > 0 && d->hidden % 32 == 0 && d->hidden <= 8192 && d->n_actions > 0 &&
+                   d->n_actions <= 64, RLKS_ERR_UNSUPPORTED,
+               "MLP: hidden must be a multiple of 32 (<= 8192), 1 <= n_actions <= 64");
+  if (!is_wide(d))
+    RLKS_REQUIRE(d->obs_dim <= DMAX && (d->n_actions == 2 || d->n_actions == 4 || d->n_actions == 8),
+                 RLKS_ERR_UNSUPPORTED, "fused MLP kernels: obs_dim in [1, 32], 2, 4 or 8 actions");
   return RLKS_OK;
 }
 
@@ -344,6 +351,7 @@ int rlks_mlp_layout(const rlks_mlp_desc* d, int64_t* offsets, int64_t* padded, i
 int rlks_policy_forward(const rlks_mlp_desc* d, const float* params, const float* obs, int n, float* logits,
                         float* values, void* stream) {
   if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(!is_wide(d), RLKS_ERR_UNSUPPORTED, "rlks_policy_forward: this MLP needs rlks_policy_forward_ws");
   RLKS_REQUIRE(params && obs && n >= 0, RLKS_ERR_ARG, "rlks_policy_forward: bad argument");
   if (n == 0) return RLKS_OK;
   const Layout L = make_layout(d->obs_dim, d->hidden, d->n_actions);
@@ -382,8 +390,24 @@ int rlks_ppo_gather(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, uint64_t
   return RLKS_OK;
 }
 
+int rlks_policy_forward_ws(const rlks_mlp_desc* d, const float* params, const float* obs, int n, float* logits,
+                           float* values, void* workspace, int64_t ws_bytes, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  if (!is_wide(d)) return rlks_policy_forward(d, params, obs, n, logits, values, stream);
+  RLKS_REQUIRE(params && obs && n >= 0 && workspace, RLKS_ERR_ARG, "rlks_policy_forward_ws: bad argument");
+  if (n == 0) return RLKS_OK;
+  const WideWs w = wide_ws_layout(d->obs_dim, d->hidden, d->n_actions, n, (char*)workspace);
+  RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_policy_forward_ws: workspace too small");
+  return wide_forward(d, params, obs, d->obs_dim, n, w, logits, values, (hipStream_t)stream);
+}
+
 int rlks_ppo_workspace_bytes(const rlks_mlp_desc* d, int rows, int64_t* bytes) {
   if (int rc = check_desc(d)) return rc;
+  if (is_wide(d)) {
+    RLKS_REQUIRE(bytes && rows > 0, RLKS_ERR_ARG, "rlks_ppo_workspace_bytes: bad argument");
+    *bytes = wide_ws_layout(d->obs_dim, d->hidden, d->n_actions, rows, nullptr).bytes;
+    return RLKS_OK;
+  }
   if (d->precision == RLKS_PRECISION_SF16) {
     RLKS_REQUIRE(bytes && rows > 0 && rows % 256 == 0, RLKS_ERR_ARG,
                  "rlks_ppo_workspace_bytes: split-fp16 rows must be a positive multiple of 256");
@@ -451,6 +475,13 @@ int rlks_ppo_grad_phases(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, cons
                          const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes,
                          int phases, void* stream) {
   if (int rc = check_desc(d)) return rc;
+  if (is_wide(d)) {
+    RLKS_REQUIRE(co && params && dyn && mb && grad && workspace && M > 0, RLKS_ERR_ARG, "rlks_ppo_grad: bad argument");
+    const WideWs w = wide_ws_layout(d->obs_dim, d->hidden, d->n_actions, M, (char*)workspace);
+    RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_ppo_grad: workspace too small");
+    (void)phases;
+    return wide_grad(d, co, params, dyn, mb, M, grad, stats, w, (hipStream_t)stream);
+  }
   if (d->precision == RLKS_PRECISION_SF16) {
     RLKS_REQUIRE(co && params && dyn && mb && grad && workspace, RLKS_ERR_ARG, "rlks_ppo_grad: null argument");
     return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, phases, (hipStream_t)stream);
@@ -546,6 +577,7 @@ int rlks_kl_update(float* dyn, const double* kc, float target, void* stream) {
 int rlks_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, const rlks_rollout_bufs* b,
                  int explore, void* stream) {
   if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(!is_wide(d), RLKS_ERR_UNSUPPORTED, "rlks_rollout: this MLP / env needs rlks_rollout_ws");
   RLKS_REQUIRE(env && params && b && b->T > 0 && b->N > 0, RLKS_ERR_ARG, "rlks_rollout: bad argument");
   rlks_env_cfg cfg;
   rlks_env_config(env, &cfg);
@@ -581,6 +613,16 @@ int rlks_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, con
 int rlks_rollout_ws(rlks_env* env, const rlks_mlp_desc* d, const float* params, const rlks_rollout_bufs* b,
                     int explore, void* workspace, int64_t ws_bytes, void* stream) {
   if (int rc = check_desc(d)) return rc;
+  if (is_wide(d)) {
+    RLKS_REQUIRE(env && params && b && b->T > 0 && b->N > 0 && workspace, RLKS_ERR_ARG, "rlks_rollout_ws: bad argument");
+    rlks_env_cfg cfg;
+    rlks_env_config(env, &cfg);
+    RLKS_REQUIRE(cfg.n_envs == b->N && 3 * cfg.n_clouds == d->obs_dim && cfg.n_clouds == d->n_actions && cfg.autoreset,
+                 RLKS_ERR_ARG, "rlks_rollout_ws: env / policy / buffer shapes disagree (autoreset lanes required)");
+    const WideWs w = wide_ws_layout(d->obs_dim, d->hidden, d->n_actions, b->N, (char*)workspace);
+    RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_rollout_ws: workspace too small");
+    return wide_rollout(env, d, params, b, explore, w, (hipStream_t)stream);
+  }
   if (d->precision != RLKS_PRECISION_SF16) return rlks_rollout(env, d, params, b, explore, stream);
   RLKS_REQUIRE(env && params && b && b->T > 0 && b->N > 0 && workspace, RLKS_ERR_ARG, "rlks_rollout_ws: bad argument");
   rlks_env_cfg cfg;

@@ -746,20 +746,28 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   store(0);
   if (t0 + 1 < t1) load(t0 + 1);
   __syncthreads();
+  // X rows of the next tile are loaded one iteration ahead (their latency hides behind the MFMAs)
+  float xnext[KS * 8];
+  auto load_x = [&](int t) {
+    const float* xr = g.x + (size_t)(t * 32 + r) * stride;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = 16 * ks + 8 * h + j;
+        xnext[ks * 8 + j] = d < D ? xr[d] : (d == D ? 1.f : 0.f);
+      }
+  };
+  load_x(t0);
   for (int t = t0; t < t1; ++t) {
     const int buf = (t - t0) & 1;
     // H1 tile (rows m in registers, columns k = 32w + r on lanes) as the B operand
     h8 bh[2], bl[2];
     {
       float xv[KS * 8];
-      const float* xr = g.x + (size_t)(t * 32 + r) * stride;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int d = 16 * ks + 8 * h + j;
-          xv[ks * 8 + j] = d < D ? xr[d] : (d == D ? 1.f : 0.f);
-        }
+      for (int i = 0; i < KS * 8; ++i) xv[i] = xnext[i];
+      load_x(t + 1 < t1 ? t + 1 : t);
       float xm = 0.f;
 #pragma unroll
       for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));

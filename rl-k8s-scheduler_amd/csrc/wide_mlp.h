@@ -1,0 +1,31 @@
+// wide_mlp.h — the generic-width PPO MLP path (wide_mlp.hip) over the split-fp16 GEMM.
+#pragma once
+
+#include "mlp_common.h"
+
+namespace rlks {
+
+struct WideNet {
+  float *h1, *h2, *out, *dout;  // [M][H], [M][H], [M][A_net], [M][A_net]
+  unsigned* slots;              // operand max |x| slots
+  float* part_stat;             // [blocks][4]
+};
+struct WideWs {
+  WideNet n[2];
+  float *dza, *dzb;  // [M][H] dZ2 / dZ1
+  double* rew64;     // [M] env-step scratch (rollout)
+  unsigned* stat_slots;
+  int64_t bytes;
+  int M, blocks;
+};
+
+bool wide_needed(const rlks_mlp_desc* d);
+WideWs wide_ws_layout(int D, int H, int A, int M, char* base);
+int wide_forward(const rlks_mlp_desc* d, const float* params, const float* x, int ldx, int M, const WideWs& w,
+                 float* logits, float* values, hipStream_t s);
+int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
+              const float* mb, int M, float* grad, double* stats, const WideWs& w, hipStream_t s);
+int wide_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, const rlks_rollout_bufs* b, int explore,
+                 const WideWs& w, hipStream_t s);
+
+}  // namespace rlks

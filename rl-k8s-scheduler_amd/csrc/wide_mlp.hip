@@ -1,0 +1,310 @@
+// wide_mlp.hip — the PPO policy/value MLP for widths the fused 256-unit kernels do not cover:
+// config c5 (64 clusters x 1,024 nodes, obs 3 x 64 = 192, 64 actions, fcnet_hiddens
+// [2048, 2048], "MFMA-bound update").  Every layer is a split-fp16 GEMM (gemm_sf16.hip, fp32-
+// accurate) with the activation or its derivative fused into the epilogue; activations H1, H2 are
+// materialised in HBM (M x 2048 fp32 each), which at this width is a small fraction of the GEMM
+// time.  Same RLlib semantics as the fused path (mlp_fwd.hip / sgd_sf16.hip): FCNet tanh, separate
+// value net, PPO clipped surrogate + KL + clipped value loss + entropy (train_ppo.py:9-31).
+//
+// Per net and SGD step (M minibatch rows; W1 [H][D], W2 [H][H], W3 [A][H] torch layouts):
+//   H1 = tanh(X W1^T + b1)   H2 = tanh(H1 W2^T + b2)   out = H2 W3^T + b3          (NT GEMMs)
+//   k_wide_loss: dout [M][A] (+ per-block loss stats)
+//   dW3 = dout^T H2 (TN)   db3 = colsum(dout)
+//   dZ2 = (dout W3) * (1 - H2^2) (NN, fused)   dW2 = dZ2^T H1 (TN)   db2 = colsum(dZ2)
+//   dZ1 = (dZ2 W2) * (1 - H1^2) (NN, fused)    dW1 = dZ1^T X  (TN)   db1 = colsum(dZ1)
+// Operand scales: max |x| slots filled by rlks_absmax (X, weights) or by the producing GEMM's
+// epilogue (H1, H2, dZ2, dZ1), the loss kernel (dout).
+#include "wide_mlp.h"
+
+#include "gemm_sf16.h"
+
+namespace rlks {
+
+constexpr int WIDE_MAXA = 64;
+constexpr int LOSS_ROWS = 256;  // rows per loss block (stats partials)
+
+enum { SL_X = 0, SL_W1, SL_W2, SL_W3, SL_H1, SL_H2, SL_DOUT, SL_DZ2, SL_DZ1, SL_N = 16 };
+
+WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
+  WideWs w{};
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    char* p = base ? base + o : nullptr;
+    o += (bytes + 255) / 256 * 256;
+    return p;
+  };
+  w.M = M;
+  w.blocks = (M + LOSS_ROWS - 1) / LOSS_ROWS;
+  for (int net = 0; net < 2; ++net) {
+    const int An = net == 0 ? A : 1;
+    WideNet& n = w.n[net];
+    n.h1 = (float*)take(4LL * M * H);
+    n.h2 = (float*)take(4LL * M * H);
+    n.out = (float*)take(4LL * M * An);
+    n.dout = (float*)take(4LL * M * An);
+    n.slots = (unsigned*)take(4 * SL_N);
+    n.part_stat = (float*)take(4LL * w.blocks * 4);
+  }
+  w.dza = (float*)take(4LL * M * H);
+  w.dzb = (float*)take(4LL * M * H);
+  w.rew64 = (double*)take(8LL * M);
+  w.stat_slots = (unsigned*)take(4 * 4);
+  w.bytes = o;
+  return w;
+}
+
+bool wide_needed(const rlks_mlp_desc* d) { return d->hidden != HID || d->n_actions > 8 || d->obs_dim + 1 > 32; }
+
+// ----------------------------------------------------------------------------- kernels
+// PPO loss per row (same math as k_sf_fwdbwd's, for up to 64 actions); dout -> HBM, per-block
+// stats [policy loss, vf loss, kl, entropy], max |dout| -> slot
+template <int NET>
+__global__ __launch_bounds__(LOSS_ROWS) void k_wide_loss(const float* __restrict__ out, const float* __restrict__ x,
+                                                       int stride, int M, int D, int A, rlks_ppo_coeffs co,
+                                                       const float* __restrict__ dyn, float* __restrict__ dout,
+                                                       float* __restrict__ part_stat, unsigned* __restrict__ dmax) {
+  __shared__ float red[4][LOSS_ROWS / 64];
+  const int m = blockIdx.x * LOSS_ROWS + threadIdx.x;
+  float st[4] = {0.f, 0.f, 0.f, 0.f};
+  float mx_d = 0.f;
+  if (m < M) {
+    const float* rec = x + (size_t)m * stride;
+    const float inv_count = dyn[RLKS_DYN_INV_COUNT];
+    if (NET == 0) {
+      const float* lg = out + (size_t)m * A;
+      const float* lo = rec + D;
+      const float adv = (rec[D + A] - dyn[RLKS_DYN_ADV_MEAN]) * dyn[RLKS_DYN_ADV_INVSTD];
+      const float logp_old = rec[D + A + 2];
+      const int act = (int)rec[D + A + 3];
+      float mx = lg[0], mo = lo[0];
+      for (int a = 1; a < A; ++a) { mx = fmaxf(mx, lg[a]); mo = fmaxf(mo, lo[a]); }
+      float se = 0.f, so = 0.f;
+      for (int a = 0; a < A; ++a) { se += expf(lg[a] - mx); so += expf(lo[a] - mo); }
+      const float lse = mx + logf(se), lso = mo + logf(so);
+      float kl = 0.f, ent = 0.f;
+      for (int a = 0; a < A; ++a) {
+        const float lp = lg[a] - lse, p = expf(lp), lpo = lo[a] - lso, po = expf(lpo);
+        kl += po * (lpo - lp);
+        ent -= p * lp;
+      }
+      const float lpa = lg[act] - lse;
+      const float ratio = expf(lpa - logp_old);
+      const float lo_c = 1.f - co.clip_param, hi_c = 1.f + co.clip_param;
+      const float rc = fminf(fmaxf(ratio, lo_c), hi_c);
+      const float s1 = adv * ratio, s2 = adv * rc;
+      const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+      const float inr = (ratio >= lo_c && ratio <= hi_c) ? 1.f : 0.f;
+      const float dr = -adv * (w1 + (1.f - w1) * inr) * ratio;
+      const float klc = dyn[RLKS_DYN_KL_COEFF];
+      for (int a = 0; a < A; ++a) {
+        const float lp = lg[a] - lse, p = expf(lp), po = expf(lo[a] - lso);
+        float d = dr * ((a == act ? 1.f : 0.f) - p);
+        d += klc * (p - po);
+        d += co.entropy_coeff * p * (lp + ent);
+        d *= inv_count;
+        dout[(size_t)m * A + a] = d;
+        mx_d = fmaxf(mx_d, fabsf(d));
+      }
+      st[0] = -fminf(s1, s2);
+      st[2] = kl;
+      st[3] = ent;
+    } else {
+      const float diff = out[m] - rec[D + A + 1];
+      const float sq = diff * diff;
+      st[1] = fminf(sq, co.vf_clip_param);
+      const float d = (sq <= co.vf_clip_param) ? co.vf_loss_coeff * 2.f * diff * inv_count : 0.f;
+      dout[m] = d;
+      mx_d = fabsf(d);
+    }
+  }
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float s = wave_sum(st[i]);
+    if (l == 0) red[i][w] = s;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx_d = fmaxf(mx_d, __shfl_xor(mx_d, o, 64));
+  if (l == 0) atomicMax(dmax, __float_as_uint(mx_d));
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float s = 0.f;
+    for (int j = 0; j < LOSS_ROWS / 64; ++j) s += red[threadIdx.x][j];
+    part_stat[(size_t)blockIdx.x * 4 + threadIdx.x] = s;
+  }
+}
+
+// stats[RLKS_STAT_*] from the per-block partials of both nets (fixed order, f64)
+__global__ void k_wide_stats(const float* __restrict__ ps_pi, const float* __restrict__ ps_vf, int blocks, int rows,
+                             double* __restrict__ stats) {
+  const int i = threadIdx.x;
+  if (i >= 4) return;
+  const float* p = i == 1 ? ps_vf : ps_pi;
+  double s = 0.0;
+  for (int b = 0; b < blocks; ++b) s += (double)p[(size_t)b * 4 + i];
+  stats[i] = s;
+  if (i == 0) {
+    stats[RLKS_STAT_ROWS] = (double)rows;
+    stats[5] = stats[6] = stats[7] = 0.0;
+  }
+}
+
+// TorchCategorical over A logits for every lane (Philox counter = lane / episode / step, as the
+// fused rollout kernels): action and its log-probability
+__global__ void k_wide_sample(EnvView v, const float* __restrict__ logits, int A, int explore,
+                              int32_t* __restrict__ actions, float* __restrict__ logp) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= v.N) return;
+  const float* lg = logits + (size_t)m * A;
+  float mx = lg[0];
+  int amax = 0;
+  for (int a = 1; a < A; ++a)
+    if (lg[a] > mx) { mx = lg[a]; amax = a; }
+  float se = 0.f;
+  for (int a = 0; a < A; ++a) se += expf(lg[a] - mx);
+  int act = amax;
+  if (explore) {
+    const u32x4 x = philox4x32_10(u32x4{(uint32_t)(v.env_offset + m), (uint32_t)v.episode[m], (uint32_t)v.step[m],
+                                        (uint32_t)RLKS_PURPOSE_ACTION << 16},
+                                  v.k0, v.k1);
+    const float u = (float)u53(x.x, x.y) * se;
+    float c = 0.f;
+    act = A - 1;
+    for (int a = 0; a < A; ++a) {
+      c += expf(lg[a] - mx);
+      if (u < c) { act = a; break; }
+    }
+  }
+  actions[m] = act;
+  logp[m] = lg[act] - mx - logf(se);
+}
+
+// ----------------------------------------------------------------------------- host
+namespace {
+
+struct Net {
+  const float *w1, *b1, *w2, *b2, *w3, *b3;
+};
+
+Net net_of(const float* params, const Layout& L, int net) {
+  const NetPtrs P = net_ptrs_host(params, L, net);
+  return Net{P.w1, P.b1, P.w2, P.b2, P.w3, P.b3};
+}
+
+int gemm(const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C, int ldc, int M, int N, int K,
+         int epi, const float* bias, const float* aux, int ldaux, const unsigned* amax, const unsigned* bmax,
+         unsigned* cmax, hipStream_t s) {
+  GemmArgs g{};
+  g.A = A; g.B = B; g.C = C; g.bias = bias; g.aux = aux;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldaux = ldaux;
+  g.ta = ta; g.tb = tb; g.epi = epi; g.accumulate = 0;
+  g.amax = amax; g.bmax = bmax; g.cmax = cmax;
+  return launch_gemm_sf16(g, s);
+}
+
+// forward of net `net` over M rows of x (row stride ldx): H1, H2 and out in the workspace
+int forward_net(const rlks_mlp_desc* d, const Net& P, const WideNet& n, const float* x, int ldx, int M, int net,
+                hipStream_t s) {
+  const int D = d->obs_dim, H = d->hidden, An = net == 0 ? d->n_actions : 1;
+  unsigned* sl = n.slots;
+  if (int rc = launch_absmax(x, M, D, ldx, sl + SL_X, s)) return rc;
+  if (int rc = launch_absmax(P.w1, H, D, D, sl + SL_W1, s)) return rc;
+  if (int rc = launch_absmax(P.w2, H, H, H, sl + SL_W2, s)) return rc;
+  if (int rc = launch_absmax(P.w3, An, H, H, sl + SL_W3, s)) return rc;
+  if (int rc = gemm(x, ldx, 0, P.w1, D, 1, n.h1, H, M, H, D, GEMM_TANH_BIAS, P.b1, nullptr, 0, sl + SL_X,
+                    sl + SL_W1, sl + SL_H1, s))
+    return rc;
+  if (int rc = gemm(n.h1, H, 0, P.w2, H, 1, n.h2, H, M, H, H, GEMM_TANH_BIAS, P.b2, nullptr, 0, sl + SL_H1,
+                    sl + SL_W2, sl + SL_H2, s))
+    return rc;
+  return gemm(n.h2, H, 0, P.w3, H, 1, n.out, An, M, An, H, GEMM_BIAS, P.b3, nullptr, 0, sl + SL_H2, sl + SL_W3,
+              nullptr, s);
+}
+
+}  // namespace
+
+int wide_forward(const rlks_mlp_desc* d, const float* params, const float* x, int ldx, int M, const WideWs& w,
+                 float* logits, float* values, hipStream_t s) {
+  const Layout L = make_layout(d->obs_dim, d->hidden, d->n_actions);
+  for (int net = 0; net < 2; ++net) {
+    float* dst = net == 0 ? logits : values;
+    if (!dst) continue;
+    const WideNet& n = w.n[net];
+    RLKS_HIP(hipMemsetAsync(n.slots, 0, 4 * SL_N, s));
+    if (int rc = forward_net(d, net_of(params, L, net), n, x, ldx, M, net, s)) return rc;
+    const int An = net == 0 ? d->n_actions : 1;
+    RLKS_HIP(hipMemcpyAsync(dst, n.out, sizeof(float) * M * An, hipMemcpyDeviceToDevice, s));
+  }
+  return RLKS_OK;
+}
+
+int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
+              const float* mb, int M, float* grad, double* stats, const WideWs& w, hipStream_t s) {
+  const int D = d->obs_dim, H = d->hidden, A = d->n_actions, stride = mb_stride(D, A);
+  const Layout L = make_layout(D, H, A);
+  for (int net = 0; net < 2; ++net) {
+    const int An = net == 0 ? A : 1;
+    const WideNet& n = w.n[net];
+    const Net P = net_of(params, L, net);
+    float* g = grad;
+    const int64_t* o = L.off + 6 * net;
+    unsigned* sl = n.slots;
+    RLKS_HIP(hipMemsetAsync(sl, 0, 4 * SL_N, s));
+    if (int rc = forward_net(d, P, n, mb, stride, M, net, s)) return rc;
+    if (net == 0)
+      hipLaunchKernelGGL(k_wide_loss<0>, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
+                         n.dout, n.part_stat, sl + SL_DOUT);
+    else
+      hipLaunchKernelGGL(k_wide_loss<1>, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
+                         n.dout, n.part_stat, sl + SL_DOUT);
+    RLKS_LAUNCHED();
+    // head: dW3 = dout^T H2, db3 = colsum(dout)
+    if (int rc = gemm(n.dout, An, 1, n.h2, H, 0, g + o[4], H, An, H, M, GEMM_STORE, nullptr, nullptr, 0,
+                      sl + SL_DOUT, sl + SL_H2, nullptr, s))
+      return rc;
+    if (int rc = launch_colsum(n.dout, M, An, An, g + o[5], 0, s)) return rc;
+    // dZ2 = (dout W3) (1 - H2^2); dW2 = dZ2^T H1; db2
+    if (int rc = gemm(n.dout, An, 0, P.w3, H, 0, w.dza, H, M, H, An, GEMM_DTANH, nullptr, n.h2, H, sl + SL_DOUT,
+                      sl + SL_W3, sl + SL_DZ2, s))
+      return rc;
+    if (int rc = gemm(w.dza, H, 1, n.h1, H, 0, g + o[2], H, H, H, M, GEMM_STORE, nullptr, nullptr, 0, sl + SL_DZ2,
+                      sl + SL_H1, nullptr, s))
+      return rc;
+    if (int rc = launch_colsum(w.dza, M, H, H, g + o[3], 0, s)) return rc;
+    // dZ1 = (dZ2 W2) (1 - H1^2); dW1 = dZ1^T X; db1
+    if (int rc = gemm(w.dza, H, 0, P.w2, H, 0, w.dzb, H, M, H, H, GEMM_DTANH, nullptr, n.h1, H, sl + SL_DZ2,
+                      sl + SL_W2, sl + SL_DZ1, s))
+      return rc;
+    if (int rc = gemm(w.dzb, H, 1, mb, stride, 0, g + o[0], D, H, D, M, GEMM_STORE, nullptr, nullptr, 0, sl + SL_DZ1,
+                      sl + SL_X, nullptr, s))
+      return rc;
+    if (int rc = launch_colsum(w.dzb, M, H, H, g + o[1], 0, s)) return rc;
+  }
+  if (stats) {
+    hipLaunchKernelGGL(k_wide_stats, dim3(1), dim3(64), 0, s, w.n[0].part_stat, w.n[1].part_stat, w.blocks, M, stats);
+    RLKS_LAUNCHED();
+  }
+  return RLKS_OK;
+}
+
+int wide_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, const rlks_rollout_bufs* b, int explore,
+                 const WideWs& w, hipStream_t s) {
+  const int N = b->N, D = d->obs_dim, A = d->n_actions;
+  RLKS_REQUIRE(w.M >= N, RLKS_ERR_ARG, "rlks_rollout_ws: workspace rows < envs");
+  const EnvView v = view(env);
+  for (int t = 0; t < b->T; ++t) {
+    const float* obs = b->obs + (size_t)t * N * D;
+    if (int rc = wide_forward(d, params, obs, D, N, w, b->logits + (size_t)t * N * A, b->values + (size_t)t * N, s))
+      return rc;
+    hipLaunchKernelGGL(k_wide_sample, dim3(cdiv(N, 256)), dim3(256), 0, s, v, b->logits + (size_t)t * N * A, A,
+                       explore, b->actions + (size_t)t * N, b->logp + (size_t)t * N);
+    RLKS_LAUNCHED();
+    if (int rc = rlks_env_step(env, b->actions + (size_t)t * N, b->obs + (size_t)(t + 1) * N * D, w.rew64,
+                               b->rewards + (size_t)t * N, b->dones + (size_t)t * N, nullptr, nullptr, nullptr, nullptr,
+                               s))
+      return rc;
+  }
+  return wide_forward(d, params, b->obs + (size_t)b->T * N * D, D, N, w, nullptr, b->values + (size_t)b->T * N, s);
+}
+
+}  // namespace rlks

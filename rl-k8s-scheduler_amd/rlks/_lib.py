@@ -22,7 +22,7 @@ RLKS_DYN_ADV_MEAN, RLKS_DYN_ADV_INVSTD, RLKS_DYN_KL_COEFF, RLKS_DYN_INV_COUNT = 
 RLKS_STAT_SIZE = 8
 RLKS_PHASE_FWD, RLKS_PHASE_DW2, RLKS_PHASE_DH1, RLKS_PHASE_REDUCE, RLKS_PHASE_ALL = 1, 2, 4, 8, 15
 RLKS_PHASE_FWD_PI, RLKS_PHASE_FWD_VF, RLKS_PHASE_PREP = 16, 32, 64
-RLKS_PRECISION_FP32, RLKS_PRECISION_SF16 = 0, 1
+RLKS_PRECISION_FP32, RLKS_PRECISION_SF16, RLKS_PRECISION_WIDE = 0, 1, 2
 RLKS_STAT_POLICY_LOSS, RLKS_STAT_VF_LOSS, RLKS_STAT_KL, RLKS_STAT_ENTROPY, RLKS_STAT_ROWS = 0, 1, 2, 3, 4
 
 
@@ -38,6 +38,17 @@ class EnvCfg(C.Structure):
         ("arrival_mode", C.c_int32), ("arrival_rate", C.c_double), ("depart_prob", C.c_double),
         ("init_occupancy", C.c_double), ("reject_penalty", C.c_double),
     ]
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [("a", C.c_void_p), ("b", C.c_void_p), ("c", C.c_void_p), ("bias", C.c_void_p), ("aux", C.c_void_p),
+                ("m", C.c_int32), ("n", C.c_int32), ("k", C.c_int32), ("lda", C.c_int32), ("ldb", C.c_int32),
+                ("ldc", C.c_int32), ("ldaux", C.c_int32), ("trans_a", C.c_int32), ("trans_b", C.c_int32),
+                ("epilogue", C.c_int32), ("accumulate", C.c_int32), ("reserved", C.c_int32),
+                ("a_max", C.c_void_p), ("b_max", C.c_void_p), ("c_max", C.c_void_p)]
+
+
+RLKS_GEMM_STORE, RLKS_GEMM_TANH_BIAS, RLKS_GEMM_BIAS, RLKS_GEMM_DTANH = 0, 1, 2, 3
 
 
 class MlpDesc(C.Structure):
@@ -85,6 +96,9 @@ SIGNATURES = {
     "rlks_mlp_layout": [C.POINTER(MlpDesc), C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64)],
     "rlks_policy_forward": [C.POINTER(MlpDesc), _P, _P, _I, _P, _P, _P],
     "rlks_rollout": [_P, C.POINTER(MlpDesc), _P, C.POINTER(RolloutBufs), _I, _P],
+    "rlks_gemm_sf16": [C.POINTER(GemmDesc), _P],
+    "rlks_absmax": [_P, _I, _I, _I, _P, _P],
+    "rlks_policy_forward_ws": [C.POINTER(MlpDesc), _P, _P, _I, _P, _P, _P, _I64, _P],
     "rlks_rollout_ws": [_P, C.POINTER(MlpDesc), _P, C.POINTER(RolloutBufs), _I, _P, _I64, _P],
     "rlks_minibatch_stride": [C.POINTER(MlpDesc)],
     "rlks_ppo_gather": [C.POINTER(MlpDesc), C.POINTER(RolloutBufs), C.c_uint64, _I, _I64, _I, _P, _P, _P],

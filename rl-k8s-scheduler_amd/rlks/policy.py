@@ -103,6 +103,21 @@ class PolicyParams:
         if values is None:
             values = torch.empty(n, dtype=torch.float32, device=obs.device)
         obs = obs.contiguous()
-        _lib.call("rlks_policy_forward", C.byref(self.desc), _lib.ptr(self.flat), _lib.ptr(obs), n,
-                  _lib.ptr(logits), _lib.ptr(values), torch.cuda.current_stream(obs.device).cuda_stream)
+        stream = torch.cuda.current_stream(obs.device).cuda_stream
+        if self.wide():  # generic-width path: needs a workspace for the activations
+            wsb = C.c_int64()
+            _lib.call("rlks_ppo_workspace_bytes", C.byref(self.desc), max(1, n), C.byref(wsb))
+            if getattr(self, "_fws", None) is None or self._fws.numel() < wsb.value:
+                self._fws = torch.empty(wsb.value, dtype=torch.uint8, device=obs.device)
+            _lib.call("rlks_policy_forward_ws", C.byref(self.desc), _lib.ptr(self.flat), _lib.ptr(obs), n,
+                      _lib.ptr(logits), _lib.ptr(values), _lib.ptr(self._fws), self._fws.numel(), stream)
+        else:
+            _lib.call("rlks_policy_forward", C.byref(self.desc), _lib.ptr(self.flat), _lib.ptr(obs), n,
+                      _lib.ptr(logits), _lib.ptr(values), stream)
         return logits, values
+
+    def wide(self):
+        """True when the generic-width path runs (the fused kernels cover hidden 256, obs < 32 and
+        2 / 4 / 8 actions)"""
+        return (self.desc.precision == _lib.RLKS_PRECISION_WIDE or self.H != 256 or self.A not in (2, 4, 8)
+                or self.D + 1 > 32)

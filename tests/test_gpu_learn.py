@@ -82,10 +82,11 @@ def test_gae_golden_vectors():
 
 
 # ----------------------------------------------------------------------------- MLP
-def _params(d, seed=0, D=6, A=2, scale_b=0.1):
+def _params(d, seed=0, D=6, A=2, scale_b=0.1, H=None):
     from rlks.policy import PolicyParams
 
-    p = PolicyParams(D, 256, A, device=d, seed=seed)
+    H = H if H is not None else (256 if (D + 1 <= 32 and A in (2, 4, 8)) else 2048)
+    p = PolicyParams(D, H, A, device=d, seed=seed)
     # non-zero biases so that every bias path is exercised
     g = torch.Generator().manual_seed(seed + 1)
     for i in (1, 3, 5, 7, 9, 11):
@@ -167,6 +168,59 @@ def test_ppo_grad_matches_oracle(rows, A, precision):
     for k, j in (("policy_loss", 0), ("vf_loss", 1), ("kl", 2), ("entropy", 3)):
         assert abs(st[j] - est[k]) <= 1e-5 * max(abs(est[k]), 1e-3 * rows), k
     assert st[4] == rows
+
+
+@pytest.mark.parametrize("rows,D,H,A", [(512, 6, 256, 2), (384, 12, 512, 4), (256, 192, 2048, 64), (300, 24, 96, 8)])
+def test_wide_grad_matches_oracle(rows, D, H, A):
+    """generic-width path (wide_mlp.hip: split-fp16 GEMMs with fused epilogues), incl. the c5 shape
+    (obs 3 x 64 clusters, 64 actions, hidden 2048) and ragged rows; same 1e-5 bar"""
+    from rlks import _lib
+
+    d = _dev()
+    p = _params(d, seed=rows + H, D=D, A=A, H=H)
+    p.desc.precision = _lib.RLKS_PRECISION_WIDE
+    rng = np.random.default_rng(rows + H)
+    mb = _minibatch(rows, rng, D=D, A=A, p=p, d=d)
+    _, vv = p.forward(torch.from_numpy(mb[:, :D].copy()).to(d))
+    mb[:, D + A + 1] = vv.cpu().numpy() + rng.standard_normal(rows).astype(np.float32) * 4
+    adv_mean, adv_invstd, klc = 0.3, 0.7, 0.2
+    dyn = torch.tensor([adv_mean, adv_invstd, klc, 1.0 / rows, 0, 0, 0, 0], dtype=torch.float32, device=d)
+    co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.01)
+    wsb = C.c_int64()
+    _lib.call("rlks_ppo_workspace_bytes", C.byref(p.desc), rows, C.byref(wsb))
+    ws = torch.empty(wsb.value, dtype=torch.uint8, device=d)
+    grad = torch.zeros(p.padded, device=d)
+    stats = torch.zeros(8, dtype=torch.float64, device=d)
+    mbt = torch.from_numpy(mb).to(d)
+    _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
+              rows, grad.data_ptr(), stats.data_ptr(), ws.data_ptr(), ws.numel(), None)
+    g = grad.cpu().numpy()
+    eg, est = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, H, A, mb, entropy_coeff=0.01,
+                                   kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd)
+    from rlks.policy import TENSOR_NAMES
+
+    for i, (name, _, _) in enumerate(TENSOR_NAMES):
+        n = int(np.prod(p.shapes[i]))
+        a = g[p.offsets[i]: p.offsets[i] + n]
+        b = eg[p.offsets[i]: p.offsets[i] + n]
+        assert np.linalg.norm(a - b) <= 1e-5 * np.linalg.norm(b) + 1e-12, name
+        close(a, b)
+    st = stats.cpu().numpy()
+    for k, j in (("policy_loss", 0), ("vf_loss", 1), ("kl", 2), ("entropy", 3)):
+        assert abs(st[j] - est[k]) <= 1e-5 * max(abs(est[k]), 1e-3 * rows), k
+    assert st[4] == rows
+
+
+@pytest.mark.parametrize("n,D,H,A", [(1000, 192, 2048, 64), (77, 12, 512, 4)])
+def test_wide_forward_matches_oracle(n, D, H, A):
+    d = _dev()
+    p = _params(d, seed=n, D=D, A=A, H=H)
+    rng = np.random.default_rng(n)
+    obs = rng.random((n, D)).astype(np.float32)
+    lg, v = p.forward(torch.from_numpy(obs).to(d))
+    el, ev = oracle.mlp_forward(p.flat.cpu().numpy(), p.offsets, D, H, A, obs)
+    close(lg.cpu().numpy(), el)
+    close(v.cpu().numpy(), ev)
 
 
 def test_adam_matches_torch():
