@@ -7,7 +7,10 @@ epochs of 65,536-row minibatches (8 per epoch) of RLlib's default PPO (FCNet [25
 separate value net, Adam lr 3e-4, gamma 0.99).  A "step" is one full PPO iteration.  Synthetic
 data (the env itself generates it); random-init weights; fp32 throughout.
 
-  python bench.py --gpus N --steps K --warmup W
+  python bench.py --gpus N --steps K --warmup W [--config c2|c3|c4|c5]
+  (--config picks another BASELINE.json workload — c3: 65,536 node-level envs x 8 clusters x 256
+   nodes; c4: 131,072 envs/GPU, the 8-GPU 1,048,576-env shard; c5: 64 x 1,024 nodes with bursty
+   arrivals and the [2048, 2048] policy on the generic-width path; the default is c2)
   (N > 1: launched by torch.distributed.run; one rank per GPU over RCCL; weak scaling —
    every rank owns its own 4,096 lanes, the global minibatch is 65,536 x N rows)
 
@@ -37,21 +40,63 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # dense fp16/bf16 MFMA peak (MI355X_MICROARCH.md)
 # algorithmic (fp32) FLOPs is a third of the f16 peak
 SF16_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 
-# algorithmic work per row of each SGD-step kernel (D = 6, H = 256, A = 2, both nets)
-D_, H_, A_ = 6, 256, 2
-FLOPS_PER_ROW = {
-    # per net: forward 2(DH + H^2 + H*A_net) + head backward (dout W3 and dW3) 4*H*A_net
-    "k_fwd_head_pi": 2 * (D_ * H_ + H_ * H_ + H_ * A_) + 4 * H_ * A_,
-    "k_fwd_head_vf": 2 * (D_ * H_ + H_ * H_ + H_) + 4 * H_,
-    "k_dw2": 2 * 2 * H_ * H_,                       # dW2 = dZ2^T H1, both nets
-    "k_dh1": 2 * 2 * H_ * H_ + 2 * 2 * D_ * H_,     # dH1 = dZ2 W2 and dW1 = dZ1^T X, both nets
-    # split-fp16 kernels (sgd_sf16.hip), algorithmic fp32 FLOPs per row:
-    # F1 per net = forward + head backward + dH1 = dZ2 W2 + dW1 = dZ1^T X
-    # (one launch covers both nets: forward + head backward + dH1 = dZ2 W2 + dW1 = dZ1^T X)
-    "k_sf_fwdbwd": (2 * (D_ * H_ + H_ * H_ + H_ * A_) + 4 * H_ * A_ + 2 * H_ * H_ + 2 * D_ * H_)
-                   + (2 * (D_ * H_ + H_ * H_ + H_) + 4 * H_ + 2 * H_ * H_ + 2 * D_ * H_),
-    "k_sf_dw2": 2 * 2 * H_ * H_,                    # dW2 = dZ2^T H1, both nets
+
+
+def flops_per_row(name, D=6, H=256, A=2):
+    """algorithmic (fp32) FLOPs per minibatch row of each SGD-step kernel, both nets"""
+    fwd = lambda An: 2 * (D * H + H * H + H * An)  # noqa: E731  per net forward
+    head = lambda An: 4 * H * An                    # noqa: E731  head backward: dout W3 and dW3
+    return {
+        "k_fwd_head_pi": fwd(A) + head(A),
+        "k_fwd_head_vf": fwd(1) + head(1),
+        "k_dw2": 2 * 2 * H * H,                     # dW2 = dZ2^T H1, both nets
+        "k_dh1": 2 * 2 * H * H + 2 * 2 * D * H,     # dH1 = dZ2 W2 and dW1 = dZ1^T X, both nets
+        # split-fp16 F1 (sgd_sf16.hip): forward + head backward + dH1 = dZ2 W2 + dW1 = dZ1^T X, both nets
+        "k_sf_fwdbwd": sum(fwd(An) + head(An) + 2 * H * H + 2 * D * H for An in (A, 1)),
+        "k_sf_dw2": 2 * 2 * H * H,                  # dW2 = dZ2^T H1, both nets
+        # generic-width path (wide_mlp.hip): the whole gradient (forward, head, dW2, dH1, dW1), both nets
+        "wide_grad": sum(fwd(An) + head(An) + 4 * H * H + 2 * D * H for An in (A, 1)),
+    }[name]
+
+
+# BASELINE.json configs (SURVEY §8d); "c1" is the reference's single-env CPU plumbing case
+CONFIGS = {
+    "c2": dict(envs=4096, clusters=2, nodes=0, hidden=256, minibatch=65536,
+               text="c2: 4,096 envs/GPU x 2-cloud table, T=128 rollout + GAE + PPO update "
+                    "(10 epochs x 8 minibatches of 65,536 rows/GPU, FCNet [256,256] tanh)",
+               cpu=dict(n_envs=4096, T=128, minibatch=65536)),
+    "c3": dict(envs=65536, clusters=8, nodes=256, hidden=256, minibatch=65536, arrivals="poisson",
+               text="c3: 65,536 envs/GPU x 8 clusters x 256 nodes (Poisson(1) arrivals, first-fit, stationary "
+                    "departures), T=128 rollout + GAE + PPO update (10 epochs x 128 minibatches of 65,536 rows, "
+                    "FCNet [256,256] tanh, obs 24, 8 actions)",
+               cpu=dict(n_envs=4096, T=32, minibatch=65536)),
+    "c4": dict(envs=131072, clusters=2, nodes=0, hidden=256, minibatch=65536,
+               text="c4: 131,072 envs/GPU (1,048,576 over 8 GPUs) x 2-cloud table, T=128 rollout + GAE + PPO "
+                    "update (10 epochs x 256 minibatches of 65,536 rows/GPU, FCNet [256,256] tanh)",
+               cpu=dict(n_envs=4096, T=128, minibatch=65536)),
+    "c5": dict(envs=16384, clusters=64, nodes=1024, hidden=2048, minibatch=65536, arrivals="bursty",
+               text="c5: 16,384 envs/GPU x 64 clusters x 1,024 nodes (bursty Locust-shaped arrivals, first-fit), "
+                    "T=128 rollout + GAE + PPO update (10 epochs x 32 minibatches of 65,536 rows, FCNet "
+                    "[2048,2048] tanh, obs 192, 64 actions)",
+               cpu=dict(n_envs=256, T=16, minibatch=4096)),
 }
+
+
+def env_setup(name):
+    """(table, NodeSpec or None) of a config"""
+    from rlks.env import NodeSpec, bursty_trace
+    from rlks.tables import load_table, synthetic_table
+
+    c = CONFIGS[name]
+    if not c["nodes"]:
+        return load_table(), None
+    tab = synthetic_table(c["clusters"], 100, seed=42)
+    trace = bursty_trace() if c.get("arrivals") == "bursty" else None
+    return tab, NodeSpec(c["clusters"], c["nodes"], arrival_rate=1.0, arrival_trace=trace, depart_prob="stationary",
+                         init_occupancy=0.5)
+
+
+ROOFLINE_KERNELS = ("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1", "k_sf_fwdbwd", "k_sf_dw2", "wide_grad")
 ENV_BYTES_PER_STEP = 4 + 8 + 24 + 4 + 1  # action, step r/w, obs, reward, done (SURVEY §8d)
 GAE_BYTES_PER_STEP = 17                  # r, V, done in; A, vtarg out
 
@@ -61,9 +106,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--envs", type=int, default=4096, help="lanes per GPU")
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS), help="BASELINE.json workload")
+    ap.add_argument("--envs", type=int, default=None, help="lanes per GPU (default: the config's)")
     ap.add_argument("--rollout", type=int, default=128)
-    ap.add_argument("--minibatch", type=int, default=65536, help="rows per GPU per SGD step")
+    ap.add_argument("--minibatch", type=int, default=None, help="rows per GPU per SGD step (default: the config's)")
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -71,7 +117,7 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_timing(algo, torch, reps=20):
+def kernel_timing(algo, torch, config="c2", reps=20):
     """average duration (ms) of each kernel, measured with HIP events on the launch stream"""
     from rlks import _lib
 
@@ -97,7 +143,11 @@ def kernel_timing(algo, torch, reps=20):
 
     _lib.call("rlks_ppo_gather", desc, C.byref(algo.bufs), 1, 0, 0, algo.mb, algo.dyn.data_ptr(),
               algo.mbuf.data_ptr(), s.cuda_stream)
-    if algo.precision == "sf16":
+    D, H, A = algo.D, algo.H, algo.A
+    if algo.precision == "wide":
+        phases = ()  # generic-width path: one sequence of GEMM launches, timed as a whole below
+        peak, peak_name = SF16_PEAK_TFLOPS, "frac_sf16_mfma"
+    elif algo.precision == "sf16":
         phase(_lib.RLKS_PHASE_ALL)()  # weight splits + dZ2 in place for the per-phase timings
         phases = (("k_sf_prep", _lib.RLKS_PHASE_PREP),
                   ("k_sf_fwdbwd", _lib.RLKS_PHASE_FWD_PI | _lib.RLKS_PHASE_FWD_VF),
@@ -110,21 +160,25 @@ def kernel_timing(algo, torch, reps=20):
     for name, mask in phases:
         ms = timed(phase(mask))
         rec = {"ms": ms}
-        if name in FLOPS_PER_ROW:
-            tf = FLOPS_PER_ROW[name] * algo.mb / (ms * 1e-3) / 1e12
+        if name in ROOFLINE_KERNELS:
+            tf = flops_per_row(name, D, H, A) * algo.mb / (ms * 1e-3) / 1e12
             rec.update({"tflops": tf, peak_name: tf / peak, "frac_fp32_mfma_peak": tf / FP32_MFMA_PEAK_TFLOPS})
         out[name] = rec
     ms = timed(lambda: _lib.call("rlks_ppo_grad", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(),
                                  algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None,
-                                 algo.ws.data_ptr(), algo.ws.numel(), s.cuda_stream))
+                                 algo.ws.data_ptr(), algo.ws.numel(), s.cuda_stream), n=reps if H <= 256 else 3)
     out["sgd_grad_total"] = {"ms": ms}
+    if algo.precision == "wide":
+        tf = flops_per_row("wide_grad", D, H, A) * algo.mb / (ms * 1e-3) / 1e12
+        out["wide_grad"] = {"ms": ms, "tflops": tf, peak_name: tf / peak, "frac_fp32_mfma_peak": tf / FP32_MFMA_PEAK_TFLOPS}
     b = algo.buf
     N, T = algo.N, algo.T
-    ms = timed(lambda: _lib.call("rlks_env_sample_step", algo.env.handle, b["logits"].data_ptr(), 1,
-                                 b["actions"].data_ptr(), b["logp"].data_ptr(), b["obs"][1].data_ptr(),
-                                 b["rewards"].data_ptr(), b["dones"].data_ptr(), s.cuda_stream))
-    gbs = ENV_BYTES_PER_STEP * N / (ms * 1e-3) / 1e9
-    out["k_sample_step"] = {"ms": ms, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS, "lanes": N}
+    if algo.env.cfg.nodes_per_cluster == 0:
+        ms = timed(lambda: _lib.call("rlks_env_sample_step", algo.env.handle, b["logits"].data_ptr(), 1,
+                                     b["actions"].data_ptr(), b["logp"].data_ptr(), b["obs"][1].data_ptr(),
+                                     b["rewards"].data_ptr(), b["dones"].data_ptr(), s.cuda_stream))
+        gbs = ENV_BYTES_PER_STEP * N / (ms * 1e-3) / 1e9
+        out["k_sample_step"] = {"ms": ms, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS, "lanes": N}
     ms = timed(lambda: _lib.call("rlks_gae", b["rewards"].data_ptr(), b["values"].data_ptr(), b["dones"].data_ptr(),
                                  0.99, 1.0, T, N, b["adv"].data_ptr(), b["vtarg"].data_ptr(), algo.gae_part.data_ptr(),
                                  s.cuda_stream))
@@ -132,9 +186,14 @@ def kernel_timing(algo, torch, reps=20):
     out["k_gae"] = {"ms": ms, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
     ms = timed(lambda: _lib.call("rlks_rollout_ws", algo.env.handle, desc, algo.params.flat.data_ptr(),
                                  C.byref(algo.bufs), 1, algo.ws.data_ptr(), algo.ws.numel(), s.cuda_stream), n=3)
-    # T fused (pi forward + sample + env step) launches + one batched value pass over (T+1) N rows
-    flops = (T * N + (T + 1) * N) * 269824 / 2
+    # both nets' forward of the (T + 1) N visited observations (logits of T N of them)
+    flops = (T + 1) * N * (flops_per_row("k_fwd_head_pi", D, H, A) - 4 * H * A
+                           + flops_per_row("k_fwd_head_vf", D, H, A) - 4 * H)
     out["rollout"] = {"ms": ms, "env_steps_per_s": T * N / (ms * 1e-3), "tflops": flops / (ms * 1e-3) / 1e12}
+    if config == "c3":
+        out["k_node_step_c3"] = node_env_timing(algo, torch, timed)
+    if config != "c2":
+        return out
     # the standalone env step kernel at a size where HBM, not launch latency, bounds it
     from rlks import VecK8sMultiCloudEnv
 
@@ -248,12 +307,19 @@ def main():
 
     from rlks.ppo import PPO, PPOConfig
 
+    preset = CONFIGS[args.config]
+    envs = args.envs or preset["envs"]
+    minibatch = args.minibatch or preset["minibatch"]
+    H = preset["hidden"]
+    table, nodes = env_setup(args.config)
     cfg = (PPOConfig().environment("K8sMultiCloudEnv").framework("torch")
-           .training(train_batch_size=args.envs * args.rollout * world, sgd_minibatch_size=args.minibatch * world,
-                     num_sgd_iter=args.epochs, lr=3e-4, gamma=0.99, sgd_precision=args.precision)
+           .training(train_batch_size=envs * args.rollout * world, sgd_minibatch_size=minibatch * world,
+                     num_sgd_iter=args.epochs, lr=3e-4, gamma=0.99, sgd_precision=args.precision,
+                     model={"fcnet_hiddens": [H, H]})
            .debugging(seed=42))
-    cfg.num_envs = args.envs
+    cfg.num_envs = envs
     cfg.rollout_fragment_length = args.rollout
+    cfg.table, cfg.nodes = table, nodes
     algo = PPO(config=cfg, device=dev)
 
     for _ in range(args.warmup):
@@ -278,7 +344,7 @@ def main():
     value = steps_total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    kernels = None if args.no_kernel_timing else kernel_timing(algo, torch)
+    kernels = None if args.no_kernel_timing else kernel_timing(algo, torch, args.config)
     # sanity: the policy is learning something finite
     st = algo.stats.cpu().numpy()
     finite = bool((st == st).all())
@@ -289,17 +355,20 @@ def main():
         if kernels:
             # the dominant kernel as rocprofv3 --stats ranks them: largest share of GPU time (each
             # runs once per SGD step, so: the longest launch)
-            cands = [k for k in kernels if k in FLOPS_PER_ROW]
+            cands = [k for k in kernels if k in ROOFLINE_KERNELS]
             dom = max(cands, key=lambda k: kernels[k]["ms"])
             k = kernels[dom]
-            peak = SF16_PEAK_TFLOPS if algo.precision == "sf16" else FP32_MFMA_PEAK_TFLOPS
+            peak = FP32_MFMA_PEAK_TFLOPS if algo.precision == "fp32" else SF16_PEAK_TFLOPS
             roofline = {"bound": "mfma", "kernel": dom, "achieved": k["tflops"], "peak": peak,
                         "unit": "TFLOP/s", "frac": k["tflops"] / peak, "traffic": None,
-                        "flop_per_launch": FLOPS_PER_ROW[dom] * algo.mb, "avg_launch_ms": k["ms"],
-                        "peak_basis": ("split-fp16: 2.5 PF dense f16 MFMA / 3 products per fp32-accurate FLOP"
-                                       if algo.precision == "sf16" else "fp32 MFMA dense peak")}
+                        "flop_per_launch": flops_per_row(dom, algo.D, algo.H, algo.A) * algo.mb,
+                        "avg_launch_ms": k["ms"],
+                        "peak_basis": ("fp32 MFMA dense peak" if algo.precision == "fp32" else
+                                       "split-fp16: 2.5 PF dense f16 MFMA / 3 products per fp32-accurate FLOP")}
+            if dom == "wide_grad":
+                roofline["note"] = "generic-width path: the whole SGD-step gradient (a sequence of split-fp16 GEMM launches)"
             pmc = pmc_traffic()
-            if pmc and dom in pmc:
+            if pmc and args.config == "c2" and dom in pmc:
                 roofline["traffic"] = pmc[dom]["hbm_bytes_per_launch"]
                 roofline["traffic_source"] = pmc["source"]
         cpu = None
@@ -307,8 +376,10 @@ def main():
             sys.path.insert(0, str(ROOT / "oracle"))
             from cpu_ppo import time_cpu_iteration
 
-            c = time_cpu_iteration(n_envs=args.envs, T=args.rollout, minibatch=args.minibatch, epochs=args.epochs,
-                                   threads=min(16, os.cpu_count() or 1))
+            cc = preset["cpu"]
+            c = time_cpu_iteration(n_envs=cc["n_envs"], T=cc["T"], minibatch=cc["minibatch"], epochs=args.epochs,
+                                   threads=min(16, os.cpu_count() or 1), table=table, nodes=nodes, hidden=H,
+                                   label=args.config)
             cpu = {"value": c["value"], "unit": "env-steps/s", "cores": c["cores"], "kind": "port",
                    "sample": c["sample"]}
         result = {
@@ -316,9 +387,8 @@ def main():
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp32" if algo.precision == "fp32" else "fp32 (split-fp16 MFMA, fp32-accurate)", "data": "synthetic (env-generated rollouts, random-init FCNet)",
-            "config": {"workload": "c2: 4,096 envs/GPU x 2-cloud table, T=128 rollout + GAE + PPO update "
-                                   "(10 epochs x 8 minibatches of 65,536 rows/GPU, FCNet [256,256] tanh)",
-                       "envs_per_gpu": args.envs, "rollout_steps": args.rollout, "minibatch_per_gpu": algo.mb,
+            "config": {"workload": preset["text"], "name": args.config,
+                       "envs_per_gpu": envs, "rollout_steps": args.rollout, "minibatch_per_gpu": algo.mb,
                        "epochs": args.epochs, "global_batch": algo.samples * world, "sgd_precision": algo.precision,
                        "parallelism": f"dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "finite": finite,

@@ -67,7 +67,8 @@ int rlks_env_reset(rlks_env* env, const uint8_t* mask_dev, float* obs_dev, void*
 /* step(action) (:115-144) for all lanes.  status_dev[0] = invalid actions (when > 0 NO lane
  * steps: the reference asserts before any change, :116); status_dev[1] = lanes that ran past the
  * last table row (the reference's IndexError, :91).  reward64 is bit-exact f64 (no FMA);
- * reward32/truncated/step_out/final_obs may be NULL.  Node-level envs (nodes_per_cluster > 0)
+ * reward32 its f32 rounding; one of the two reward pointers, truncated, step_out and final_obs
+ * may be NULL.  Node-level envs (nodes_per_cluster > 0)
  * run the node sweep (departures, arrivals, first-fit) in the same call.
  * status_dev == NULL declares the actions trusted (produced by rlks sampling): no validation
  * launch and no status report. */

@@ -21,9 +21,11 @@ def _mlp(torch, D, H, A):
     return net(A), net(1)
 
 
-def time_cpu_iteration(n_envs=4096, T=128, minibatch=65536, epochs=10, epochs_timed=1, threads=None, seed=0):
+def time_cpu_iteration(n_envs=4096, T=128, minibatch=65536, epochs=10, epochs_timed=1, threads=None, seed=0,
+                       table=None, nodes=None, hidden=256, label="c2"):
     """Returns dict(value=env-steps/s, cores, sample, seconds).  Times the full rollout plus
-    `epochs_timed` of the `epochs` SGD epochs, and scales the update to `epochs`."""
+    `epochs_timed` of the `epochs` SGD epochs, and scales the update to `epochs`.  `table` /
+    `nodes` (an rlks.env.NodeSpec) select the node-level env of configs c3 / c5."""
     import torch
 
     import oracle
@@ -33,10 +35,19 @@ def time_cpu_iteration(n_envs=4096, T=128, minibatch=65536, epochs=10, epochs_ti
     cores = torch.get_num_threads()
     from rlks.tables import load_table
 
-    tab = load_table()
-    env = oracle.OracleEnv(oracle.make_cfg(n_envs, tab.n_rows, tab.n_clouds, noise_mode=0, seed=seed, autoreset=1),
-                           tab.cost, tab.latency)
-    D, A, H = 3 * tab.n_clouds, tab.n_clouds, 256
+    tab = table if table is not None else load_table()
+    if nodes is None:
+        env = oracle.OracleEnv(oracle.make_cfg(n_envs, tab.n_rows, tab.n_clouds, noise_mode=0, seed=seed, autoreset=1),
+                               tab.cost, tab.latency)
+    else:
+        tr = nodes.arrival_trace
+        env = oracle.OracleEnv(
+            oracle.make_cfg(n_envs, tab.n_rows, tab.n_clouds, noise_mode=0, seed=seed, autoreset=1,
+                            nodes=nodes.nodes_per_cluster, arrival_mode=0 if tr is None else 1,
+                            arrival_rate=nodes.arrival_rate, depart_prob=nodes.depart_prob,
+                            init_occupancy=nodes.init_occupancy, reject_penalty=nodes.reject_penalty),
+            tab.cost, tab.latency, nodes.node_cpu_m, nodes.node_mem_mi, tr)
+    D, A, H = 3 * tab.n_clouds, tab.n_clouds, int(hidden)
     torch.manual_seed(seed)
     pi, vf = _mlp(torch, D, H, A)
     opt = torch.optim.Adam(list(pi.parameters()) + list(vf.parameters()), lr=3e-4)
@@ -72,7 +83,7 @@ def time_cpu_iteration(n_envs=4096, T=128, minibatch=65536, epochs=10, epochs_ti
     t1 = time.perf_counter()
     for _ in range(epochs_timed):
         perm = torch.randperm(S)
-        for b in range(S // minibatch):
+        for b in range(max(1, S // minibatch)):
             idx = perm[b * minibatch:(b + 1) * minibatch]
             lg = pi(X[idx])
             lp = torch.log_softmax(lg, 1)
@@ -88,6 +99,6 @@ def time_cpu_iteration(n_envs=4096, T=128, minibatch=65536, epochs=10, epochs_ti
     t_epoch = (time.perf_counter() - t1) / epochs_timed
     total = t_roll + epochs * t_epoch
     return {"value": S / total, "cores": cores, "seconds": t_roll + epochs_timed * t_epoch,
-            "sample": (f"one c2 iteration ({n_envs} envs x {T} steps rollout with the C env oracle + torch-CPU fp32 "
-                       f"FCNet; update timed for {epochs_timed} of {epochs} epochs of {S // minibatch} x {minibatch}-row "
+            "sample": (f"one {label} iteration ({n_envs} envs x {T} steps rollout with the C env oracle + torch-CPU fp32 "
+                       f"FCNet [{H},{H}]; update timed for {epochs_timed} of {epochs} epochs of {S // minibatch} x {minibatch}-row "
                        f"minibatches and scaled): rollout {t_roll:.2f} s, epoch {t_epoch:.2f} s")}

@@ -114,7 +114,7 @@ __global__ void k_env_step(EnvView v, const double* __restrict__ cost, const dou
     StepOut r = step_lane(v, s_tab, lane, actions[lane], obs + (size_t)lane * D,
                           final_obs ? final_obs + (size_t)lane * D : nullptr);
     over = r.overrun;
-    rew64[lane] = r.reward;
+    if (rew64) rew64[lane] = r.reward;
     if (rew32) rew32[lane] = (float)r.reward;
     term[lane] = (uint8_t)r.done;
     if (trunc) trunc[lane] = 0;
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __r
     if (live) {
       if (!act) {  // iloc[t] out of bounds before any change
         over = true;
-        rew64[env] = 0.0;
+        if (rew64) rew64[env] = 0.0;
         if (rew32) rew32[env] = 0.f;
         term[env] = 0;
         if (step_out) step_out[env] = t;
@@ -317,7 +317,7 @@ __global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __r
             v.episode[env] = ep + 1;
           }
         }
-        rew64[env] = r;
+        if (rew64) rew64[env] = r;
         if (rew32) rew32[env] = (float)r;
         term[env] = (uint8_t)done;
         if (step_out) step_out[env] = t1;
@@ -643,7 +643,7 @@ int rlks_env_reset(rlks_env* e, const uint8_t* mask, float* obs, void* stream) {
 int rlks_env_step(rlks_env* e, const int32_t* actions, float* obs, double* rew64, float* rew32,
                   uint8_t* term, uint8_t* trunc, int32_t* step_out, float* final_obs, int32_t* status,
                   void* stream) {
-  RLKS_REQUIRE(e && actions && obs && rew64 && term, RLKS_ERR_ARG, "rlks_env_step: null argument");
+  RLKS_REQUIRE(e && actions && obs && (rew64 || rew32) && term, RLKS_ERR_ARG, "rlks_env_step: null argument");
   hipStream_t s = (hipStream_t)stream;
   const unsigned grid = cdiv(e->cfg.n_envs, ENV_BLOCK);
   if (status) {  // NULL: trusted actions (e.g. from the sampler), no validation / overrun report

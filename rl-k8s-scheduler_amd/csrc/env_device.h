@@ -42,7 +42,7 @@ struct rlks_env {
 namespace rlks {
 
 constexpr int ENV_BLOCK = 256;
-constexpr int MAX_TABLE_BYTES = 96 * 1024;  // LDS budget for the staged tables
+constexpr int MAX_TABLE_BYTES = 128 * 1024;  // LDS budget for the staged tables (gfx950: 160 KB per workgroup)
 
 struct EnvView {
   int N, T, C, max_steps, noise_mode, autoreset, env_offset;

@@ -37,7 +37,8 @@ __global__ __launch_bounds__(256) void k_dw2(Dw2Args g) {
   for (int e = tid; e < GB; e += 256) sb1[e] = P.b1[k0 + e];
 
   float4 pa0, pa1, pa2, pa3;
-  float px = 0.f;
+  constexpr int XN = (BK * DD + 255) / 256;  // X values per thread per 32-row chunk
+  float px[XN];
 #define DW2_LOAD(mc)                                                                                \
   do {                                                                                              \
     const float* src_ = dz2 + (size_t)((mc) + (tid >> 5)) * H + n0 + 4 * (tid & 31);                   \
@@ -46,10 +47,18 @@ __global__ __launch_bounds__(256) void k_dw2(Dw2Args g) {
     pa2 = *reinterpret_cast<const float4*>(src_ + 16 * H);                                          \
     pa3 = *reinterpret_cast<const float4*>(src_ + 24 * H);                                          \
   } while (0)
-#define DW2_LOAD_X(mc) \
-  if (tid < BK * DD) px = g.x[(size_t)((mc) + tid / DD) * g.x_stride + tid % DD]
+#define DW2_LOAD_X(mc)                                                                              \
+  _Pragma("unroll") for (int i_ = 0; i_ < XN; ++i_) {                                               \
+    const int e_ = tid + 256 * i_;                                                                  \
+    if (e_ < BK * DD) px[i_] = g.x[(size_t)((mc) + e_ / DD) * g.x_stride + e_ % DD];                \
+  }
+#define DW2_STORE_X(b)                                                                              \
+  _Pragma("unroll") for (int i_ = 0; i_ < XN; ++i_) {                                               \
+    const int e_ = tid + 256 * i_;                                                                  \
+    if (e_ < BK * DD) sX[(b) * BK * ds + (e_ / DD) * ds + e_ % DD] = px[i_];                        \
+  }
   DW2_LOAD_X(mbeg);
-  if (tid < BK * DD) sX[(tid / DD) * ds + tid % DD] = px;
+  DW2_STORE_X(0);
   DW2_LOAD(mbeg);
   if (mbeg + BK < mend) DW2_LOAD_X(mbeg + BK);
 
@@ -71,7 +80,7 @@ __global__ __launch_bounds__(256) void k_dw2(Dw2Args g) {
       *reinterpret_cast<float4*>(dst + 16 * GB) = pa2;
       *reinterpret_cast<float4*>(dst + 24 * GB) = pa3;
     }
-    if (mc + BK < mend && tid < BK * DD) sX[(buf ^ 1) * BK * ds + (tid / DD) * ds + tid % DD] = px;
+    if (mc + BK < mend) { DW2_STORE_X(buf ^ 1); }
     // H1 recompute: sB[m][k] = tanh(b1[k] + X[m] . W1[k]); the row is wave-uniform
     const float* xb = sX + buf * BK * ds;
     {
@@ -258,6 +267,7 @@ __global__ __launch_bounds__(256) void k_dh1(Dh1Args g) {
 
 #undef DW2_LOAD
 #undef DW2_LOAD_X
+#undef DW2_STORE_X
 #undef DH1_LOAD
 
 int launch_dw2(const Dw2Args& a, int D, int splits, hipStream_t s) {

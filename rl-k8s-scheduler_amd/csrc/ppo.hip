@@ -332,6 +332,54 @@ static int check_desc(const rlks_mlp_desc* d) {
   return RLKS_OK;
 }
 
+// Node-level envs (nodes_per_cluster > 0): the node sweep has its own workgroup shape (k_node_step:
+// 64 envs x W waves), so a rollout step is three launches on the stream: forward of both nets on
+// obs[t] (logits[t], values[t]) -> Categorical sample (actions[t], logp[t]) -> trusted env step
+// (obs[t + 1], f32 rewards[t], dones[t]); then the bootstrap V(obs[T]).  `w` = the split-fp16
+// weights (SF16) or nullptr (fp32 kernels).
+static int node_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, const rlks_rollout_bufs* b,
+                        int explore, const SfWs* w, hipStream_t s) {
+  const int N = b->N, D = d->obs_dim, A = d->n_actions;
+  const Layout L = make_layout(D, HID, A);
+  SfRollArgs r{};
+  if (w) {
+    if (int rc = sf_prep(d, *w, params, s)) return rc;
+    for (int net = 0; net < 2; ++net) {
+      const NetPtrs P = net_ptrs_host(params, L, net);
+      r.n[net] = SfRollNet{w->w[net].w1h, w->w[net].w1l, w->w[net].w2rh, w->w[net].w2rl, P.b2, P.w3, P.b3, w->w[net].sc};
+    }
+    r.M = N; r.D = D; r.A = A; r.T = 0;
+  }
+  auto forward = [&](const float* x, float* logits, float* values) -> int {
+    if (w) {
+      SfRollArgs a = r;
+      a.x = const_cast<float*>(x);
+      a.logits = logits;
+      a.values = values;
+      return launch_sf_roll(a, FWD_ONLY, s);
+    }
+    for (int net = 0; net < 2; ++net) {
+      float* out = net == 0 ? logits : values;
+      if (!out) continue;
+      FwdArgs f{};
+      f.P = net_ptrs_host(params, L, net);
+      f.x = x; f.x_stride = D; f.M = N; f.D = D; f.A_pi = A; f.out = out;
+      if (int rc = launch_fwd_head(f, net, A, FWD_ONLY, s)) return rc;
+    }
+    return RLKS_OK;
+  };
+  const EnvView v = view(env);
+  for (int t = 0; t < b->T; ++t) {
+    const size_t tN = (size_t)t * N;
+    if (int rc = forward(b->obs + tN * D, b->logits + tN * A, b->values + tN)) return rc;
+    if (int rc = launch_sample(v, b->logits + tN * A, A, explore, b->actions + tN, b->logp + tN, s)) return rc;
+    if (int rc = rlks_env_step(env, b->actions + tN, b->obs + (tN + N) * D, nullptr, b->rewards + tN, b->dones + tN,
+                               nullptr, nullptr, nullptr, nullptr, s))
+      return rc;
+  }
+  return forward(b->obs + (size_t)b->T * N * D, nullptr, b->values + (size_t)b->T * N);
+}
+
 }  // namespace rlks
 
 using namespace rlks;
@@ -583,10 +631,12 @@ int rlks_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, con
   rlks_env_config(env, &cfg);
   RLKS_REQUIRE(cfg.n_envs == b->N && 3 * cfg.n_clouds == d->obs_dim && cfg.n_clouds == d->n_actions,
                RLKS_ERR_ARG, "rlks_rollout: env / policy / buffer shapes disagree");
-  RLKS_REQUIRE(cfg.nodes_per_cluster == 0, RLKS_ERR_UNSUPPORTED,
-               "rlks_rollout: fused rollout covers the table env; node-level envs step through rlks_env_step");
-  const int N = b->N, D = d->obs_dim, A = d->n_actions;
   hipStream_t s = (hipStream_t)stream;
+  if (cfg.nodes_per_cluster > 0) {
+    RLKS_REQUIRE(cfg.autoreset, RLKS_ERR_ARG, "rlks_rollout: node-level rollout needs autoreset lanes");
+    return node_rollout(env, d, params, b, explore, nullptr, s);
+  }
+  const int N = b->N, D = d->obs_dim, A = d->n_actions;
   const Layout L = make_layout(D, d->hidden, A);
   // per step: policy forward fused with sampling and the env step (one launch, pi net only)
   FwdArgs f{};
@@ -629,12 +679,14 @@ int rlks_rollout_ws(rlks_env* env, const rlks_mlp_desc* d, const float* params, 
   rlks_env_config(env, &cfg);
   RLKS_REQUIRE(cfg.n_envs == b->N && 3 * cfg.n_clouds == d->obs_dim && cfg.n_clouds == d->n_actions,
                RLKS_ERR_ARG, "rlks_rollout_ws: env / policy / buffer shapes disagree");
-  RLKS_REQUIRE(cfg.nodes_per_cluster == 0, RLKS_ERR_UNSUPPORTED,
-               "rlks_rollout_ws: fused rollout covers the table env; node-level envs step through rlks_env_step");
   const int N = b->N, D = d->obs_dim, A = d->n_actions;
   const SfWs w = sf_ws_layout(D, A, 0, (char*)workspace);
   RLKS_REQUIRE(ws_bytes >= w.weight_bytes, RLKS_ERR_ARG, "rlks_rollout_ws: workspace too small");
   hipStream_t s = (hipStream_t)stream;
+  if (cfg.nodes_per_cluster > 0) {
+    RLKS_REQUIRE(cfg.autoreset, RLKS_ERR_ARG, "rlks_rollout_ws: node-level rollout needs autoreset lanes");
+    return node_rollout(env, d, params, b, explore, &w, s);
+  }
   if (int rc = sf_prep(d, w, params, s)) return rc;
   const Layout L = make_layout(D, HID, A);
   SfRollArgs a{};

@@ -25,6 +25,9 @@ int wide_forward(const rlks_mlp_desc* d, const float* params, const float* x, in
                  float* logits, float* values, hipStream_t s);
 int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
               const float* mb, int M, float* grad, double* stats, const WideWs& w, hipStream_t s);
+// TorchCategorical over [N][A] logits (Philox sample, or argmax when explore == 0) -> actions, logp
+int launch_sample(const EnvView& v, const float* logits, int A, int explore, int32_t* actions, float* logp,
+                  hipStream_t s);
 int wide_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, const rlks_rollout_bufs* b, int explore,
                  const WideWs& w, hipStream_t s);
 

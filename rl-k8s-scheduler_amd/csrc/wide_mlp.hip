@@ -287,6 +287,13 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
   return RLKS_OK;
 }
 
+int launch_sample(const EnvView& v, const float* logits, int A, int explore, int32_t* actions, float* logp,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(k_wide_sample, dim3(cdiv(v.N, 256)), dim3(256), 0, s, v, logits, A, explore, actions, logp);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
 int wide_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, const rlks_rollout_bufs* b, int explore,
                  const WideWs& w, hipStream_t s) {
   const int N = b->N, D = d->obs_dim, A = d->n_actions;
@@ -296,9 +303,9 @@ int wide_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* params, con
     const float* obs = b->obs + (size_t)t * N * D;
     if (int rc = wide_forward(d, params, obs, D, N, w, b->logits + (size_t)t * N * A, b->values + (size_t)t * N, s))
       return rc;
-    hipLaunchKernelGGL(k_wide_sample, dim3(cdiv(N, 256)), dim3(256), 0, s, v, b->logits + (size_t)t * N * A, A,
-                       explore, b->actions + (size_t)t * N, b->logp + (size_t)t * N);
-    RLKS_LAUNCHED();
+    if (int rc = launch_sample(v, b->logits + (size_t)t * N * A, A, explore, b->actions + (size_t)t * N,
+                               b->logp + (size_t)t * N, s))
+      return rc;
     if (int rc = rlks_env_step(env, b->actions + (size_t)t * N, b->obs + (size_t)(t + 1) * N * D, w.rew64,
                                b->rewards + (size_t)t * N, b->dones + (size_t)t * N, nullptr, nullptr, nullptr, nullptr,
                                s))

@@ -72,11 +72,14 @@ class PPOConfig:
         self.noise = "philox"         # env utilisation noise: "philox" or "mt19937"
         self.data_path = None
         self.table = None
+        self.nodes = None             # rlks.env.NodeSpec: node-level envs (configs c3 / c5)
         self.adam_betas = (0.9, 0.999)
         self.adam_eps = 1e-8
         # SGD-step matrix arithmetic (include/rlks_types.h RLKS_PRECISION_*): "sf16" = split-fp16
         # MFMA (fp32-accurate, 16x the fp32 matrix rate; minibatch rows per rank % 256 == 0),
-        # "fp32" = fp32 MFMA; "auto" = sf16 where the minibatch allows it
+        # "fp32" = fp32 MFMA; "auto" = sf16 where the minibatch allows it.  Policies the fused
+        # kernels do not cover (hidden != 256, obs > 31, actions not 2 / 4 / 8) always run the
+        # generic-width split-fp16 path ("wide")
         self.sgd_precision = "auto"
 
     # ---- builder methods (names as in RLlib)
@@ -139,7 +142,7 @@ class PPOConfig:
         return self
 
     def to_dict(self):
-        d = {k: v for k, v in self.__dict__.items() if k not in ("env", "table")}
+        d = {k: v for k, v in self.__dict__.items() if k not in ("env", "table", "nodes")}
         d["env"] = getattr(self.env, "__name__", str(self.env)) if self.env is not None else None
         d["lambda"] = d.pop("lambda_")
         return d
@@ -184,6 +187,8 @@ class PPO:
         table = cfg.table if cfg.table is not None else load_table(cfg.data_path)
         self.table = table
         C_ = table.n_clouds
+        if cfg.nodes is not None and cfg.nodes.n_clouds != C_:
+            raise ValueError(f"NodeSpec has {cfg.nodes.n_clouds} clusters, the table {C_}")
         self.D, self.A, self.H = 3 * C_, C_, cfg.hidden()
         self.N = cfg.lanes()
         self.T = max(1, math.ceil(cfg.train_batch_size / (self.N * self.world)))
@@ -200,15 +205,19 @@ class PPO:
         self.seed = seed
         with torch.cuda.device(self.device):
             self.env = DeviceEnv(make_cfg(self.N, table, noise=cfg.noise, seed=seed, autoreset=True,
-                                          env_offset=ddp.lane_range(self.N, self.rank)[0]), table, self.device)
+                                          env_offset=ddp.lane_range(self.N, self.rank)[0], nodes=cfg.nodes),
+                                 table, self.device, cfg.nodes)
             self.params = PolicyParams(self.D, self.H, self.A, device=self.device, seed=seed)
             prec = cfg.sgd_precision
-            if prec == "auto":
+            if self.params.wide():
+                prec = "wide"
+            elif prec == "auto":
                 prec = "sf16" if self.mb % 256 == 0 else "fp32"
-            if prec not in ("sf16", "fp32") or (prec == "sf16" and self.mb % 256):
+            if prec not in ("sf16", "fp32", "wide") or (prec == "sf16" and self.mb % 256):
                 raise ValueError(f"sgd_precision {cfg.sgd_precision!r} with {self.mb} minibatch rows per rank")
             self.precision = prec
-            self.params.desc.precision = _lib.RLKS_PRECISION_SF16 if prec == "sf16" else _lib.RLKS_PRECISION_FP32
+            self.params.desc.precision = {"sf16": _lib.RLKS_PRECISION_SF16, "fp32": _lib.RLKS_PRECISION_FP32,
+                                          "wide": _lib.RLKS_PRECISION_WIDE}[prec]
             P = self.params.padded
             f32 = dict(dtype=torch.float32, device=self.device)
             self.adam_m = torch.zeros(P, **f32)
@@ -232,9 +241,12 @@ class PPO:
                                          b["dones"].data_ptr(), b["adv"].data_ptr(), b["vtarg"].data_ptr(), T, N)
             self.stride = _lib.lib().rlks_minibatch_stride(C.byref(self.params.desc))
             self.mbuf = torch.zeros(self.mb, self.stride, **f32)
-            wsb = C.c_int64()
+            # one workspace for the SGD step and the rollout (split weights; wide: N-row activations)
+            wsb, wsr = C.c_int64(), C.c_int64()
             _lib.call("rlks_ppo_workspace_bytes", C.byref(self.params.desc), self.mb, C.byref(wsb))
-            self.ws = torch.empty(wsb.value, dtype=torch.uint8, device=self.device)
+            _lib.call("rlks_ppo_workspace_bytes", C.byref(self.params.desc),
+                      N if prec == "wide" else self.mb, C.byref(wsr))
+            self.ws = torch.empty(max(wsb.value, wsr.value), dtype=torch.uint8, device=self.device)
             self.n_partials = _lib.lib().rlks_gae_partials_count(N)
             self.gae_part = torch.zeros(self.n_partials, 2, dtype=torch.float64, device=self.device)
             self.adv_sums = torch.zeros(3, dtype=torch.float64, device=self.device)

@@ -128,7 +128,7 @@ def _minibatch(rows, rng, D=6, A=2, p=None, d=None):
 
 
 @pytest.mark.parametrize("rows,A,precision", [(256, 2, 0), (4096, 2, 0), (256, 2, 1), (4096, 2, 1), (65536, 2, 1),
-                                              (512, 4, 1), (512, 8, 1)])
+                                              (512, 4, 1), (512, 8, 1), (512, 4, 0), (1024, 8, 0)])
 def test_ppo_grad_matches_oracle(rows, A, precision):
     """precision 0: fp32 MFMA kernels; 1: split-fp16 MFMA kernels (sgd_sf16.hip) — same 1e-5 bar"""
     from rlks import _lib

@@ -2,6 +2,8 @@
 arrivals, first-fit placement, integer resource accounting) against the C oracle: observations,
 f64 rewards, terminations, every node's free millicores / MiB, the per-cluster aggregates and the
 placement counters must be bit-identical."""
+import ctypes as C_
+
 import numpy as np
 import pytest
 
@@ -103,3 +105,79 @@ def test_nodes_full_c3_size():
     assert torch.equal(used, (cap_cpu[None, :, None] - fc).sum(-1).to(torch.int32))
     util = used.float() / (nodes * cap_cpu[None, :]).float()
     assert torch.equal(obs[:, 2 * C:], util)
+
+
+# ----------------------------------------------------------------------------- PPO on node envs
+def _close(x, ref, rtol=1e-5):
+    x = np.asarray(x, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(x - ref)
+    assert (err <= rtol * np.abs(ref) + rtol * max(1e-30, float(np.abs(ref).max()))).all(), f"max err {err.max():.3e}"
+
+
+@pytest.mark.parametrize("C,nodes,H,N,T,mb,precision", [
+    (8, 64, 256, 2048, 24, 8192, "auto"),    # c3 shape (obs 24, 8 actions), split-fp16 rollout forward
+    (8, 64, 256, 1024, 16, 4096, "fp32"),    # same env, fp32-MFMA rollout forward
+    (16, 32, 384, 512, 12, 2048, "auto"),    # generic-width path (hidden 384, obs 48, 16 actions)
+])
+def test_ppo_on_node_envs(C, nodes, H, N, T, mb, precision):
+    """PPO rollout over node-level envs (rlks_rollout_ws: forward -> sample -> node step per step):
+    transitions replayed bit-exactly by the C oracle fed the rollout's actions, logits / values
+    vs the fp64 oracle, logp consistent, GAE, one SGD gradient, then two train() iterations"""
+    from rlks import _lib
+    from rlks.env import NodeSpec
+    from rlks.ppo import PPO, PPOConfig
+    from rlks.tables import synthetic_table
+
+    d = _dev()
+    tab = synthetic_table(C, 100, seed=7)
+    spec = NodeSpec(C, nodes, arrival_rate=2.0, depart_prob=0.05, init_occupancy=0.5, reject_penalty=0.1)
+    cfg = (PPOConfig().framework("torch")
+           .training(train_batch_size=N * T, sgd_minibatch_size=mb, num_sgd_iter=2, lr=3e-4, gamma=0.99,
+                     sgd_precision=precision, model={"fcnet_hiddens": [H, H]})
+           .debugging(seed=5))
+    cfg.num_envs, cfg.table, cfg.nodes = N, tab, spec
+    algo = PPO(config=cfg, device=d)
+    assert algo.T == T and algo.D == 3 * C and algo.A == C
+    assert algo.precision == ("wide" if H != 256 else ("fp32" if precision == "fp32" else "sf16"))
+    algo.rollout(explore=True)
+    b = {k: v.cpu().numpy() for k, v in algo.buf.items()}
+    assert b["actions"].min() >= 0 and b["actions"].max() < C and len(np.unique(b["actions"])) == C
+    ora = oracle.OracleEnv(oracle.make_cfg(N, 100, C, noise_mode=0, seed=5, autoreset=1, nodes=nodes, arrival_rate=2.0,
+                                           depart_prob=0.05, init_occupancy=0.5, reject_penalty=0.1),
+                           tab.cost, tab.latency, spec.node_cpu_m, spec.node_mem_mi, None)
+    np.testing.assert_array_equal(ora.reset().view(np.uint32), b["obs"][0].view(np.uint32))
+    for t in range(T):
+        o, r, term, _, _, _ = ora.step(b["actions"][t])
+        np.testing.assert_array_equal(o.view(np.uint32), b["obs"][t + 1].view(np.uint32))
+        np.testing.assert_array_equal(r.astype(np.float32).view(np.uint32), b["rewards"][t].view(np.uint32))
+        np.testing.assert_array_equal(term, b["dones"][t])
+    lo = b["logits"].astype(np.float64)
+    mx = lo.max(-1, keepdims=True)
+    lsm = lo - mx - np.log(np.exp(lo - mx).sum(-1, keepdims=True))
+    _close(np.take_along_axis(lsm, b["actions"][..., None].astype(int), -1)[..., 0], b["logp"])
+    flat = algo.params.flat.cpu().numpy()
+    for t in (0, T // 2, T):
+        el, ev = oracle.mlp_forward(flat, algo.params.offsets, 3 * C, H, C, b["obs"][t])
+        _close(b["values"][t], ev)
+        if t < T:
+            _close(b["logits"][t], el)
+    algo.advantages()
+    ea, evt = oracle.gae(b["rewards"], b["values"], b["dones"], 0.99, 1.0)
+    _close(algo.buf["adv"].cpu().numpy(), ea)
+    _close(algo.buf["vtarg"].cpu().numpy(), evt)
+    _lib.call("rlks_ppo_gather", C_.byref(algo.params.desc), C_.byref(algo.bufs), 3, 0, 0, algo.mb,
+              algo.dyn.data_ptr(), algo.mbuf.data_ptr(), None)
+    mbh = algo.mbuf.cpu().numpy()
+    dyn = algo.dyn.cpu().numpy()
+    _lib.call("rlks_ppo_grad", C_.byref(algo.params.desc), C_.byref(algo.coeffs), algo.params.flat.data_ptr(),
+              algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, algo.ws.data_ptr(),
+              algo.ws.numel(), None)
+    eg, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 3 * C, H, C, mbh, kl_coeff=float(dyn[2]),
+                                 adv_mean=float(dyn[0]), adv_inv_std=float(dyn[1]))
+    g = algo.grad.cpu().numpy()
+    assert np.linalg.norm(g - eg) <= 1e-5 * np.linalg.norm(eg)
+    for _ in range(2):
+        r = algo.train()
+        assert np.isfinite(r["info"]["learner"]["default_policy"]["learner_stats"]["policy_loss"])
+    assert bool(torch.isfinite(algo.params.flat).all())
