@@ -63,7 +63,7 @@ struct Stager {
       const int f = tid + 256 * i;
       int row, k;
       if (!T) { row = f >> 3; k = 4 * (f & 7); }     // 128 rows x 8 float4
-      else { k = f >> 5; row = 4 * (f & 31); }       // 32 k x 32 float4
+      else { k = 4 * (tid >> 5) + i; row = 4 * (tid & 31); }  // 4 k x 4 rows per thread (i = k)
       const int gr = r0 + row, gk = k0 + k;
       float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
       if (!T) {
@@ -109,15 +109,24 @@ struct Stager {
         }
         *reinterpret_cast<h4*>(buf + coff(row, k)) = hi;
         *reinterpret_cast<h4*>(buf + GCH + coff(row, k)) = lo;
-      } else {
-        const int k = f >> 5, row = 4 * (f & 31);
+      }
+    }
+    if (T) {  // register transpose: row j of the thread's 4 x 4 block is 4 consecutive k -> one h4
+      const int k = 4 * (tid >> 5), row = 4 * (tid & 31);
+      const float e[4][4] = {{v[0].x, v[0].y, v[0].z, v[0].w}, {v[1].x, v[1].y, v[1].z, v[1].w},
+                             {v[2].x, v[2].y, v[2].z, v[2].w}, {v[3].x, v[3].y, v[3].z, v[3].w}};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 4; ++j) {
+        h4 hi, lo;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
           _Float16 a, b;
-          split1(e[j] * s, a, b);
-          buf[coff(row + j, k)] = a;
-          buf[GCH + coff(row + j, k)] = b;
+          split1(e[i][j] * s, a, b);
+          hi[i] = a;
+          lo[i] = b;
         }
+        *reinterpret_cast<h4*>(buf + coff(row + j, k)) = hi;
+        *reinterpret_cast<h4*>(buf + GCH + coff(row + j, k)) = lo;
       }
     }
   }
@@ -126,7 +135,7 @@ struct Stager {
 }  // namespace
 
 template <bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(256) void k_gemm_sf16(GemmArgs g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_gemm_sf16(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   _Float16* sm = reinterpret_cast<_Float16*>(lds);  // [2 buf][A hi, A lo, B hi, B lo][GCH]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
@@ -135,8 +144,11 @@ __global__ __launch_bounds__(256) void k_gemm_sf16(GemmArgs g) {
   const int ea = sf_exp(__uint_as_float(*g.amax)), eb = sf_exp(__uint_as_float(*g.bmax));
   const float sa = ldexpf(1.f, ea), sb = ldexpf(1.f, eb), unscale = ldexpf(1.f, -ea - eb);
 
-  Stager<TA> SA;
-  Stager<!TB> SB;  // B is staged as rows n: B stored [N][K] (TB) has k contiguous
+  // register ring of two chunks per operand: while chunk c is multiplied, chunks c + 1 (parked in
+  // LDS at the start of iteration c) and c + 2 / c + 3 are in flight, so a load has two MFMA
+  // blocks to arrive instead of one
+  Stager<TA> SA0, SA1;
+  Stager<!TB> SB0, SB1;  // B is staged as rows n: B stored [N][K] (TB) has k contiguous
   const bool va = (g.lda & 3) == 0 && ((uintptr_t)g.A & 15) == 0;
   const bool vb = (g.ldb & 3) == 0 && ((uintptr_t)g.B & 15) == 0;
   f32x16 acc[2][2];
@@ -147,57 +159,66 @@ __global__ __launch_bounds__(256) void k_gemm_sf16(GemmArgs g) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
 
-  const int nk = (g.K + GKC - 1) / GKC;
-  SA.load(g.A, g.lda, g.M, g.K, m0, 0, tid, va);
-  SB.load(g.B, g.ldb, g.N, g.K, n0, 0, tid, vb);
-  SA.store(sm, sa, tid);
-  SB.store(sm + 2 * GCH, sb, tid);
+  // this workgroup's K range (split-K: layer z of `splits`, each kper long, a multiple of GKC)
+  const int kper = g.splits > 1 ? (((g.K + g.splits - 1) / g.splits + GKC - 1) / GKC) * GKC : g.K;
+  const int kb = blockIdx.z * kper, ke = min(g.K, kb + kper);
+  const int nk = ke > kb ? (ke - kb + GKC - 1) / GKC : 0;
+  SA0.load(g.A, g.lda, g.M, ke, m0, kb, tid, va);
+  SB0.load(g.B, g.ldb, g.N, ke, n0, kb, tid, vb);
+  SA0.store(sm, sa, tid);
+  SB0.store(sm + 2 * GCH, sb, tid);
   if (nk > 1) {
-    SA.load(g.A, g.lda, g.M, g.K, m0, GKC, tid, va);
-    SB.load(g.B, g.ldb, g.N, g.K, n0, GKC, tid, vb);
+    SA1.load(g.A, g.lda, g.M, ke, m0, kb + GKC, tid, va);
+    SB1.load(g.B, g.ldb, g.N, ke, n0, kb + GKC, tid, vb);
+  }
+  if (nk > 2) {
+    SA0.load(g.A, g.lda, g.M, ke, m0, kb + 2 * GKC, tid, va);
+    SB0.load(g.B, g.ldb, g.N, ke, n0, kb + 2 * GKC, tid, vb);
   }
   __syncthreads();
-  for (int c = 0; c < nk; ++c) {
-    const _Float16* buf = sm + (c & 1) * 4 * GCH;
-    h8 fa[2][2][2], fb[2][2][2];  // [tile][s][hi/lo]
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int ra = wm * 64 + 32 * i + r, rb = wn * 64 + 32 * i + r, k = 16 * s + 8 * h;
-        fa[i][s][0] = *reinterpret_cast<const h8*>(buf + coff(ra, k));
-        fa[i][s][1] = *reinterpret_cast<const h8*>(buf + GCH + coff(ra, k));
-        fb[i][s][0] = *reinterpret_cast<const h8*>(buf + 2 * GCH + coff(rb, k));
-        fb[i][s][1] = *reinterpret_cast<const h8*>(buf + 3 * GCH + coff(rb, k));
-      }
-    if (c + 1 < nk) {  // park chunk c + 1 in the other buffer, fetch chunk c + 2
-      _Float16* nb = sm + ((c + 1) & 1) * 4 * GCH;
-      SA.store(nb, sa, tid);
-      SB.store(nb + 2 * GCH, sb, tid);
-      if (c + 2 < nk) {
-        SA.load(g.A, g.lda, g.M, g.K, m0, (c + 2) * GKC, tid, va);
-        SB.load(g.B, g.ldb, g.N, g.K, n0, (c + 2) * GKC, tid, vb);
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mma(fa[i][s][1], fb[j][s][0], acc[i][j]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mma(fa[i][s][0], fb[j][s][1], acc[i][j]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mma(fa[i][s][0], fb[j][s][0], acc[i][j]);
-    }
-    __syncthreads();
+  // iteration c: fragments of chunk c (LDS buffer c & 1); chunk c + 1 from ring slot RA / RB into
+  // the other buffer; that slot then fetches chunk c + 3; the MFMAs of chunk c
+#define GEMM_ITER(c, RA, RB)                                                                        \
+  {                                                                                                 \
+    const _Float16* buf = sm + ((c) & 1) * 4 * GCH;                                                 \
+    h8 fa[2][2][2], fb[2][2][2];                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                   \
+    _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                                 \
+      const int ra = wm * 64 + 32 * i + r, rb = wn * 64 + 32 * i + r, k = 16 * s + 8 * h;           \
+      fa[i][s][0] = *reinterpret_cast<const h8*>(buf + coff(ra, k));                                \
+      fa[i][s][1] = *reinterpret_cast<const h8*>(buf + GCH + coff(ra, k));                          \
+      fb[i][s][0] = *reinterpret_cast<const h8*>(buf + 2 * GCH + coff(rb, k));                      \
+      fb[i][s][1] = *reinterpret_cast<const h8*>(buf + 3 * GCH + coff(rb, k));                      \
+    }                                                                                               \
+    if ((c) + 1 < nk) {                                                                             \
+      _Float16* nb = sm + (((c) + 1) & 1) * 4 * GCH;                                                \
+      RA.store(nb, sa, tid);                                                                        \
+      RB.store(nb + 2 * GCH, sb, tid);                                                              \
+      if ((c) + 3 < nk) {                                                                           \
+        RA.load(g.A, g.lda, g.M, ke, m0, kb + ((c) + 3) * GKC, tid, va);                            \
+        RB.load(g.B, g.ldb, g.N, ke, n0, kb + ((c) + 3) * GKC, tid, vb);                            \
+      }                                                                                             \
+    }                                                                                               \
+    _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                                 \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                 \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[i][j] = mma(fa[i][s][1], fb[j][s][0], acc[i][j]); \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                 \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[i][j] = mma(fa[i][s][0], fb[j][s][1], acc[i][j]); \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                 \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[i][j] = mma(fa[i][s][0], fb[j][s][0], acc[i][j]); \
+    }                                                                                               \
+    __syncthreads();                                                                                \
   }
+  for (int c = 0; c < nk; c += 2) {
+    GEMM_ITER(c, SA1, SB1)  // chunk c + 1 (odd) lives in slot 1
+    if (c + 1 < nk) GEMM_ITER(c + 1, SA0, SB0)
+  }
+#undef GEMM_ITER
 
   // epilogue: C rows m = m0 + wm 64 + 32 i + acc_row(q), column n = n0 + wn 64 + 32 j + r
+  const bool split = g.splits > 1;
+  float* const Cout = split ? g.part + (size_t)blockIdx.z * g.M * g.N : g.C;
+  const int ldc = split ? g.N : g.ldc;
   float cmax = 0.f;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -217,12 +238,12 @@ __global__ __launch_bounds__(256) void k_gemm_sf16(GemmArgs g) {
           const float gg = g.aux[(size_t)m * g.ldaux + n];
           v *= 1.f - gg * gg;
         }
-        if (g.accumulate) v += g.C[(size_t)m * g.ldc + n];
-        g.C[(size_t)m * g.ldc + n] = v;
+        if (g.accumulate && !split) v += g.C[(size_t)m * g.ldc + n];
+        Cout[(size_t)m * ldc + n] = v;
         cmax = fmaxf(cmax, fabsf(v));
       }
   }
-  if (g.cmax) {
+  if (g.cmax && !split) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cmax = fmaxf(cmax, __shfl_xor(cmax, o, 64));
     if (l == 0) atomicMax(g.cmax, __float_as_uint(cmax));
@@ -243,19 +264,45 @@ __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int
   if ((threadIdx.x & 63) == 0) atomicMax(slot, __float_as_uint(mx));
 }
 
-// column sums of a [rows][cols] matrix: out[c] (+)= sum_r x[r][c]; one thread per column, f64
-__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ x, int rows, int cols, int ld,
+// column sums of a [rows][cols] matrix over the row range of layer blockIdx.y (rows_per rows):
+// out[y * cols + c] (or, with one layer, out[c] (+)=) = sum_r x[r][c]; one thread per column, f64
+__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ x, int rows, int cols, int ld, int rows_per,
                                                 float* __restrict__ out, int accumulate) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
   double s = 0.0;
-  for (int rr = 0; rr < rows; ++rr) s += (double)x[(size_t)rr * ld + c];
-  out[c] = accumulate ? out[c] + (float)s : (float)s;
+  for (int rr = r0; rr < r1; ++rr) s += (double)x[(size_t)rr * ld + c];
+  if (gridDim.y > 1) out[(size_t)blockIdx.y * cols + c] = (float)s;
+  else out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+// out[i] (+)= sum_z part[z][i] in a fixed order (f64): the second pass of split-K / split colsum;
+// out is [rows][ld] with n = rows * cols elements per layer
+__global__ __launch_bounds__(256) void k_split_reduce(const float* __restrict__ part, int splits, int rows, int cols,
+                                                      float* __restrict__ out, int ld, int accumulate) {
+  const size_t n = (size_t)rows * cols;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    double s = 0.0;
+    for (int z = 0; z < splits; ++z) s += (double)part[(size_t)z * n + i];
+    const size_t rr = i / cols, cc = i - rr * cols;
+    float* o = out + rr * ld + cc;
+    *o = accumulate ? *o + (float)s : (float)s;
+  }
+}
+
+static int launch_split_reduce(const float* part, int splits, int rows, int cols, float* out, int ld, int accumulate,
+                               hipStream_t s) {
+  const size_t n = (size_t)rows * cols;
+  const unsigned blocks = (unsigned)std::min<size_t>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(k_split_reduce, dim3(blocks), dim3(256), 0, s, part, splits, rows, cols, out, ld, accumulate);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
 }
 
 template <bool TA, bool TB>
 static int launch_t(const GemmArgs& a, hipStream_t s) {
-  const dim3 grid(cdiv(a.N, GT), cdiv(a.M, GT));
+  const dim3 grid(cdiv(a.N, GT), cdiv(a.M, GT), a.splits > 1 ? a.splits : 1);
   const size_t lds = (size_t)2 * 4 * GCH * sizeof(_Float16);
   switch (a.epi) {
     case GEMM_STORE: hipLaunchKernelGGL((k_gemm_sf16<TA, TB, GEMM_STORE>), grid, dim3(256), lds, s, a); break;
@@ -268,12 +315,30 @@ static int launch_t(const GemmArgs& a, hipStream_t s) {
   return RLKS_OK;
 }
 
-int launch_gemm_sf16(const GemmArgs& a, hipStream_t s) {
-  RLKS_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.A && a.B && a.C && a.amax && a.bmax, RLKS_ERR_ARG, "gemm: bad argument");
+static int launch_any(const GemmArgs& a, hipStream_t s) {
   if (!a.ta && !a.tb) return launch_t<false, false>(a, s);
   if (!a.ta && a.tb) return launch_t<false, true>(a, s);
   if (a.ta && !a.tb) return launch_t<true, false>(a, s);
   return launch_t<true, true>(a, s);
+}
+
+int gemm_splits(int M, int N, int K) {
+  const int tiles = cdiv(M, GT) * cdiv(N, GT);
+  int sp = std::max(1, 2048 / tiles);          // >= 2048 workgroups: 8 per CU
+  sp = std::min(sp, std::max(1, K / 512));     // >= 16 K chunks per workgroup
+  return std::min(sp, 64);
+}
+
+int launch_gemm_sf16(const GemmArgs& a, hipStream_t s) {
+  RLKS_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.A && a.B && a.C && a.amax && a.bmax, RLKS_ERR_ARG, "gemm: bad argument");
+  if (a.splits <= 1) return launch_any(a, s);
+  RLKS_REQUIRE(a.part && a.epi == GEMM_STORE, RLKS_ERR_ARG, "gemm: split-K needs a partial buffer and GEMM_STORE");
+  // layers beyond the last non-empty K range would write zero partials: trim them
+  const int kper = ((cdiv(a.K, a.splits) + GKC - 1) / GKC) * GKC;
+  GemmArgs b = a;
+  b.splits = cdiv(a.K, kper);
+  if (int rc = launch_any(b, s)) return rc;
+  return launch_split_reduce(a.part, b.splits, a.M, a.N, a.C, a.ldc, a.accumulate, s);
 }
 
 int launch_absmax(const float* x, int rows, int cols, int ld, unsigned* slot, hipStream_t s) {
@@ -284,10 +349,17 @@ int launch_absmax(const float* x, int rows, int cols, int ld, unsigned* slot, hi
   return RLKS_OK;
 }
 
-int launch_colsum(const float* x, int rows, int cols, int ld, float* out, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(k_colsum, dim3(cdiv(cols, 256)), dim3(256), 0, s, x, rows, cols, ld, out, accumulate);
+int colsum_splits(int rows) { return std::min(128, std::max(1, rows / 512)); }
+
+int launch_colsum(const float* x, int rows, int cols, int ld, float* out, int accumulate, float* part,
+                  hipStream_t s) {
+  const int sp = part ? colsum_splits(rows) : 1;
+  const int rows_per = cdiv(rows, sp);
+  hipLaunchKernelGGL(k_colsum, dim3(cdiv(cols, 256), sp), dim3(256), 0, s, x, rows, cols, ld, rows_per,
+                     sp > 1 ? part : out, accumulate);
   RLKS_LAUNCHED();
-  return RLKS_OK;
+  if (sp == 1) return RLKS_OK;
+  return launch_split_reduce(part, sp, 1, cols, out, cols, accumulate, s);
 }
 
 }  // namespace rlks

@@ -14,6 +14,7 @@ struct WideWs {
   WideNet n[2];
   float *dza, *dzb;  // [M][H] dZ2 / dZ1
   double* rew64;     // [M] env-step scratch (rollout)
+  float* part;       // split-K / split column-sum partials of the weight gradients
   unsigned* stat_slots;
   int64_t bytes;
   int M, blocks;

@@ -48,6 +48,13 @@ WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
   w.dza = (float*)take(4LL * M * H);
   w.dzb = (float*)take(4LL * M * H);
   w.rew64 = (double*)take(8LL * M);
+  {  // weight-gradient partials: dW3 [A][H], dW2 [H][H], dW1 [H][D] (K = M), column sums of M rows
+    int64_t pf = (int64_t)colsum_splits(M) * H;
+    pf = std::max(pf, (int64_t)gemm_splits(A, H, M) * A * H);
+    pf = std::max(pf, (int64_t)gemm_splits(H, H, M) * H * H);
+    pf = std::max(pf, (int64_t)gemm_splits(H, D, M) * H * D);
+    w.part = (float*)take(4 * pf);
+  }
   w.stat_slots = (unsigned*)take(4 * 4);
   w.bytes = o;
   return w;
@@ -193,8 +200,12 @@ Net net_of(const float* params, const Layout& L, int net) {
 
 int gemm(const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C, int ldc, int M, int N, int K,
          int epi, const float* bias, const float* aux, int ldaux, const unsigned* amax, const unsigned* bmax,
-         unsigned* cmax, hipStream_t s) {
+         unsigned* cmax, hipStream_t s, float* part = nullptr) {
   GemmArgs g{};
+  if (part) {  // weight gradient (K = minibatch rows): split K over workgroup layers
+    g.splits = gemm_splits(M, N, K);
+    g.part = part;
+  }
   g.A = A; g.B = B; g.C = C; g.bias = bias; g.aux = aux;
   g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldaux = ldaux;
   g.ta = ta; g.tb = tb; g.epi = epi; g.accumulate = 0;
@@ -260,25 +271,25 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     RLKS_LAUNCHED();
     // head: dW3 = dout^T H2, db3 = colsum(dout)
     if (int rc = gemm(n.dout, An, 1, n.h2, H, 0, g + o[4], H, An, H, M, GEMM_STORE, nullptr, nullptr, 0,
-                      sl + SL_DOUT, sl + SL_H2, nullptr, s))
+                      sl + SL_DOUT, sl + SL_H2, nullptr, s, w.part))
       return rc;
-    if (int rc = launch_colsum(n.dout, M, An, An, g + o[5], 0, s)) return rc;
+    if (int rc = launch_colsum(n.dout, M, An, An, g + o[5], 0, w.part, s)) return rc;
     // dZ2 = (dout W3) (1 - H2^2); dW2 = dZ2^T H1; db2
     if (int rc = gemm(n.dout, An, 0, P.w3, H, 0, w.dza, H, M, H, An, GEMM_DTANH, nullptr, n.h2, H, sl + SL_DOUT,
                       sl + SL_W3, sl + SL_DZ2, s))
       return rc;
     if (int rc = gemm(w.dza, H, 1, n.h1, H, 0, g + o[2], H, H, H, M, GEMM_STORE, nullptr, nullptr, 0, sl + SL_DZ2,
-                      sl + SL_H1, nullptr, s))
+                      sl + SL_H1, nullptr, s, w.part))
       return rc;
-    if (int rc = launch_colsum(w.dza, M, H, H, g + o[3], 0, s)) return rc;
+    if (int rc = launch_colsum(w.dza, M, H, H, g + o[3], 0, w.part, s)) return rc;
     // dZ1 = (dZ2 W2) (1 - H1^2); dW1 = dZ1^T X; db1
     if (int rc = gemm(w.dza, H, 0, P.w2, H, 0, w.dzb, H, M, H, H, GEMM_DTANH, nullptr, n.h1, H, sl + SL_DZ2,
                       sl + SL_W2, sl + SL_DZ1, s))
       return rc;
     if (int rc = gemm(w.dzb, H, 1, mb, stride, 0, g + o[0], D, H, D, M, GEMM_STORE, nullptr, nullptr, 0, sl + SL_DZ1,
-                      sl + SL_X, nullptr, s))
+                      sl + SL_X, nullptr, s, w.part))
       return rc;
-    if (int rc = launch_colsum(w.dzb, M, H, H, g + o[1], 0, s)) return rc;
+    if (int rc = launch_colsum(w.dzb, M, H, H, g + o[1], 0, w.part, s)) return rc;
   }
   if (stats) {
     hipLaunchKernelGGL(k_wide_stats, dim3(1), dim3(64), 0, s, w.n[0].part_stat, w.n[1].part_stat, w.blocks, M, stats);

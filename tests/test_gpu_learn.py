@@ -170,7 +170,8 @@ def test_ppo_grad_matches_oracle(rows, A, precision):
     assert st[4] == rows
 
 
-@pytest.mark.parametrize("rows,D,H,A", [(512, 6, 256, 2), (384, 12, 512, 4), (256, 192, 2048, 64), (300, 24, 96, 8)])
+@pytest.mark.parametrize("rows,D,H,A", [(512, 6, 256, 2), (384, 12, 512, 4), (256, 192, 2048, 64), (300, 24, 96, 8),
+                                        (8192, 24, 512, 8), (4096, 192, 2048, 64)])  # split-K weight gradients
 def test_wide_grad_matches_oracle(rows, D, H, A):
     """generic-width path (wide_mlp.hip: split-fp16 GEMMs with fused epilogues), incl. the c5 shape
     (obs 3 x 64 clusters, 64 actions, hidden 2048) and ragged rows; same 1e-5 bar"""
