@@ -61,6 +61,11 @@ int rlks_env_config(const rlks_env* env, rlks_env_cfg* out);
 int rlks_env_seed(rlks_env* env, const uint8_t* mask_dev, const uint32_t* keys_dev,
                   const int32_t* keylen_dev, int key_stride, void* stream);
 
+/* Advance each masked lane's MT19937 stream by n_draws_dev[lane] random() calls (int64 per lane;
+ * MT19937 mode only).  Batched evaluation uses it to give lane e the stream position of episode e
+ * of the reference's sequential loop (final_evaluation.py:42-49, one process-global generator). */
+int rlks_env_mt_discard(rlks_env* env, const uint8_t* mask_dev, const int64_t* n_draws_dev, void* stream);
+
 /* reset() (:106-112) for the lanes in mask (NULL = all): current_step = 0, obs of row 0. */
 int rlks_env_reset(rlks_env* env, const uint8_t* mask_dev, float* obs_dev, void* stream);
 

@@ -21,6 +21,16 @@
 namespace rlks {
 
 // ----------------------------------------------------------------------------- kernels
+// Skip n_draws[lane] calls of random() (2 words each) on every masked lane: positions lane e of a
+// batched evaluation at the point of the process-global stream that episode e of the reference's
+// sequential loop starts from (final_evaluation.py:42-49: 200 draws per 99-step episode).
+__global__ void k_mt_discard(EnvView v, const uint8_t* __restrict__ mask, const int64_t* __restrict__ n_draws) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= v.N) return;
+  if (mask && !mask[lane]) return;
+  for (int64_t i = 2 * n_draws[lane]; i > 0; --i) (void)mt_next(v.mt, v.N, lane);
+}
+
 __global__ void k_mt_seed(EnvView v, const uint8_t* __restrict__ mask, const uint32_t* __restrict__ keys,
                           const int32_t* __restrict__ keylen, int key_stride, uint64_t default_seed) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
@@ -628,6 +638,16 @@ int rlks_env_seed(rlks_env* e, const uint8_t* mask, const uint32_t* keys, const 
   RLKS_REQUIRE(!keys || (keylen && key_stride > 0), RLKS_ERR_ARG, "rlks_env_seed: bad key arrays");
   hipLaunchKernelGGL(k_mt_seed, dim3(cdiv(e->cfg.n_envs, ENV_BLOCK)), dim3(ENV_BLOCK), 0,
                      (hipStream_t)stream, view(e), mask, keys, keylen, key_stride, e->cfg.seed);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_env_mt_discard(rlks_env* e, const uint8_t* mask, const int64_t* n_draws, void* stream) {
+  RLKS_REQUIRE(e && n_draws, RLKS_ERR_ARG, "rlks_env_mt_discard: null argument");
+  RLKS_REQUIRE(e->cfg.noise_mode == RLKS_NOISE_MT19937, RLKS_ERR_STATE,
+               "rlks_env_mt_discard: only the MT19937 noise mode has per-lane generator state");
+  hipLaunchKernelGGL(k_mt_discard, dim3(cdiv(e->cfg.n_envs, ENV_BLOCK)), dim3(ENV_BLOCK), 0,
+                     (hipStream_t)stream, view(e), mask, n_draws);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }

@@ -82,6 +82,7 @@ SIGNATURES = {
     "rlks_env_counters": [_P, _I, _P, _P],
     "rlks_env_config": [_P, C.POINTER(EnvCfg)],
     "rlks_env_seed": [_P, _P, _P, _P, _I, _P],
+    "rlks_env_mt_discard": [_P, _P, _P, _P],
     "rlks_env_reset": [_P, _P, _P, _P],
     "rlks_env_step": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "rlks_env_sample_step": [_P, _P, _I, _P, _P, _P, _P, _P, _P],

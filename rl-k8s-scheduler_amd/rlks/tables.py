@@ -79,13 +79,51 @@ def load_table(path=None) -> Table:
     return _from_columns(z["table"], [str(c) for c in z["columns"]], str(PACKAGED))
 
 
+def minmax_scale(x: np.ndarray) -> np.ndarray:
+    """sklearn MinMaxScaler().fit_transform per column (normalize_data.py:25-26), in its own
+    arithmetic: scale = 1 / range (a zero range counts as 1), min = -data_min * scale,
+    x * scale + min; NaNs are ignored by the fit and kept"""
+    x = np.asarray(x, dtype=np.float64)
+    lo, hi = np.nanmin(x, axis=0), np.nanmax(x, axis=0)
+    rng = hi - lo
+    scale = 1.0 / np.where(rng == 0.0, 1.0, rng)
+    return x * scale + (0.0 - lo * scale)
+
+
+def build_reference_table(steps: int = 100, seed: int = 42, cpu_aws=None, cpu_azure=None) -> Table:
+    """generate_real_pricing.py:3-18 + normalize_data.py:5-29 restated.
+
+    np.random.seed(seed); cost_aws = 0.0104 + U(-0.001, 0.001), cost_azure = 0.0208 + U(...),
+    latency_aws = 70 + U(-10, 10), latency_azure = 60 + U(-10, 10) (draws in that order); the cpu
+    columns hold one value in row 0 (the mean Locust 'Average Response Time', :14-15, None = NaN)
+    and NaN below; every column min-max scaled.  The result differs from the committed CSV by
+    < 5e-14 (its writer's platform and pandas' CSV round trip), so the committed bits stay the
+    env's source of truth (load_table); this builder feeds tables of other lengths and seeds."""
+    rs = np.random.RandomState(seed)
+    cols = {"step": np.arange(steps, dtype=np.float64)}
+    cols["cost_aws"] = 0.0104 + rs.uniform(-0.001, 0.001, steps)
+    cols["cost_azure"] = 0.0208 + rs.uniform(-0.001, 0.001, steps)
+    cols["latency_aws"] = 70 + rs.uniform(-10, 10, steps)
+    cols["latency_azure"] = 60 + rs.uniform(-10, 10, steps)
+    for name, v in (("cpu_aws", cpu_aws), ("cpu_azure", cpu_azure)):
+        c = np.full(steps, np.nan)
+        c[0] = np.nan if v is None else float(v)
+        cols[name] = c
+    names = list(cols)
+    raw = np.stack([cols[n] for n in names], axis=1)
+    with np.errstate(invalid="ignore"):
+        norm = np.column_stack([minmax_scale(raw[:, j]) if not np.all(np.isnan(raw[:, j])) else raw[:, j]
+                                for j in range(raw.shape[1])])
+    return _from_columns(norm, names, f"build_reference_table(steps={steps}, seed={seed})")
+
+
 def synthetic_table(n_clouds: int, n_rows: int = 100, seed: int = 42) -> Table:
     """C-cloud table in the style of generate_real_pricing.py:3-18 + normalize_data.py:18-29.
 
     Per cloud c: cost = base_c + U(-0.001, 0.001) with base_c ~ U(0.009, 0.022), latency =
     lat_c + U(-10, 10) with lat_c ~ U(50, 80); every column then min-max scaled to [0, 1]
-    (sklearn MinMaxScaler semantics: (x - min) / (max - min)).  At C = 2 with the reference's
-    bases (0.0104 / 0.0208 and 70 / 60) this is the reference generator.
+    (minmax_scale: sklearn MinMaxScaler arithmetic).  At C = 2 the bases are the reference's
+    (0.0104 / 0.0208 and 70 / 60) and the cost / latency columns equal build_reference_table's.
     """
     rng = np.random.RandomState(seed)
     if n_clouds == 2:
@@ -95,13 +133,8 @@ def synthetic_table(n_clouds: int, n_rows: int = 100, seed: int = 42) -> Table:
         lbase = rng.uniform(50.0, 80.0, n_clouds)
     cost = np.stack([cbase[c] + rng.uniform(-0.001, 0.001, n_rows) for c in range(n_clouds)], axis=1)
     lat = np.stack([lbase[c] + rng.uniform(-10, 10, n_rows) for c in range(n_clouds)], axis=1)
-
-    def mm(x):
-        lo, hi = x.min(axis=0), x.max(axis=0)
-        return (x - lo) / np.where(hi > lo, hi - lo, 1.0)
-
-    cost, lat = mm(cost), mm(lat)
+    cost, lat = minmax_scale(cost), minmax_scale(lat)
     names = [f"c{c}" for c in range(n_clouds)]
     cols = ["step"] + [f"cost_{n}" for n in names] + [f"latency_{n}" for n in names]
-    raw = np.concatenate([np.linspace(0, 1, n_rows)[:, None], cost, lat], axis=1)
+    raw = np.concatenate([minmax_scale(np.arange(n_rows, dtype=np.float64)[:, None]), cost, lat], axis=1)
     return Table(np.ascontiguousarray(cost), np.ascontiguousarray(lat), cols, raw, f"synthetic(C={n_clouds})")

@@ -124,8 +124,9 @@ def test_tables(golden_table):
     with pytest.raises(FileNotFoundError, match="normalize_data.py"):
         load_table("/nonexistent/normalized_rl_data.csv")
     s = synthetic_table(8, seed=42)
-    assert s.cost.shape == (100, 8) and s.cost.min() == 0.0 and s.cost.max() == 1.0
-    assert np.all(s.latency.min(0) == 0.0) and np.all(s.latency.max(0) == 1.0)
+    # MinMaxScaler arithmetic (x * scale + min): the column maximum lands within a few ulp of 1
+    assert s.cost.shape == (100, 8) and s.cost.min() == 0.0 and abs(s.cost.max() - 1.0) <= 1e-15
+    assert np.all(s.latency.min(0) == 0.0) and np.all(np.abs(s.latency.max(0) - 1.0) <= 1e-15)
 
 
 def test_drop_in_import_paths():
