@@ -231,9 +231,10 @@ template <int A_, int NET, int KD, int NG, int W>
 __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
   constexpr int NTHR = 64 * W;
   constexpr int KS = KD / 16;   // k-steps of the first layer
-  // NG: accumulator row groups (8 rows each) holding the rows d <= D of dW1a^T.  NG = 1 (D < 8,
-  // the reference's 2-cloud obs) accumulates dW1a^T in LDS; wider obs keep it in registers.
-  constexpr bool DW1_LDS = NG == 1;
+  // NG: accumulator row groups (8 rows each) holding the rows d <= D of dW1a^T.  Each k-tile's
+  // dW1a^T block goes to an LDS slot (double-buffered over k-tiles) and is summed over the W waves
+  // two k-tiles later, so no accumulator outlives its k-tile (registers stay below 512 for A = 8).
+  constexpr int DWR = 8 * NG;   // LDS rows per dW1a^T column
   const SfNet& N = g.n[NET];
   extern __shared__ __attribute__((aligned(16))) float lds[];
   _Float16* sCh = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][SF_CH]  (64 KB)
@@ -241,7 +242,7 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
   float* sW3 = sB2 + HID;                            // [A_][HID]
   _Float16* sW1 = reinterpret_cast<_Float16*>(sW3 + A_ * HID);  // [2 hi/lo][HID k][KD] (swizzled)
   h8* sXT = reinterpret_cast<h8*>(sW1 + 2 * HID * KD);          // [W][2 s][2 hi/lo][64 lanes]
-  float* sDW = reinterpret_cast<float*>(sXT + W * 4 * 64);   // DW1_LDS: [2][W][32 k][8 d]
+  float* sDW = reinterpret_cast<float*>(sXT + W * 4 * 64);   // [2][W][32 k][DWR d]
 
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int D = g.D, stride = g.x_stride;
@@ -530,15 +531,22 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
   SF_STAMP(5);
   // ---- dH1 = dZ2 W2 per 32-column k-tile; dZ1 = dH1 (1 - H1^2); dW1a^T = Xa^T dZ1
   // dZ1 enters the split at 2^(e_dz + e_w2 - 23): |dH1 2^(e_dz + e_w2)| <= 256 2^15 2^15
-  float dw1[DW1_LDS ? 1 : 8][4 * NG];
   const int blk = blockIdx.x;
-  auto dw1_flush = [&](int kt) {  // thread tid < 32 (D + 1): element (k = 32 kt + tid / (D+1), d)
-    const int nd = D + 1, kk = tid / nd, d = tid - kk * nd, k = 32 * kt + kk;
-    float s = 0.f;
+  auto dw1_flush = [&](int kt) {  // elements (k = 32 kt + e / (D+1), d = e mod (D+1)), fixed wave order
+    const int nd = D + 1;
+    auto one = [&](int e) {
+      const int kk = e / nd, d = e - kk * nd, k = 32 * kt + kk;
+      float s = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < W; ++ww) s += sDW[(((kt & 1) * W + ww) * 32 + kk) * 8 + d];
-    if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
-    else N.part_b1[(size_t)blk * HID + k] = s;
+      for (int ww = 0; ww < W; ++ww) s += sDW[(((kt & 1) * W + ww) * 32 + kk) * DWR + d];
+      if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
+      else N.part_b1[(size_t)blk * HID + k] = s;
+    };
+    if constexpr (32 * DWR <= NTHR) {  // one element per thread at most
+      if (tid < 32 * nd) one(tid);
+    } else {
+      for (int e = tid; e < 32 * nd; e += NTHR) one(e);
+    }
   };
   const float sz1 = pow2(-23);
   const float u1 = pow2(23 - ex - edz - e_w2);
@@ -578,13 +586,11 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
     wacc2 = mma(x1h, zh[1], wacc2);
 #pragma unroll
     for (int q = 0; q < 16; ++q) wacc[q] += wacc2[q];
-    if constexpr (DW1_LDS) {
-      // rows d = 4h + 0..3 of column k: one 16-byte store into this wave's slot of k-tile kt
-      float4 v = {wacc[0] * u1, wacc[1] * u1, wacc[2] * u1, wacc[3] * u1};
-      *reinterpret_cast<float4*>(sDW + (((kt & 1) * W + w) * 32 + r) * 8 + 4 * h) = v;
-    } else {
+    // rows d = 8g + 4h + 0..3 of column k: 16-byte stores into this wave's slot of k-tile kt
 #pragma unroll
-      for (int q = 0; q < 4 * NG; ++q) dw1[kt][q] = wacc[q] * u1;
+    for (int gq = 0; gq < NG; ++gq) {
+      float4 v = {wacc[4 * gq] * u1, wacc[4 * gq + 1] * u1, wacc[4 * gq + 2] * u1, wacc[4 * gq + 3] * u1};
+      *reinterpret_cast<float4*>(sDW + (((kt & 1) * W + w) * 32 + r) * DWR + 8 * gq + 4 * h) = v;
     }
   };
   f32x16 der, dprev, derprev;
@@ -632,43 +638,16 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
       derprev[q] = der[q];
       der[q] = nder[q];
     }
-    if constexpr (DW1_LDS)
-      if (kt > 1 && tid < 32 * (D + 1)) dw1_flush(kt - 2);
+    if (kt > 1) dw1_flush(kt - 2);
     vm_drain();
     __syncthreads();
   }
   dw1_tile(7, dprev, derprev);
-  if constexpr (DW1_LDS) {
-    if (tid < 32 * (D + 1)) dw1_flush(6);
-    __syncthreads();
-  }
+  dw1_flush(6);
+  __syncthreads();
   SF_STAMP(6);
-  // ---- workgroup epilogue: fixed-order sums of dW1a^T over the 8 waves -> per-block partials
-  if constexpr (DW1_LDS) {
-    if (tid < 32 * (D + 1)) dw1_flush(7);
-  } else {
-    float* sP = reinterpret_cast<float*>(sCh);  // [W][HID][8] per pass of 8 rows
-    for (int d0 = 0; d0 <= D; d0 += 8) {
-#pragma unroll
-      for (int kt = 0; kt < 8; ++kt)
-#pragma unroll
-        for (int q = 0; q < 4 * NG; ++q) {
-          const int d = acc_row(q, l);
-          if (d >= d0 && d < d0 + 8 && d <= D) sP[(w * HID + 32 * kt + r) * 8 + (d - d0)] = dw1[kt][q];
-        }
-      __syncthreads();
-      const int nd = min(8, D + 1 - d0);
-      for (int e = tid; e < HID * nd; e += NTHR) {
-        const int k = e / nd, dd = e - k * nd, d = d0 + dd;
-        float s = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < W; ++ww) s += sP[(ww * HID + k) * 8 + dd];
-        if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
-        else N.part_b1[(size_t)blk * HID + k] = s;
-      }
-      __syncthreads();
-    }
-  }
+  // ---- workgroup epilogue: the last k-tile's fixed-order sum over the W waves
+  dw1_flush(7);
   SF_STAMP(7);
 }
 
@@ -829,7 +808,7 @@ extern "C" int rlks_dbg_sf_stamps(unsigned long long* host) {
 size_t sf_f1_lds_bytes(int A_, int NG, int KD, int W) {
   return (size_t)2 * 2 * SF_CH * sizeof(_Float16) + (size_t)(HID + A_ * HID) * sizeof(float) +
          (size_t)2 * HID * KD * sizeof(_Float16) + (size_t)W * 4 * 64 * 16 +
-         (NG == 1 ? (size_t)2 * W * 32 * 8 * sizeof(float) : 0);
+         (size_t)2 * W * 32 * 8 * NG * sizeof(float);
 }
 
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
