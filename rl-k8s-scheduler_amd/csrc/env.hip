@@ -142,7 +142,24 @@ __global__ void k_env_step(EnvView v, const double* __restrict__ cost, const dou
 // LDS, wave 0 does the reward / step / episode bookkeeping, the auto-reset lanes re-draw their
 // occupancy, and the whole workgroup writes the 64 contiguous obs rows.  Same order and counters
 // as oracle/rlks_oracle.c:nodes_step_lane.
-constexpr int NODE_CHUNK = 8;
+constexpr int NODE_CHUNK = 16;
+// Cache policy of the node sweep.  NT (streaming) loads and stores suit a sweep that rewrites few
+// nodes: at c3's stationary churn (~1e-3 writes per node-step) they raise the sweep from 57% to
+// 61% of HBM peak.  With heavy churn the partial-line write-backs of non-resident lines cost more
+// than NT saves (depart_prob 0.02: 0.36 -> 0.44 ms), so launch_node_step picks the policy from the
+// expected writes per node.
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ void node_store(int2* p, int2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(i32x2{v.x, v.y}, reinterpret_cast<i32x2*>(p));
+  else *p = v;
+}
+template <bool NT>
+__device__ __forceinline__ i32x4 node_load2(const int4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(p));
+  else return *reinterpret_cast<const i32x4*>(p);
+}
 
 __device__ __forceinline__ float node_obs(const EnvView& v, const double* __restrict__ cost,
                                           const double* __restrict__ lat, const int32_t* s_used, int row,
@@ -154,6 +171,7 @@ __device__ __forceinline__ float node_obs(const EnvView& v, const double* __rest
   return __fdiv_rn((float)s_used[c * 64 + e], (float)(v.nodes * v.cap[c]));
 }
 
+template <bool NT>
 __global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __restrict__ cost,
                                                     const double* __restrict__ lat,
                                                     const int32_t* __restrict__ actions, float* __restrict__ obs,
@@ -186,7 +204,7 @@ __global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __r
   __syncthreads();
   const uint32_t gid = (uint32_t)(v.env_offset + env);
   const int32_t pc = v.pod_cpu, pm = v.pod_mem;
-  int2* base = v.free + (size_t)blockIdx.x * (size_t)C * N * 64 + l;
+  int2* base = v.free + (size_t)blockIdx.x * (size_t)C * N * 64 + 2 * l;
   unsigned long long n_checks = 0, n_placed = 0, n_rej = 0, n_dep = 0, n_wr = 0;
   for (int c = w; c < C; c += W) {
     int32_t used = 0;
@@ -196,19 +214,23 @@ __global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __r
       int passed = 0, placed = 0, departed = 0, written = 0;
       int2* col = base + (size_t)c * N * 64;
       int32_t sum_free = 0;
-      const int2* p = col;
-      for (int n0 = 0; n0 < N; n0 += NODE_CHUNK, p += NODE_CHUNK * 64) {
+      const int4* p = reinterpret_cast<const int4*>(col);
+      for (int n0 = 0; n0 < N; n0 += NODE_CHUNK, p += NODE_CHUNK / 2 * 64) {
         int2 f[NODE_CHUNK];
         int pods[NODE_CHUNK];
 #pragma unroll
-        for (int q = 0; q < NODE_CHUNK; ++q) f[q] = p[q * 64];  // immediate offsets from one pointer
+        for (int q = 0; q < NODE_CHUNK / 2; ++q) {  // 16 B per lane: a node pair, one pointer
+          const i32x4 x = node_load2<NT>(p + q * 64);
+          f[2 * q] = make_int2(x[0], x[1]);
+          f[2 * q + 1] = make_int2(x[2], x[3]);
+        }
         int any = 0;
 #pragma unroll
         for (int q = 0; q < NODE_CHUNK; ++q) {
           pods[q] = (int)(__umul24((uint32_t)(cc - f[q].x), v.pod_mag) >> v.pod_shift);
           any |= pods[q];
         }
-        int2* pw = col + (size_t)n0 * 64;
+        int2* pw = col + (size_t)n0 * 64;  // node n0 + q at pw[node_off(q)] (n0 even)
         unsigned dep_mask = 0;  // nodes already written by a departure this chunk
         if (any) {  // departures: every pod-slot leaves with depart_prob (4 nodes per Philox draw)
 #pragma unroll
@@ -236,7 +258,7 @@ __global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __r
                 departed += d;
                 ++written;
                 dep_mask |= 1u << q;
-                pw[q * 64] = f[q];
+                node_store<NT>(pw + node_off(q), f[q]);
               }
             }
           }
@@ -254,7 +276,7 @@ __global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __r
                 put = true;
               }
               if (put) {
-                pw[q * 64] = f[q];
+                node_store<NT>(pw + node_off(q), f[q]);
                 written += !((dep_mask >> q) & 1u);  // one write-back per node, as the oracle counts
               }
               if (rem > 0) ++passed;
@@ -437,7 +459,7 @@ __global__ void k_node_transpose(EnvView v, int32_t* __restrict__ fc, int32_t* _
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // destination index
   if (i >= cn * v.N) return;
   const size_t lane = i / cn, g = i % cn;
-  const int2 f = node_col(v, (int)lane)[g * 64];
+  const int2 f = node_col(v, (int)lane)[node_off(g)];
   if (fc) fc[i] = f.x;
   if (fm) fm[i] = f.y;
 }
@@ -675,8 +697,14 @@ int rlks_env_step(rlks_env* e, const int32_t* actions, float* obs, double* rew64
   if (e->cfg.nodes_per_cluster > 0) {
     const int C = e->cfg.n_clouds, W = std::min(C, 16), M1 = e->maxp + 1;
     const size_t lds = (size_t)M1 * 16 + (size_t)M1 * M1 * sizeof(uint32_t) + ((size_t)C * 64 + 3 * 64) * sizeof(int32_t);
-    hipLaunchKernelGGL(k_node_step, dim3(cdiv(e->cfg.n_envs, 64)), dim3(64 * W), lds, s, view(e), e->d_cost,
-                       e->d_lat, actions, obs, rew64, rew32, term, trunc, step_out, final_obs, status);
+    // expected node writes per node-step ~ depart_prob x mean pods (+ arrivals, < 1 per env-step)
+    const bool nt = e->cfg.depart_prob * e->maxp < 0.02;
+    if (nt)
+      hipLaunchKernelGGL(k_node_step<true>, dim3(cdiv(e->cfg.n_envs, 64)), dim3(64 * W), lds, s, view(e), e->d_cost,
+                         e->d_lat, actions, obs, rew64, rew32, term, trunc, step_out, final_obs, status);
+    else
+      hipLaunchKernelGGL(k_node_step<false>, dim3(cdiv(e->cfg.n_envs, 64)), dim3(64 * W), lds, s, view(e), e->d_cost,
+                         e->d_lat, actions, obs, rew64, rew32, term, trunc, step_out, final_obs, status);
     RLKS_LAUNCHED();
     return RLKS_OK;
   }

@@ -32,7 +32,7 @@ struct rlks_env {
   int n_trace;
   int maxp;             // most pods a node can hold (over all clusters)
   uint32_t* d_cdf;      // [maxp+1][maxp+1] Binomial(n, depart_prob) CDF in 1/65536 units
-  int2* d_free;         // [ceil(n_envs/64)][C*N][64] {free millicores, free MiB}
+  int2* d_free;         // [ceil(n_envs/64)][C*N/2][64][2] {free millicores, free MiB}
   int32_t* d_used_cpu;  // [C][n_envs]
   unsigned long long* d_counters;  // [5] node checks, pods placed, pods rejected, pods departed,
                                    // nodes written (opt-in)
@@ -115,14 +115,17 @@ __device__ __forceinline__ double noise(const EnvView& v, int lane, int t, int c
 
 // ---------------------------------------------------------------- node-level extension
 // DESIGN.md §4 (builder-defined; same algorithm and the same Philox counters as
-// oracle/rlks_oracle.c).  Node state is int2 {free cpu, free mem}, tiled by wavefront:
-// [ceil(n_envs/64)][C*N][64], so a wave's read of node g is one coalesced 512-byte access and a
-// workgroup's 64 envs occupy one contiguous C*N*512-byte region that the step kernel streams.
+// oracle/rlks_oracle.c).  Node state is int2 {free cpu, free mem}, tiled by wavefront in node
+// pairs: [ceil(n_envs/64)][C*N/2][64 lanes][2 nodes], so a wave's read of nodes (2p, 2p+1) is one
+// coalesced 1-KB access of 16 B per lane and a workgroup's 64 envs occupy one contiguous
+// C*N*512-byte region that the step kernel streams.  Node g of a lane sits at col[node_off(g)].
 __device__ __forceinline__ int2* node_col(const EnvView& v, int lane) {  // node 0 of `lane`
-  return v.free + (size_t)(lane >> 6) * (size_t)v.C * v.nodes * 64 + (lane & 63);
+  return v.free + (size_t)(lane >> 6) * (size_t)v.C * v.nodes * 64 + 2 * (lane & 63);
 }
+__device__ __forceinline__ size_t node_off(size_t g) { return (g >> 1) * 128 + (g & 1); }
 
-// initial occupancy of cluster c for one lane (episode `episode`); col = node_col(lane) + c*N*64.
+// initial occupancy of cluster c for one lane (episode `episode`); col = node_col(lane) + c*N*64
+// (N even: cluster c starts on a pair boundary).
 // Returns the cluster's used millicores.
 __device__ __forceinline__ int32_t nodes_reset_cluster(const EnvView& v, int2* col, int c, uint32_t gid,
                                                        int episode) {
@@ -136,7 +139,7 @@ __device__ __forceinline__ int32_t nodes_reset_cluster(const EnvView& v, int2* c
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int32_t pods = (int32_t)(((uint64_t)w[j] * (uint64_t)m1) >> 32);
-      col[(size_t)(n4 + j) * 64] = make_int2(cc - pods * v.pod_cpu, cm - pods * v.pod_mem);
+      col[node_off(n4 + j)] = make_int2(cc - pods * v.pod_cpu, cm - pods * v.pod_mem);
       used += pods * v.pod_cpu;
     }
   }
