@@ -56,8 +56,23 @@ __device__ __forceinline__ int coff(int row, int k) {
 template <bool T>
 struct Stager {
   float4 v[4];
+  // interior chunk: four unmasked float4 loads, issued back to back (the masked path compiles to a
+  // load -> wait per element, which serialises the loads' latency)
+  __device__ __forceinline__ void load_full(const float* X, int ld, int r0, int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = tid + 256 * i;
+      const size_t off = !T ? (size_t)(r0 + (f >> 3)) * ld + k0 + 4 * (f & 7)
+                            : (size_t)(k0 + 4 * (tid >> 5) + i) * ld + r0 + 4 * (tid & 31);
+      v[i] = *reinterpret_cast<const float4*>(X + off);
+    }
+  }
   // vec: ld % 4 == 0 and X 16-byte aligned (float4 loads), else four scalar loads
   __device__ __forceinline__ void load(const float* X, int ld, int rows, int K, int r0, int k0, int tid, bool vec) {
+    if (vec && r0 + GT <= rows && k0 + GKC <= K) {
+      load_full(X, ld, r0, k0, tid);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = tid + 256 * i;
@@ -178,7 +193,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __syncthreads();
   // iteration c: fragments of chunk c (LDS buffer c & 1); chunk c + 1 from ring slot RA / RB into
   // the other buffer; that slot then fetches chunk c + 3; the MFMAs of chunk c
-#define GEMM_ITER(c, RA, RB)                                                                        \
+#define GEMM_ITER(c, RA, RB, STEADY)                                                                \
   {                                                                                                 \
     const _Float16* buf = sm + ((c) & 1) * 4 * GCH;                                                 \
     h8 fa[2][2][2], fb[2][2][2];                                                                    \
@@ -190,11 +205,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       fb[i][s][0] = *reinterpret_cast<const h8*>(buf + 2 * GCH + coff(rb, k));                      \
       fb[i][s][1] = *reinterpret_cast<const h8*>(buf + 3 * GCH + coff(rb, k));                      \
     }                                                                                               \
-    if ((c) + 1 < nk) {                                                                             \
+    if (STEADY || (c) + 1 < nk) {                                                                   \
       _Float16* nb = sm + (((c) + 1) & 1) * 4 * GCH;                                                \
       RA.store(nb, sa, tid);                                                                        \
       RB.store(nb + 2 * GCH, sb, tid);                                                              \
-      if ((c) + 3 < nk) {                                                                           \
+      if (STEADY) {                                                                                 \
+        RA.load_full(g.A, g.lda, m0, kb + ((c) + 3) * GKC, tid);                                    \
+        RB.load_full(g.B, g.ldb, n0, kb + ((c) + 3) * GKC, tid);                                    \
+      } else if ((c) + 3 < nk) {                                                                    \
         RA.load(g.A, g.lda, g.M, ke, m0, kb + ((c) + 3) * GKC, tid, va);                            \
         RB.load(g.B, g.ldb, g.N, ke, n0, kb + ((c) + 3) * GKC, tid, vb);                            \
       }                                                                                             \
@@ -209,9 +227,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }                                                                                               \
     __syncthreads();                                                                                \
   }
-  for (int c = 0; c < nk; c += 2) {
-    GEMM_ITER(c, SA1, SB1)  // chunk c + 1 (odd) lives in slot 1
-    if (c + 1 < nk) GEMM_ITER(c + 1, SA0, SB0)
+  // steady state (interior tile, every operand chunk whole): branch-free bodies with unmasked loads;
+  // then the general masked iterations for the last chunks (or the whole range of an edge tile)
+  int c = 0;
+  if (va && vb && m0 + GT <= g.M && n0 + GT <= g.N && kb + nk * GKC <= ke) {
+    for (; c + 4 < nk; c += 2) {
+      GEMM_ITER(c, SA1, SB1, true)  // chunk c + 1 (odd) lives in slot 1
+      GEMM_ITER(c + 1, SA0, SB0, true)
+    }
+  }
+  for (; c < nk; c += 2) {
+    GEMM_ITER(c, SA1, SB1, false)
+    if (c + 1 < nk) GEMM_ITER(c + 1, SA0, SB0, false)
   }
 #undef GEMM_ITER
 
