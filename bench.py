@@ -299,8 +299,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL ("nccl") over xGMI, one GPU per rank.  RLKS_DIST_BACKEND=gloo is for rehearsing the
+        # multi-rank path with several ranks on fewer GPUs (ranks share devices round-robin).
+        backend = os.environ.get("RLKS_DIST_BACKEND", "nccl")
+        device = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
+        torch.cuda.set_device(device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
