@@ -277,14 +277,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-// max |x| over a strided [rows][cols] fp32 matrix -> atomicMax slot (slot zeroed by the caller)
+// max |x| over a strided [rows][cols] fp32 matrix -> atomicMax slot (slot zeroed by the caller).
+// Contiguous matrices (ld == cols, 16-B aligned, n % 4 == 0) are swept as one float4 stream;
+// strided ones row by row (block-stride rows, thread-stride columns): no per-element division.
 __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int rows, int cols, int ld,
-                                                unsigned* __restrict__ slot) {
+                                                unsigned* __restrict__ slot, int flat4) {
   float mx = 0.f;
-  const size_t n = (size_t)rows * cols;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-    const size_t rr = i / cols, cc = i - rr * cols;
-    mx = fmaxf(mx, fabsf(x[rr * ld + cc]));
+  if (flat4) {
+    const size_t n4 = (size_t)rows * cols / 4;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+      const float4 v = x4[i];
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  } else {
+    for (int rr = blockIdx.x; rr < rows; rr += gridDim.x)
+      for (int cc = threadIdx.x; cc < cols; cc += 256) mx = fmaxf(mx, fabsf(x[(size_t)rr * ld + cc]));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -321,8 +329,11 @@ __global__ __launch_bounds__(256) void k_split_reduce(const float* __restrict__ 
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
     double s = 0.0;
     for (int z = 0; z < splits; ++z) s += (double)part[(size_t)z * n + i];
-    const size_t rr = i / cols, cc = i - rr * cols;
-    float* o = out + rr * ld + cc;
+    float* o = out + i;
+    if (ld != cols) {  // strided destination (no division for the common contiguous case)
+      const size_t rr = i / cols, cc = i - rr * cols;
+      o = out + rr * ld + cc;
+    }
     *o = accumulate ? *o + (float)s : (float)s;
   }
 }
@@ -379,8 +390,10 @@ int launch_gemm_sf16(const GemmArgs& a, hipStream_t s) {
 
 int launch_absmax(const float* x, int rows, int cols, int ld, unsigned* slot, hipStream_t s) {
   const size_t n = (size_t)rows * cols;
-  const unsigned blocks = (unsigned)std::min<size_t>(1024, (n + 255) / 256);
-  hipLaunchKernelGGL(k_absmax, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, x, rows, cols, ld, slot);
+  const int flat4 = ld == cols && n % 4 == 0 && ((uintptr_t)x & 15) == 0;
+  const size_t units = flat4 ? (n / 4 + 255) / 256 : (size_t)rows;
+  const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(2048, units));
+  hipLaunchKernelGGL(k_absmax, dim3(blocks), dim3(256), 0, s, x, rows, cols, ld, slot, flat4);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }
