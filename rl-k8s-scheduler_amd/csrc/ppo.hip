@@ -162,21 +162,23 @@ struct GatherArgs {
   float* mb;
 };
 
+// one thread per record element (row i = e / stride, field j): the record stores are fully
+// coalesced and each row's fields are read contiguously; the row's permuted source index is
+// recomputed per element (a few dozen ALU ops against a scattered 4-byte load)
 __global__ void k_gather(GatherArgs g) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.rows) return;
-  const uint64_t s = perm_apply(g.perm, (uint64_t)(g.row0 + i));
-  const int64_t tn = (int64_t)s;  // = t * N + n of the time-major buffers
-  float* rec = g.mb + (size_t)i * g.stride;
-  const float* o = g.b.obs + tn * g.D;
-  for (int d = 0; d < g.D; ++d) rec[d] = o[d];
-  const float* lo = g.b.logits + tn * g.A;
-  for (int a = 0; a < g.A; ++a) rec[g.D + a] = lo[a];
-  rec[g.D + g.A] = g.b.adv[tn];
-  rec[g.D + g.A + 1] = g.b.vtarg[tn];
-  rec[g.D + g.A + 2] = g.b.logp[tn];
-  rec[g.D + g.A + 3] = (float)g.b.actions[tn];
-  for (int j = g.D + g.A + 4; j < g.stride; ++j) rec[j] = 0.f;
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (uint32_t)g.rows * (uint32_t)g.stride) return;
+  const uint32_t i = e / (uint32_t)g.stride, j = e - i * (uint32_t)g.stride;
+  const int64_t tn = (int64_t)perm_apply(g.perm, (uint64_t)(g.row0 + i));  // = t * N + n
+  const int D = g.D, A = g.A;
+  float v = 0.f;
+  if ((int)j < D) v = g.b.obs[tn * D + j];
+  else if ((int)j < D + A) v = g.b.logits[tn * A + (j - D)];
+  else if ((int)j == D + A) v = g.b.adv[tn];
+  else if ((int)j == D + A + 1) v = g.b.vtarg[tn];
+  else if ((int)j == D + A + 2) v = g.b.logp[tn];
+  else if ((int)j == D + A + 3) v = (float)g.b.actions[tn];
+  g.mb[(size_t)e] = v;
 }
 
 static Perm make_perm(uint64_t seed, int epoch, uint64_t S) {
@@ -433,7 +435,9 @@ int rlks_ppo_gather(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, uint64_t
   g.A = d->n_actions;
   g.stride = mb_stride(d->obs_dim, d->n_actions);
   g.mb = mb;
-  hipLaunchKernelGGL(k_gather, dim3(cdiv(rows, 256)), dim3(256), 0, (hipStream_t)stream, g);
+  RLKS_REQUIRE((int64_t)rows * g.stride < (int64_t)1 << 31, RLKS_ERR_UNSUPPORTED,
+               "rlks_ppo_gather: at most 2^31 record elements per call");
+  hipLaunchKernelGGL(k_gather, dim3(cdiv(rows * g.stride, 256)), dim3(256), 0, (hipStream_t)stream, g);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Add k_node_step's per-launch HBM traffic (separate --pmc FETCH_SIZE / WRITE_SIZE passes over
+tools/node_step_time.py, gfx950 correction FETCH x 2) to profiles/pmc_traffic.json, keyed by the
+cache-policy variant (<true> = streaming, the c3 stationary case; <false> = default, heavy churn).
+
+usage: pmc_node_traffic.py <fetch counter csv> <write counter csv> <source> [pmc_traffic.json]"""
+import collections
+import csv
+import json
+import sys
+
+
+def per_kernel(path, counter):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter and "k_node_step" in r["Kernel_Name"]:
+            d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in d.items()}
+
+
+def main():
+    fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE"), per_kernel(sys.argv[2], "WRITE_SIZE")
+    dst = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
+    out = json.load(open(dst))
+    for k, f in fetch.items():
+        key = "k_node_step_streaming" if "<true>" in k else "k_node_step_default"
+        rd, wr = f * 1024 * 2, write.get(k, 0.0) * 1024
+        out[key] = {"kernel": k, "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+                    "source": sys.argv[3]}
+    json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
+    print(json.dumps({k: v for k, v in out.items() if k.startswith("k_node_step")}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
