@@ -274,6 +274,14 @@ def node_env_timing(algo, torch, timed, n=65536, C=8, nodes=256, depart_prob="st
            "node_checks_per_step": checks, "placed_per_step": placed, "rejected_per_step": rejected,
            "departed_per_step": departed, "nodes_written_per_step": written,
            "bytes_per_step": algo_bytes, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
+    # HBM bytes per launch from the committed PMC passes (tools/pmc_node_traffic.py), for the cache
+    # policy this churn selects (csrc/env.hip: streaming when depart_prob x max pods < 0.02)
+    pmc = pmc_traffic()
+    key = "k_node_step_streaming" if spec.depart_prob * int(np.max(spec.max_pods())) < 0.02 else "k_node_step_default"
+    if pmc and key in pmc and (n, C, nodes) == (65536, 8, 256):
+        res["traffic"] = pmc[key]["hbm_bytes_per_launch"]
+        res["traffic_over_algorithmic"] = pmc[key]["hbm_bytes_per_launch"] / (algo_bytes * n)
+        res["traffic_source"] = pmc[key]["source"]
     venv.close()
     return res
 

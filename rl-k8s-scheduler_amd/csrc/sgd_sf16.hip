@@ -106,6 +106,14 @@ __device__ __forceinline__ void sched_interleave() {
   }
 }
 
+// Xa = [X | 1 | 0] element d of a row: a load from a clamped column and an arithmetic select (X is
+// finite), so the load is unconditional and a row's loads issue back to back instead of as one
+// exec-masked load -> wait per element
+__device__ __forceinline__ float xa_elem(const float* __restrict__ xr, int d, int D) {
+  const float v = xr[d < D ? d : D - 1];
+  return fmaf(v, d < D ? 1.f : 0.f, d == D ? 1.f : 0.f);
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -261,7 +269,7 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int d = 16 * ks + 8 * h + j;
-      xv[ks * 8 + j] = d < D ? xr[d] : (d == D ? 1.f : 0.f);
+      xv[ks * 8 + j] = xa_elem(xr, d, D);
     }
   float xm = 0.f;
 #pragma unroll
@@ -359,7 +367,7 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int m = sf_perm(s, h, j);
-      xtv[s * 8 + j] = r < D ? g.x[(size_t)(row0 + m) * stride + r] : (r == D ? 1.f : 0.f);
+      xtv[s * 8 + j] = xa_elem(g.x + (size_t)(row0 + m) * stride, r, D);
     }
   // ---- H2^T = tanh(Z2^T + b2), head out[a] = b3 + sum_n W3[a][n] H2[n]
   const float inv_z2 = inv_w2 / SF_H1_SCALE;
