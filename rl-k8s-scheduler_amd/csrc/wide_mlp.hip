@@ -20,7 +20,6 @@
 
 namespace rlks {
 
-constexpr int WIDE_MAXA = 64;
 constexpr int LOSS_ROWS = 256;  // rows per loss block (stats partials)
 
 enum { SL_X = 0, SL_W1, SL_W2, SL_W3, SL_H1, SL_H2, SL_DOUT, SL_DZ2, SL_DZ1, SL_N = 16 };
