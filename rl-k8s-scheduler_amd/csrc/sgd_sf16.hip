@@ -675,6 +675,8 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   const SfNet& N = g.n[net];
   extern __shared__ __attribute__((aligned(16))) float lds[];
   _Float16* sA = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][HID n][32 m perm]
+  // fp32 dZ2^T tiles landed by LDS-DMA: [2 slots][2048 float4] (float4 f = tid + 512 i of a tile)
+  float4* sStage = reinterpret_cast<float4*>(sA + 2 * 2 * SF_CH);
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int D = g.D, stride = g.x_stride;
   const int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
@@ -692,19 +694,24 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
     wl[ks] = *reinterpret_cast<const h8*>(N.w1l + (32 * w + r) * KD + 16 * ks + 8 * h);
   }
 
-  float4 pv[4];
   float db2[4] = {0.f, 0.f, 0.f, 0.f};
+  // tile t's 32 KB into stage slot (t - t0) & 1: each lane's 16 bytes land at the wave's base +
+  // 16 lane, i.e. at float4 index tid + 512 i (no register round trip, no compiler-inserted wait)
   auto load = [&](int t) {
+    float4* dst = sStage + ((t - t0) & 1) * 2048;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      pv[i] = *reinterpret_cast<const float4*>(N.dz2t + (size_t)t * HID * 32 + (size_t)(tid + 512 * i) * 4);
+      __builtin_amdgcn_global_load_lds(N.dz2t + (size_t)t * HID * 32 + (size_t)(tid + 512 * i) * 4,
+                                       (__attribute__((address_space(3))) void*)(dst + 512 * i + 64 * w), 16, 0, 0);
   };
-  auto store = [&](int buf) {
+  // split tile t (stage slot) into the MFMA buffer `buf`
+  auto store = [&](int t, int buf) {
     _Float16* b = sA + buf * 2 * SF_CH;
+    const float4* src = sStage + ((t - t0) & 1) * 2048;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = tid + 512 * i, n = f >> 3, c = f & 7;
-      const float4 v = pv[i];
+      const float4 v = src[f];
       db2[i] += (v.x + v.y) + (v.z + v.w);
       const float vv[4] = {v.x, v.y, v.z, v.w};
       h4 hi, lo;
@@ -729,8 +736,10 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
     for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
 
   load(t0);
-  store(0);
   if (t0 + 1 < t1) load(t0 + 1);
+  vm_drain();
+  __syncthreads();
+  store(t0, 0);
   __syncthreads();
   // X rows of the next tile are loaded one iteration ahead (their latency hides behind the MFMAs)
   float xnext[KS * 8];
@@ -747,6 +756,9 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   load_x(t0);
   for (int t = t0; t < t1; ++t) {
     const int buf = (t - t0) & 1;
+    // tile t + 2 into the stage slot tile t left (split into `buf` before the last barrier); it
+    // lands while this tile's MFMAs run
+    if (t + 2 < t1) load(t + 2);
     // H1 tile (rows m in registers, columns k = 32w + r on lanes) as the B operand
     h8 bh[2], bl[2];
     {
@@ -785,8 +797,9 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
         acc[nt] = mma3(ah, al, bh[s], bl[s], acc[nt]);
       }
     }
-    if (t + 1 < t1) store(buf ^ 1);
-    if (t + 2 < t1) load(t + 2);
+    // tile t + 1 (landed during the previous iteration) split into the other MFMA buffer
+    if (t + 1 < t1) store(t + 1, buf ^ 1);
+    vm_drain();
     __syncthreads();
   }
   float* out = N.part_w2 + (size_t)blockIdx.x * HID * HID;
@@ -851,7 +864,7 @@ int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s) {
 }
 
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {
-  const size_t lds = (size_t)2 * 2 * SF_CH * sizeof(_Float16);
+  const size_t lds = (size_t)2 * 2 * SF_CH * sizeof(_Float16) + (size_t)2 * 2048 * 16;  // + fp32 stage
   if (sf_kd(a.D) == 16) hipLaunchKernelGGL(k_sf_dw2<16>, dim3(splits, 2), dim3(512), lds, s, a);
   else hipLaunchKernelGGL(k_sf_dw2<32>, dim3(splits, 2), dim3(512), lds, s, a);
   RLKS_LAUNCHED();
