@@ -119,12 +119,30 @@ class RlksError(RuntimeError):
 _lib = None
 
 
+def _warn_if_stale() -> None:
+    """Warn when a HIP source or header is newer than the library about to be loaded: a library
+    left over from an earlier build would otherwise be measured and tested silently."""
+    if "RLKS_LIB" in os.environ:
+        return
+    csrc = PKG_DIR.parent / "csrc"
+    srcs = [p for pat in ("*.hip", "*.h") for p in csrc.glob(pat)]
+    srcs += list((PKG_DIR.parent.parent / "include").glob("*.h"))
+    if not srcs:
+        return
+    newest = max(srcs, key=lambda p: p.stat().st_mtime)
+    if newest.stat().st_mtime > LIB_PATH.stat().st_mtime + 1.0:
+        import warnings
+
+        warnings.warn(f"{LIB_PATH} is older than {newest.name}; rebuild with `make -C {csrc}`", stacklevel=3)
+
+
 def lib() -> C.CDLL:
     """Load librlks.so once; raises if it is absent (no fallback path exists)."""
     global _lib
     if _lib is None:
         if not LIB_PATH.exists():
             raise RlksError(f"librlks.so not found at {LIB_PATH}; build it with `make -C {PKG_DIR.parent / 'csrc'}`")
+        _warn_if_stale()
         handle = C.CDLL(str(LIB_PATH))
         for name, argtypes in SIGNATURES.items():
             fn = getattr(handle, name)
