@@ -257,7 +257,7 @@ struct SfWs {
 static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   SfWs w{};
   const int KD = sf_kd(D), tiles = M / 32;
-  w.blocks = M / 128;  // F1 workgroups of 4 x 32 rows
+  w.blocks = M / (32 * SF_F1_W);  // F1 workgroups of SF_F1_W x 32 rows
   w.splits = 1;
   while (w.splits * 2 <= 128 && tiles % (w.splits * 2) == 0) w.splits *= 2;
   w.tiles_per_split = tiles > 0 ? tiles / w.splits : 0;

@@ -4,6 +4,13 @@
 #include "mlp_common.h"
 
 namespace rlks {
+#ifndef RLKS_F1_W
+#define RLKS_F1_W 4
+#endif
+constexpr int SF_F1_W = RLKS_F1_W;  // waves per F1 workgroup (one per SIMD); 32 rows each
+}  // namespace rlks
+
+namespace rlks {
 
 struct SfNetW {
   const float *w1, *b1, *w2;

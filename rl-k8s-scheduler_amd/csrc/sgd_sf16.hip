@@ -36,7 +36,6 @@ namespace rlks {
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
 
-constexpr int SF_F1_W = 4;          // waves per F1 workgroup (one per SIMD)
 constexpr int SF_ROWS = 256;        // minibatch rows must be a multiple of this
 constexpr int SF_CH = 8192;         // halves per staged chunk (per hi / lo array)
 constexpr float SF_H1_SCALE = 16384.f;  // tanh outputs (|h| < 1) scaled by 2^14
