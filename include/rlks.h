@@ -93,6 +93,24 @@ int rlks_env_sample_step(rlks_env* env, const float* logits_dev, int explore, in
  * zeroes the accumulators (PPO result "episode_reward_mean", train_ppo.py:29-30). */
 int rlks_env_episode_stats(rlks_env* env, double* out_dev, int clear, void* stream);
 
+/* Completed-episode log since the last clear: returns_dev[RLKS_EPLOG_CAP] (float64) and
+ * keys_dev[RLKS_EPLOG_CAP] (int64: episode << 32 | global lane) of the first RLKS_EPLOG_CAP
+ * episodes, count_dev[0] (uint32) = all episodes completed (may exceed the capacity).  Sorting by
+ * key gives completion order.  Feeds RLlib's 100-episode smoothing of episode_reward_mean
+ * (metrics_num_episodes_for_smoothing; train_ppo.py:29-30 prints it).  Any pointer may be NULL. */
+int rlks_env_episode_log(rlks_env* env, double* returns_dev, long long* keys_dev, unsigned* count_dev,
+                         int clear, void* stream);
+
+/* Snapshot of every per-lane state a resumed run needs (step / episode counters, episode returns,
+ * MT19937 words, node free cpu / mem and per-cluster used cpu): rlks_env_state_bytes gives the
+ * size; save / load copy it to / from a device buffer of that size, asynchronously on `stream`.
+ * Checkpoint / resume (agent.save() each iteration, train_ppo.py:31;
+ * PPO.from_checkpoint, eval_ppo.py:17).  Philox draws are keyed by (lane, episode, step), so the
+ * counters restore the random streams too. */
+int rlks_env_state_bytes(const rlks_env* env, int64_t* bytes);
+int rlks_env_save_state(const rlks_env* env, void* dst_dev, void* stream);
+int rlks_env_load_state(rlks_env* env, const void* src_dev, void* stream);
+
 /* node-level extension: free millicores / MiB per node as [n_envs][n_clouds][nodes] and the
  * per-cluster used millicores [n_envs][n_clouds] (any pointer may be NULL) */
 int rlks_env_node_state(rlks_env* env, int32_t* free_cpu_dev, int32_t* free_mem_dev, int32_t* used_cpu_dev,
@@ -183,6 +201,16 @@ int rlks_minibatch_stride(const rlks_mlp_desc* desc);
 int rlks_ppo_gather(const rlks_mlp_desc* desc, const rlks_rollout_bufs* bufs, uint64_t perm_seed,
                     int epoch, int64_t row0, int rows, const float* dyn_dev, float* mb_dev,
                     void* stream);
+/* Same over `groups` equal blocks of lanes (global block ids group0 .. group0 + groups - 1): block
+ * k has its own permutation of its T * (N / groups) samples and supplies rows / groups rows of every
+ * minibatch (rows [k rows/groups, (k+1) rows/groups) of mb_dev, row0 / groups onwards in its
+ * order).  A run on W ranks with one block each then draws exactly the minibatches of a
+ * single-rank run over all lanes with W blocks: training is independent of the world size up to
+ * fp32 summation order.  groups (<= 64) must divide N, rows and row0.  groups = 1, group0 = 0 is
+ * rlks_ppo_gather. */
+int rlks_ppo_gather_grouped(const rlks_mlp_desc* desc, const rlks_rollout_bufs* bufs, uint64_t perm_seed,
+                            int epoch, int groups, int group0, int64_t row0, int rows, const float* dyn_dev,
+                            float* mb_dev, void* stream);
 
 /* Gradient of the RLlib PPO loss (mean over `rows`*world rows via dyn[INV_COUNT]) w.r.t. the
  * flat parameters -> grad_dev (padded_count floats).  stats_dev (double[RLKS_STAT_SIZE]) gets

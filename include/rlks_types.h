@@ -22,6 +22,11 @@ enum {
   RLKS_NOISE_MT19937 = 1   /* per-lane CPython MT19937 (random.seed / random.random), bit-exact */
 };
 
+/* completed-episode log capacity (rlks_env_episode_log): RLlib smooths episode_reward_mean over at
+ * least the last 100 episodes (metrics_num_episodes_for_smoothing), so 100+ individual returns per
+ * iteration are all a host ever needs */
+enum { RLKS_EPLOG_CAP = 128 };
+
 /* Philox counter purposes (ctr[3] high half) */
 enum {
   RLKS_PURPOSE_OBS = 1,

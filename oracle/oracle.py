@@ -67,6 +67,8 @@ def lib():
         h.ro_binom_cdf32.argtypes = [C.c_int, C.c_double, C.c_void_p]
         h.ro_env_lane_step.argtypes = [C.c_void_p, C.c_int]
         h.ro_env_lane_episode.argtypes = [C.c_void_p, C.c_int]
+        h.ro_env_lane_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        h.ro_philox_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
         _lib = h
     return _lib
 
@@ -83,6 +85,58 @@ def philox(ctr, key):
     o, op = _u32(np.zeros(4))
     lib().ro_philox4x32_10(cp, kp, op)
     return o.copy()
+
+
+def philox_batch(ctr, key):
+    """Philox4x32-10 of counters ctr [n][4] under key [2] -> uint32 [n][4]"""
+    c = np.ascontiguousarray(ctr, np.uint32).reshape(-1, 4)
+    k = np.ascontiguousarray(key, np.uint32)
+    out = np.zeros_like(c)
+    lib().ro_philox_batch(c.ctypes.data, k.ctypes.data, out.ctypes.data, c.shape[0])
+    return out
+
+
+def u53(a, b):
+    """vectorised ro_u53 (exact in float64)"""
+    return ((a >> 5).astype(np.float64) * 67108864.0 + (b >> 6).astype(np.float64)) * (1.0 / 9007199254740992.0)
+
+
+PURPOSE_ACTION = 2  # include/rlks_types.h RLKS_PURPOSE_ACTION
+
+
+def sample_actions(logits, gids, episodes, steps, seed):
+    """TorchCategorical draws as the rollout kernels make them (rollout_sf16.hip k_sf_roll,
+    env.hip k_sample_step): u = f32(u53(Philox(ctr = {global lane, episode, step, ACTION << 16},
+    key = seed)) words 0, 1) * sum_a exp(l_a - max), action = first a with u < cumsum(exp(l - max))
+    (all float32, sums in index order).  logits [n][A] float32.
+    Returns (actions int32 [n], margin [n]: |u - nearest cumulative boundary| in units of
+    float32 ulp(boundary) — draws within a couple of ulp may differ by exp() rounding)."""
+    lg = np.asarray(logits, np.float32)
+    n, A = lg.shape
+    mx = lg.max(1, keepdims=True)
+    ex = np.exp(lg - mx).astype(np.float32)
+    se = np.zeros(n, np.float32)
+    for a in range(A):
+        se = (se + ex[:, a]).astype(np.float32)
+    ctr = np.zeros((n, 4), np.uint32)
+    ctr[:, 0] = np.asarray(gids, np.uint32)
+    ctr[:, 1] = np.asarray(episodes, np.uint32)
+    ctr[:, 2] = np.asarray(steps, np.uint32)
+    ctr[:, 3] = PURPOSE_ACTION << 16
+    x = philox_batch(ctr, [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF])
+    u = (u53(x[:, 0], x[:, 1]).astype(np.float32) * se).astype(np.float32)
+    act = np.full(n, A - 1, np.int32)
+    found = np.zeros(n, bool)
+    c = np.zeros(n, np.float32)
+    margin = np.full(n, np.inf)
+    for a in range(A):
+        c = (c + ex[:, a]).astype(np.float32)
+        hit = (~found) & (u < c)
+        act[hit] = a
+        found |= hit
+        if a < A - 1:
+            margin = np.minimum(margin, np.abs(u.astype(np.float64) - c) / np.spacing(np.maximum(c, 1e-30)))
+    return act, margin
 
 
 def seed_words(seed: int):
@@ -172,6 +226,16 @@ class OracleEnv:
     def lane_step(self, i):
         return lib().ro_env_lane_step(self.h, i)
 
+    def lane_episode(self, i):
+        return lib().ro_env_lane_episode(self.h, i)
+
+    def lane_counters(self):
+        """(step [n], episode [n]) int32 of every lane"""
+        st = np.zeros(self.n, np.int32)
+        ep = np.zeros(self.n, np.int32)
+        lib().ro_env_lane_counters(self.h, st.ctypes.data, ep.ctypes.data)
+        return st, ep
+
     def __del__(self):
         try:
             lib().ro_env_destroy(self.h)
@@ -225,18 +289,19 @@ def mlp_forward(flat, off, D, H, A, obs):
 
 
 def ppo_loss_grad(flat, off, D, H, A, mb, *, clip_param=0.3, vf_clip_param=10.0, vf_loss_coeff=1.0,
-                  entropy_coeff=0.0, kl_coeff=0.2, adv_mean=0.0, adv_inv_std=1.0, count=None):
-    """Gradient of RLlib's PPO torch loss w.r.t. the flat parameters, float64 autograd.
+                  entropy_coeff=0.0, kl_coeff=0.2, adv_mean=0.0, adv_inv_std=1.0, count=None, dtype=np.float64):
+    """Gradient of RLlib's PPO torch loss w.r.t. the flat parameters, float64 autograd
+    (dtype=np.float32: the same in torch fp32 on the CPU, the precision baseline of the tests).
 
     mb: packed minibatch records [rows][stride] = [obs D | logits_old A | adv | vtarg | logp_old | action]
     Returns (grad (same length as flat), stats dict of per-row sums).
     """
     import torch
 
-    rec = torch.as_tensor(np.asarray(mb, np.float64))
+    rec = torch.as_tensor(np.asarray(mb, dtype))
     rows = rec.shape[0]
     count = rows if count is None else count
-    f = torch.tensor(np.asarray(flat, np.float64), requires_grad=True)
+    f = torch.tensor(np.asarray(flat, dtype), requires_grad=True)
     x = rec[:, :D]
     lo = rec[:, D: D + A]
     adv = (rec[:, D + A] - adv_mean) * adv_inv_std
@@ -280,6 +345,128 @@ def adam(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8):
     denom = (vt.sqrt() / (bc2 ** 0.5)).add_(eps)
     pt.addcdiv_(mt, denom, value=-(lr / bc1))
     return pt.numpy(), mt.numpy(), vt.numpy()
+
+
+def adam64(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8):
+    """the same Adam step in float64 (numpy), the whole-iteration reference"""
+    m = m + (1 - beta1) * (g - m)
+    v = beta2 * v + (1 - beta2) * g * g
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    return p - (lr / bc1) * (m / (np.sqrt(v) / np.sqrt(bc2) + eps)), m, v
+
+
+# ----------------------------------------------------------------------------- minibatch order
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def _mix32(x):
+    x = x.astype(np.uint64)
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & _M32
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & _M32
+    x ^= x >> np.uint64(16)
+    return x
+
+
+def perm_keys(seed: int, epoch: int, S: int):
+    """(half, mask, round keys) of the per-epoch Feistel bijection (csrc/ppo.hip make_perm)"""
+    bits = 2
+    while (1 << bits) < S:
+        bits += 1
+    bits += bits & 1
+    half = bits // 2
+    m64 = (1 << 64) - 1
+    z = (seed ^ ((0x9E3779B97F4A7C15 * (epoch + 1)) & m64)) & m64
+    keys = []
+    for _ in range(4):  # splitmix64
+        z = (z + 0x9E3779B97F4A7C15) & m64
+        x = z
+        x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & m64
+        x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & m64
+        keys.append((x ^ (x >> 31)) & 0xFFFFFFFF)
+    return half, (1 << half) - 1, keys
+
+
+def epoch_permutation(seed: int, epoch: int, S: int) -> np.ndarray:
+    """sample index (t * N + n) of every minibatch row position of epoch `epoch`: a balanced
+    4-round Feistel network on [0, 2^(2 half)) cycle-walked into [0, S) — restates
+    csrc/ppo.hip perm_apply / k_gather (rows b*mb .. (b+1)*mb of the result form minibatch b)"""
+    half, mask, keys = perm_keys(seed, epoch, S)
+    x = np.arange(S, dtype=np.uint64)
+    out = np.empty(S, np.uint64)
+    todo = np.arange(S)
+    cur = x.copy()
+    sh, mk = np.uint64(half), np.uint64(mask)
+    while todo.size:
+        L, R = cur >> sh, cur & mk
+        for r in range(4):
+            nl = R
+            R = (L ^ _mix32(R ^ np.uint64(keys[r]))) & mk
+            L = nl
+        cur = (L << sh) | R
+        done = cur < np.uint64(S)
+        out[todo[done]] = cur[done]
+        todo, cur = todo[~done], cur[~done]
+    return out.astype(np.int64)
+
+
+GROUP_KEY = 0x632BE59BD9B4E019  # csrc/ppo.hip rlks_ppo_gather_grouped: per-group seed offset
+
+
+def minibatch_indices(seed: int, epoch: int, T: int, N: int, mb: int, groups: int = 1, group0: int = 0):
+    """[n_mb][mb] sample indices (t * N + n) of epoch `epoch`'s minibatches as
+    rlks_ppo_gather_grouped lays them out: lane block k (global id group0 + k) has its own Feistel
+    permutation of its T * (N / groups) samples and fills rows [k mb/g, (k+1) mb/g) of every
+    minibatch."""
+    Ng, mbg = N // groups, mb // groups
+    Sg = T * Ng
+    n_mb = Sg // mbg
+    out = np.empty((n_mb, mb), np.int64)
+    for k in range(groups):
+        s = (seed + GROUP_KEY * (group0 + k)) & ((1 << 64) - 1)
+        p = epoch_permutation(s, epoch, Sg)[: n_mb * mbg].reshape(n_mb, mbg)
+        out[:, k * mbg:(k + 1) * mbg] = (p // Ng) * N + k * Ng + (p % Ng)
+    return out
+
+
+def ppo_iteration(flat, off, D, H, A, buf, *, perm_seed, epochs, mb, lr, gamma=0.99, lam=1.0, kl_coeff=0.2,
+                  kl_target=0.01, adam_m=None, adam_v=None, adam_step=0, clip_param=0.3, vf_clip_param=10.0,
+                  vf_loss_coeff=1.0, entropy_coeff=0.0, groups=1):
+    """One PPO learner update in float64 over a recorded rollout (RLlib old-stack semantics as in
+    rlks.ppo: GAE, standardisation, `epochs` x (samples // mb) minibatches in the per-epoch Feistel
+    order, loss gradient by autograd, Adam, mean-KL coefficient update).  `buf` holds the rollout
+    arrays obs [T+1][N][D], logits [T][N][A], values [T+1][N], actions, logp, rewards, dones [T][N].
+    Returns (params, adam_m, adam_v, new kl_coeff, per-step stats)."""
+    T, N = buf["rewards"].shape
+    S = T * N
+    adv, vt = gae(buf["rewards"], buf["values"], buf["dones"], gamma, lam)
+    a = adv.reshape(-1)
+    mean, inv_std = a.mean(), 1.0 / max(1e-4, a.std())
+    rec = np.concatenate([buf["obs"][:T].reshape(S, D), buf["logits"].reshape(S, A), a[:, None],
+                          vt.reshape(S, 1), buf["logp"].reshape(S, 1), buf["actions"].reshape(S, 1)], axis=1)
+    p = np.asarray(flat, np.float64).copy()
+    m = np.zeros_like(p) if adam_m is None else np.asarray(adam_m, np.float64).copy()
+    v = np.zeros_like(p) if adam_v is None else np.asarray(adam_v, np.float64).copy()
+    step = adam_step
+    stats = []
+    for ep in range(epochs):
+        order = minibatch_indices(perm_seed, ep, T, N, mb, groups)
+        for b in range(order.shape[0]):
+            rows = rec[order[b]]
+            g, st = ppo_loss_grad(p, off, D, H, A, rows, clip_param=clip_param, vf_clip_param=vf_clip_param,
+                                  vf_loss_coeff=vf_loss_coeff, entropy_coeff=entropy_coeff, kl_coeff=kl_coeff,
+                                  adv_mean=mean, adv_inv_std=inv_std)
+            step += 1
+            p, m, v = adam64(p, g, m, v, step, lr)
+            stats.append(st)
+    kl = np.mean([s["kl"] / s["rows"] for s in stats])
+    if kl > 2.0 * kl_target:
+        kl_coeff *= 1.5
+    elif kl < 0.5 * kl_target:
+        kl_coeff *= 0.5
+    return p, m, v, kl_coeff, stats
 
 
 def binom_cdf32(maxp, p):

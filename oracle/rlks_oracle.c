@@ -44,6 +44,11 @@ void ro_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+/* n counters ctr[n][4] -> out[n][4] */
+void ro_philox_batch(const uint32_t* ctr, const uint32_t key[2], uint32_t* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) ro_philox4x32_10(ctr + 4 * i, key, out + 4 * i);
+}
+
 /* 53-bit uniform in [0,1) from two 32-bit words, CPython genrand_res53's construction */
 double ro_u53(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
@@ -346,6 +351,10 @@ int ro_env_seed_lane(ro_env* e, int lane, const uint32_t* key, int keylen) {
 
 int32_t ro_env_lane_step(const ro_env* e, int lane) { return e->step[lane]; }
 int32_t ro_env_lane_episode(const ro_env* e, int lane) { return e->episode[lane]; }
+void ro_env_lane_counters(const ro_env* e, int32_t* step, int32_t* episode) {
+  memcpy(step, e->step, (size_t)e->cfg.n_envs * sizeof(int32_t));
+  memcpy(episode, e->episode, (size_t)e->cfg.n_envs * sizeof(int32_t));
+}
 
 static double noise_draw(ro_env* e, int lane, int t, int c) {
   const rlks_env_cfg* cfg = &e->cfg;

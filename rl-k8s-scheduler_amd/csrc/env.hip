@@ -337,6 +337,7 @@ __global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __r
           if (done) {
             v.ret_sum[env] += ret;
             v.ep_cnt[env] += 1;
+            eplog_append(v, env, ep, ret);
             ret = 0.0;
           }
           v.ep_ret[env] = ret;
@@ -581,6 +582,9 @@ int rlks_env_create_ext(const rlks_env_cfg* cfg, const double* cost, const doubl
   alloc((void**)&e->d_ep_cnt, N * sizeof(int32_t));
   alloc((void**)&e->d_status, 4 * sizeof(int32_t));
   alloc((void**)&e->d_counters, 8 * sizeof(unsigned long long));
+  alloc((void**)&e->d_eplog, RLKS_EPLOG_CAP * sizeof(double));
+  alloc((void**)&e->d_eplog_key, RLKS_EPLOG_CAP * sizeof(long long));
+  alloc((void**)&e->d_eplog_n, sizeof(unsigned));
   if (cfg->noise_mode == RLKS_NOISE_MT19937) alloc((void**)&e->d_mt, (size_t)(MT_N + 1) * N * sizeof(uint32_t));
   if (err == hipSuccess) err = hipMemcpy(e->d_cost, cost, TC * sizeof(double), hipMemcpyHostToDevice);
   if (err == hipSuccess) err = hipMemcpy(e->d_lat, lat, TC * sizeof(double), hipMemcpyHostToDevice);
@@ -636,6 +640,7 @@ int rlks_env_destroy(rlks_env* e) {
   hipFree(e->d_cost); hipFree(e->d_lat); hipFree(e->d_step); hipFree(e->d_episode);
   hipFree(e->d_ep_ret); hipFree(e->d_ret_sum); hipFree(e->d_ep_cnt); hipFree(e->d_status);
   hipFree(e->d_counters);
+  hipFree(e->d_eplog); hipFree(e->d_eplog_key); hipFree(e->d_eplog_n);
   if (e->d_mt) hipFree(e->d_mt);
   if (e->d_cap) hipFree(e->d_cap);
   if (e->d_lam) hipFree(e->d_lam);
@@ -740,6 +745,73 @@ int rlks_env_lane_state(rlks_env* e, int32_t* steps, int32_t* episodes, void* st
   hipLaunchKernelGGL(k_lane_state, dim3(cdiv(e->cfg.n_envs, ENV_BLOCK)), dim3(ENV_BLOCK), 0,
                      (hipStream_t)stream, e->cfg.n_envs, e->d_step, e->d_episode, steps, episodes);
   RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_env_episode_log(rlks_env* e, double* returns, long long* keys, unsigned* count, int clear, void* stream) {
+  RLKS_REQUIRE(e, RLKS_ERR_ARG, "rlks_env_episode_log: null env");
+  hipStream_t s = (hipStream_t)stream;
+  if (returns) RLKS_HIP(hipMemcpyAsync(returns, e->d_eplog, RLKS_EPLOG_CAP * sizeof(double), hipMemcpyDeviceToDevice, s));
+  if (keys) RLKS_HIP(hipMemcpyAsync(keys, e->d_eplog_key, RLKS_EPLOG_CAP * sizeof(long long), hipMemcpyDeviceToDevice, s));
+  if (count) RLKS_HIP(hipMemcpyAsync(count, e->d_eplog_n, sizeof(unsigned), hipMemcpyDeviceToDevice, s));
+  if (clear) RLKS_HIP(hipMemsetAsync(e->d_eplog_n, 0, sizeof(unsigned), s));
+  return RLKS_OK;
+}
+
+// The per-lane state a resumed run needs, in a fixed order: step, episode, running and completed
+// returns, completed counts, MT19937 words (MT mode), node free cpu / mem and per-cluster used cpu
+// (node envs).  Philox draws need no state (counter = lane, episode, step, purpose).
+namespace {
+struct Seg { void* p; size_t bytes; };
+int env_segments(const rlks_env* e, Seg* out) {
+  const size_t N = e->cfg.n_envs;
+  int n = 0;
+  out[n++] = {e->d_step, N * sizeof(int32_t)};
+  out[n++] = {e->d_episode, N * sizeof(int32_t)};
+  out[n++] = {e->d_ep_ret, N * sizeof(double)};
+  out[n++] = {e->d_ret_sum, N * sizeof(double)};
+  out[n++] = {e->d_ep_cnt, N * sizeof(int32_t)};
+  if (e->d_mt) out[n++] = {e->d_mt, (size_t)(MT_N + 1) * N * sizeof(uint32_t)};
+  if (e->cfg.nodes_per_cluster > 0) {
+    out[n++] = {e->d_free, (size_t)e->cfg.n_clouds * e->cfg.nodes_per_cluster * cdiv((long)N, 64) * 64 * sizeof(int2)};
+    out[n++] = {e->d_used_cpu, (size_t)e->cfg.n_clouds * N * sizeof(int32_t)};
+  }
+  return n;
+}
+size_t aligned(size_t b) { return (b + 255) / 256 * 256; }
+}  // namespace
+
+int rlks_env_state_bytes(const rlks_env* e, int64_t* bytes) {
+  RLKS_REQUIRE(e && bytes, RLKS_ERR_ARG, "rlks_env_state_bytes: null argument");
+  Seg seg[8];
+  const int n = env_segments(e, seg);
+  size_t b = 0;
+  for (int i = 0; i < n; ++i) b += aligned(seg[i].bytes);
+  *bytes = (int64_t)b;
+  return RLKS_OK;
+}
+
+int rlks_env_save_state(const rlks_env* e, void* dst, void* stream) {
+  RLKS_REQUIRE(e && dst, RLKS_ERR_ARG, "rlks_env_save_state: null argument");
+  Seg seg[8];
+  const int n = env_segments(e, seg);
+  char* o = (char*)dst;
+  for (int i = 0; i < n; ++i) {
+    RLKS_HIP(hipMemcpyAsync(o, seg[i].p, seg[i].bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    o += aligned(seg[i].bytes);
+  }
+  return RLKS_OK;
+}
+
+int rlks_env_load_state(rlks_env* e, const void* src, void* stream) {
+  RLKS_REQUIRE(e && src, RLKS_ERR_ARG, "rlks_env_load_state: null argument");
+  Seg seg[8];
+  const int n = env_segments(e, seg);
+  const char* o = (const char*)src;
+  for (int i = 0; i < n; ++i) {
+    RLKS_HIP(hipMemcpyAsync(seg[i].p, o, seg[i].bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    o += aligned(seg[i].bytes);
+  }
   return RLKS_OK;
 }
 

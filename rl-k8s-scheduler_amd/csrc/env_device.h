@@ -37,6 +37,11 @@ struct rlks_env {
   unsigned long long* d_counters;  // [5] node checks, pods placed, pods rejected, pods departed,
                                    // nodes written (opt-in)
   int counters_on;
+  // completed-episode log since the last rlks_env_episode_log(clear): the first RLKS_EPLOG_CAP
+  // returns with key (episode << 32 | global lane); the count keeps running past the capacity
+  double* d_eplog;
+  long long* d_eplog_key;
+  unsigned* d_eplog_n;
 };
 
 namespace rlks {
@@ -65,6 +70,9 @@ struct EnvView {
   int2* free;           // [ceil(n_envs/64)][C*N][64] {free millicores, free MiB}: one 8-byte load per node
   int32_t* used_cpu;    // [C][n_envs]
   unsigned long long* counters;  // null unless enabled
+  double* eplog;        // [RLKS_EPLOG_CAP] completed-episode returns (see rlks_env)
+  long long* eplog_key;
+  unsigned* eplog_n;
 };
 
 inline EnvView view(const rlks_env* e) {
@@ -86,7 +94,25 @@ inline EnvView view(const rlks_env* e) {
   v.penalty = e->cfg.reject_penalty;
   v.cap = e->d_cap; v.lam = e->d_lam; v.cdf = e->d_cdf; v.free = e->d_free;
   v.used_cpu = e->d_used_cpu; v.counters = e->counters_on ? e->d_counters : nullptr;
+  v.eplog = e->d_eplog; v.eplog_key = e->d_eplog_key; v.eplog_n = e->d_eplog_n;
   return v;
+}
+
+// Append the returns of the lanes whose episode just ended.  Called by exactly those lanes (a
+// divergent branch): one atomic per wave, slots by rank among the active lanes.  The log order is
+// restored on the host by the key (episode, global lane), i.e. completion order (all lanes step in
+// lockstep), so the atomic's order does not matter.
+__device__ __forceinline__ void eplog_append(const EnvView& v, int lane, int episode, double ret) {
+  const unsigned long long m = __ballot(1);
+  const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+  unsigned base = 0;
+  if (rank == 0) base = atomicAdd(v.eplog_n, (unsigned)__popcll(m));
+  base = __builtin_amdgcn_readfirstlane(base);
+  const unsigned i = base + rank;
+  if (i < (unsigned)RLKS_EPLOG_CAP) {
+    v.eplog[i] = ret;
+    v.eplog_key[i] = ((long long)episode << 32) | (long long)(unsigned)(v.env_offset + lane);
+  }
 }
 
 // stage [T][C] cost then latency tables into LDS (f64)
@@ -220,6 +246,7 @@ __device__ __forceinline__ StepOut step_lane(const EnvView& v, const double* s_t
   if (r.done) {
     v.ret_sum[lane] += ret;
     v.ep_cnt[lane] += 1;
+    eplog_append(v, lane, ep, ret);
     ret = 0.0;
   }
   v.ep_ret[lane] = ret;

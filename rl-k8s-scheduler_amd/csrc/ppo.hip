@@ -154,22 +154,28 @@ __device__ __forceinline__ uint64_t perm_apply(const Perm& P, uint64_t x) {
   return x;
 }
 
+constexpr int MAX_GROUPS = 64;
 struct GatherArgs {
   rlks_rollout_bufs b;
-  Perm perm;
-  int64_t row0;
-  int rows, D, A, stride;
+  Perm perm[MAX_GROUPS];  // one bijection of [0, T * Ng) per lane group
+  int64_t row0g;          // first row of this minibatch within each group's permutation
+  int rows, rows_g, Ng, D, A, stride;
   float* mb;
 };
 
 // one thread per record element (row i = e / stride, field j): the record stores are fully
 // coalesced and each row's fields are read contiguously; the row's permuted source index is
-// recomputed per element (a few dozen ALU ops against a scattered 4-byte load)
+// recomputed per element (a few dozen ALU ops against a scattered 4-byte load).  Rows
+// [k rows_g, (k+1) rows_g) come from lane group k: its permutation p -> (t = p / Ng, lane
+// k Ng + p mod Ng).
 __global__ void k_gather(GatherArgs g) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (uint32_t)g.rows * (uint32_t)g.stride) return;
   const uint32_t i = e / (uint32_t)g.stride, j = e - i * (uint32_t)g.stride;
-  const int64_t tn = (int64_t)perm_apply(g.perm, (uint64_t)(g.row0 + i));  // = t * N + n
+  const uint32_t k = i / (uint32_t)g.rows_g, ii = i - k * (uint32_t)g.rows_g;
+  const uint64_t p = perm_apply(g.perm[k], (uint64_t)(g.row0g + ii));
+  const uint64_t t = p / (uint64_t)g.Ng, nl = p - t * (uint64_t)g.Ng;
+  const int64_t tn = (int64_t)(t * (uint64_t)g.b.N + (uint64_t)k * g.Ng + nl);  // = t * N + n
   const int D = g.D, A = g.A;
   float v = 0.f;
   if ((int)j < D) v = g.b.obs[tn * D + j];
@@ -421,15 +427,30 @@ int rlks_minibatch_stride(const rlks_mlp_desc* d) { return d ? mb_stride(d->obs_
 
 int rlks_ppo_gather(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, uint64_t perm_seed, int epoch,
                     int64_t row0, int rows, const float* dyn, float* mb, void* stream) {
+  return rlks_ppo_gather_grouped(d, b, perm_seed, epoch, 1, 0, row0, rows, dyn, mb, stream);
+}
+
+int rlks_ppo_gather_grouped(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, uint64_t perm_seed, int epoch,
+                            int groups, int group0, int64_t row0, int rows, const float* dyn, float* mb,
+                            void* stream) {
   RLKS_REQUIRE(d && b && mb && rows >= 0, RLKS_ERR_ARG, "rlks_ppo_gather: bad argument");
+  RLKS_REQUIRE(groups >= 1 && groups <= MAX_GROUPS && group0 >= 0 && b->N % groups == 0 && rows % groups == 0 &&
+                   row0 % groups == 0, RLKS_ERR_ARG,
+               "rlks_ppo_gather: groups must divide the lanes, the rows and row0 (at most 64 groups)");
   (void)dyn;  // advantages are standardised inside the loss kernel from dyn
-  const uint64_t S = (uint64_t)b->T * (uint64_t)b->N;
-  RLKS_REQUIRE(row0 >= 0 && (uint64_t)(row0 + rows) <= S, RLKS_ERR_ARG, "rlks_ppo_gather: rows out of range");
+  const int Ng = b->N / groups;
+  const uint64_t Sg = (uint64_t)b->T * (uint64_t)Ng;
+  RLKS_REQUIRE(row0 >= 0 && (uint64_t)(row0 + rows) / groups <= Sg, RLKS_ERR_ARG, "rlks_ppo_gather: rows out of range");
   if (rows == 0) return RLKS_OK;
   GatherArgs g{};
   g.b = *b;
-  g.perm = make_perm(perm_seed, epoch, S);
-  g.row0 = row0;
+  // group k's key: perm_seed for global group 0 (the single-group gather), else perm_seed offset by
+  // an odd 64-bit multiple of the global group id
+  for (int k = 0; k < groups; ++k)
+    g.perm[k] = make_perm(perm_seed + 0x632BE59BD9B4E019ull * (uint64_t)(group0 + k), epoch, Sg);
+  g.row0g = row0 / groups;
+  g.rows_g = rows / groups;
+  g.Ng = Ng;
   g.rows = rows;
   g.D = d->obs_dim;
   g.A = d->n_actions;

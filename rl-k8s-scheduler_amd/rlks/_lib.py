@@ -24,6 +24,7 @@ RLKS_PHASE_FWD, RLKS_PHASE_DW2, RLKS_PHASE_DH1, RLKS_PHASE_REDUCE, RLKS_PHASE_AL
 RLKS_PHASE_FWD_PI, RLKS_PHASE_FWD_VF, RLKS_PHASE_PREP = 16, 32, 64
 RLKS_PRECISION_FP32, RLKS_PRECISION_SF16, RLKS_PRECISION_WIDE = 0, 1, 2
 RLKS_STAT_POLICY_LOSS, RLKS_STAT_VF_LOSS, RLKS_STAT_KL, RLKS_STAT_ENTROPY, RLKS_STAT_ROWS = 0, 1, 2, 3, 4
+RLKS_EPLOG_CAP = 128
 
 
 class EnvCfg(C.Structure):
@@ -88,6 +89,10 @@ SIGNATURES = {
     "rlks_env_sample_step": [_P, _P, _I, _P, _P, _P, _P, _P, _P],
     "rlks_env_episode_stats": [_P, _P, _I, _P],
     "rlks_env_lane_state": [_P, _P, _P, _P],
+    "rlks_env_episode_log": [_P, _P, _P, _P, _I, _P],
+    "rlks_env_state_bytes": [_P, C.POINTER(_I64)],
+    "rlks_env_save_state": [_P, _P, _P],
+    "rlks_env_load_state": [_P, _P, _P],
     "rlks_philox4x32_10": [_P, _P, _P, _I, _P],
     "rlks_mt_random": [_P, _I, _P, _I, _P],
     "rlks_gae": [_P, _P, _P, _F, _F, _I, _I, _P, _P, _P, _P],
@@ -103,6 +108,8 @@ SIGNATURES = {
     "rlks_rollout_ws": [_P, C.POINTER(MlpDesc), _P, C.POINTER(RolloutBufs), _I, _P, _I64, _P],
     "rlks_minibatch_stride": [C.POINTER(MlpDesc)],
     "rlks_ppo_gather": [C.POINTER(MlpDesc), C.POINTER(RolloutBufs), C.c_uint64, _I, _I64, _I, _P, _P, _P],
+    "rlks_ppo_gather_grouped": [C.POINTER(MlpDesc), C.POINTER(RolloutBufs), C.c_uint64, _I, _I, _I, _I64, _I, _P,
+                                _P, _P],
     "rlks_ppo_workspace_bytes": [C.POINTER(MlpDesc), _I, C.POINTER(_I64)],
     "rlks_ppo_grad": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _P],
     "rlks_ppo_grad_phases": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _I, _P],

@@ -115,6 +115,19 @@ class NodeSpec:
         self.reject_penalty = float(reject_penalty)
         self.depart_prob = self.stationary_depart_prob() if depart_prob == "stationary" else float(depart_prob)
 
+    def to_dict(self) -> dict:
+        """JSON-able fields (checkpoints): from_dict(to_dict()) rebuilds the same spec"""
+        return {"n_clouds": self.n_clouds, "nodes_per_cluster": self.nodes_per_cluster,
+                "node_cpu_m": self.node_cpu_m.tolist(), "node_mem_mi": self.node_mem_mi.tolist(),
+                "pod_cpu_m": self.pod_cpu_m, "pod_mem_mi": self.pod_mem_mi, "arrival_rate": self.arrival_rate,
+                "arrival_trace": None if self.arrival_trace is None else self.arrival_trace.tolist(),
+                "depart_prob": self.depart_prob, "init_occupancy": self.init_occupancy,
+                "reject_penalty": self.reject_penalty}
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "NodeSpec":
+        return cls(**d)
+
     def max_pods(self):
         """pods a node of each cluster can hold"""
         return np.minimum(self.node_cpu_m // self.pod_cpu_m, self.node_mem_mi // self.pod_mem_mi)
@@ -169,6 +182,40 @@ class DeviceEnv:
     @property
     def stream(self):
         return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def state_bytes(self) -> int:
+        import ctypes as C
+
+        n = C.c_int64()
+        _lib.call("rlks_env_state_bytes", self.handle, C.byref(n))
+        return int(n.value)
+
+    def save_state(self):
+        """device uint8 snapshot of every per-lane state (rlks_env_save_state)"""
+        buf = self.torch.empty(self.state_bytes(), dtype=self.torch.uint8, device=self.device)
+        _lib.call("rlks_env_save_state", self.handle, _lib.ptr(buf), self.stream)
+        return buf
+
+    def load_state(self, buf):
+        buf = self.torch.as_tensor(buf).to(device=self.device, dtype=self.torch.uint8).contiguous()
+        if buf.numel() != self.state_bytes():
+            raise ValueError(f"env state snapshot has {buf.numel()} bytes, this env needs {self.state_bytes()}")
+        _lib.call("rlks_env_load_state", self.handle, _lib.ptr(buf), self.stream)
+
+    def episode_log(self, clear=True):
+        """(returns f64 [k], keys i64 [k], total count) of the episodes completed since the last
+        clear, k = min(total, RLKS_EPLOG_CAP), in completion order (sorted by episode, lane)"""
+        torch = self.torch
+        ret = torch.zeros(_lib.RLKS_EPLOG_CAP, dtype=torch.float64, device=self.device)
+        key = torch.zeros(_lib.RLKS_EPLOG_CAP, dtype=torch.int64, device=self.device)
+        cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
+        _lib.call("rlks_env_episode_log", self.handle, _lib.ptr(ret), _lib.ptr(key), _lib.ptr(cnt), int(clear),
+                  self.stream)
+        n = int(cnt.item()) & 0xFFFFFFFF
+        k = min(n, _lib.RLKS_EPLOG_CAP)
+        r, kk = ret[:k].cpu().numpy(), key[:k].cpu().numpy()
+        order = np.argsort(kk, kind="stable")
+        return r[order], kk[order], n
 
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:

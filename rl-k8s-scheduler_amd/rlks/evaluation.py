@@ -145,6 +145,35 @@ def evaluate(policy, num_episodes: int = 100, *, seed=None, table=None, device=N
         env.close()
 
 
+def evaluate_lanes(params, num_episodes: int, *, table=None, nodes=None, seed=0, device=None) -> np.ndarray:
+    """Greedy (explore=False) float64 returns of `num_episodes` episodes, one lane each, all lanes
+    in one batched env: RLlib's evaluation workers (train_final.py:19 .evaluation(
+    evaluation_interval=5, evaluation_duration=20), evaluation explore=False).  Table envs run the
+    reference-exact evaluate() above; node-level envs (configs c3 / c5) run Philox lanes keyed by
+    `seed` (episode e = lane e)."""
+    import torch
+
+    table = table if table is not None else load_table()
+    if nodes is None:
+        return evaluate(params, num_episodes, seed=seed, table=table, device=device).rewards
+    E = int(num_episodes)
+    env = VecK8sMultiCloudEnv(E, table=table, seed=int(seed), noise="philox", autoreset=False, device=device,
+                              nodes=nodes)
+    try:
+        obs = env.reset()
+        ret = torch.zeros(E, dtype=torch.float64, device=env.device)
+        logits = torch.empty(E, table.n_clouds, dtype=torch.float32, device=env.device)
+        values = torch.empty(E, dtype=torch.float32, device=env.device)
+        for _ in range(table.n_rows - 1):
+            params.forward(obs, logits, values)
+            obs, r, term, _, _ = env.step(torch.argmax(logits, dim=1).to(torch.int32))
+            ret += r
+        env.check_status()
+        return ret.cpu().numpy()
+    finally:
+        env.close()
+
+
 def round_robin_baseline(num_episodes: int = 5, **kw) -> np.ndarray:
     """train_and_compare.py:53-72: per-episode round-robin returns"""
     return evaluate("round_robin", num_episodes, **kw).rewards

@@ -22,6 +22,7 @@ Multi-GPU (torch.distributed, backend "nccl" = RCCL): each rank owns a contiguou
 """
 from __future__ import annotations
 
+import collections
 import copy
 import ctypes as C
 import json
@@ -67,6 +68,11 @@ class PPOConfig:
         self.explore = True
         self.evaluation_interval = None
         self.evaluation_duration = 10
+        self.metrics_num_episodes_for_smoothing = 100
+        self.checkpoint_env_state = True  # save() includes the lanes' env state (node state too)
+        # minibatches are drawn per block of lanes (rlks_ppo_gather_grouped): None = one block per
+        # rank.  A single-rank run with num_lane_groups = W trains exactly like W ranks.
+        self.num_lane_groups = None
         # rlks-specific knobs
         self.num_envs = None          # lanes per GPU (default: workers x envs per worker)
         self.noise = "philox"         # env utilisation noise: "philox" or "mt19937"
@@ -131,6 +137,11 @@ class PPOConfig:
             self.evaluation_duration = evaluation_duration
         return self
 
+    def reporting(self, metrics_num_episodes_for_smoothing=None, **kw):
+        if metrics_num_episodes_for_smoothing is not None:
+            self.metrics_num_episodes_for_smoothing = int(metrics_num_episodes_for_smoothing)
+        return self
+
     def debugging(self, seed=None, **kw):
         if seed is not None:
             self.seed = int(seed)
@@ -142,10 +153,29 @@ class PPOConfig:
         return self
 
     def to_dict(self):
+        """JSON-able config; the table is saved beside it by PPO.save (table.npz), the node spec
+        is inlined"""
         d = {k: v for k, v in self.__dict__.items() if k not in ("env", "table", "nodes")}
         d["env"] = getattr(self.env, "__name__", str(self.env)) if self.env is not None else None
         d["lambda"] = d.pop("lambda_")
+        d["nodes"] = self.nodes.to_dict() if self.nodes is not None else None
         return d
+
+    @classmethod
+    def from_dict(cls, d):
+        from .env import NodeSpec
+
+        c = cls()
+        for k, v in d.items():
+            if k == "lambda":
+                c.lambda_ = v
+            elif k == "adam_betas":
+                c.adam_betas = tuple(v)
+            elif k == "nodes":
+                c.nodes = NodeSpec.from_dict(v) if v is not None else None
+            elif k != "env" and hasattr(c, k):
+                setattr(c, k, v)
+        return c
 
     def copy(self):
         return copy.deepcopy(self)
@@ -195,12 +225,24 @@ class PPO:
         if cfg.rollout_fragment_length not in (None, "auto"):
             self.T = int(cfg.rollout_fragment_length)
         self.samples = self.T * self.N
+        if int(cfg.sgd_minibatch_size) % self.world:
+            raise ValueError(f"sgd_minibatch_size {cfg.sgd_minibatch_size} is not divisible by the {self.world} ranks")
         self.mb = int(cfg.sgd_minibatch_size) // self.world  # per-rank rows of a global minibatch
         if self.mb <= 0 or self.mb % 128:
             raise ValueError(f"sgd_minibatch_size per rank must be a positive multiple of 128, got {self.mb}")
+        # RLlib's torch learner (multi_gpu_train_one_step): num_batches = samples // minibatch per
+        # epoch; the train batch's remainder rows (4000 mod 256 = 160 at train_ppo.py:15-16) are
+        # not visited in that epoch.  Here every epoch draws a fresh permutation of all samples, so
+        # each epoch leaves out a different random remainder.
         self.n_mb = self.samples // self.mb
         if self.n_mb == 0:
             raise ValueError("train batch is smaller than one minibatch")
+        groups = int(cfg.num_lane_groups or self.world)
+        if groups % self.world or self.N % (groups // self.world) or self.mb % (groups // self.world):
+            raise ValueError(f"num_lane_groups {groups} must be a multiple of the {self.world} ranks and its per-rank "
+                             f"share must divide the {self.N} lanes and the {self.mb}-row minibatch")
+        self.groups = groups // self.world
+        self.group0 = self.rank * self.groups
         seed = cfg.seed if cfg.seed is not None else 0
         self.seed = seed
         with torch.cuda.device(self.device):
@@ -256,6 +298,12 @@ class PPO:
             self.ep_stats = torch.zeros(2, dtype=torch.float64, device=self.device)
             self.coeffs = _lib.PpoCoeffs(cfg.clip_param, cfg.vf_clip_param, cfg.vf_loss_coeff, cfg.entropy_coeff)
             _lib.call("rlks_env_reset", self.env.handle, None, _lib.ptr(b["obs"][0]), self.stream)
+            self.env.episode_log(clear=True)
+        # obs[0] holds the lanes' current observations only before the first rollout; afterwards
+        # they are obs[T] of the previous rollout (moved to obs[0] when the next one starts, so the
+        # update can still read obs[0..T-1])
+        self._carry = False
+        self._ep_history = collections.deque(maxlen=max(1, int(cfg.metrics_num_episodes_for_smoothing)))
         self.iteration = 0
         self.timesteps_total = 0
         self.episodes_total = 0
@@ -271,6 +319,9 @@ class PPO:
     def rollout(self, explore=True):
         s = self.stream
         b = self.buf
+        if self._carry:
+            b["obs"][0].copy_(b["obs"][self.T])
+        self._carry = True
         # sf16: one split-fp16 launch per step computes both nets (values included) and steps the
         # env; the split weights live in the SGD workspace
         _lib.call("rlks_rollout_ws", self.env.handle, C.byref(self.params.desc), _lib.ptr(self.params.flat),
@@ -288,11 +339,16 @@ class PPO:
         self._allreduce(self.adv_sums)
         _lib.call("rlks_adv_finalize", _lib.ptr(self.adv_sums), _lib.ptr(self.dyn), s)
 
+    def perm_seed(self, iteration=None):
+        """key of this iteration's minibatch permutations (resumes with the iteration counter)"""
+        it = self.iteration if iteration is None else iteration
+        return (self.seed * 1000003 + it) & (2**64 - 1)
+
     def sgd_step(self, epoch, b, stat_row):
         s = self.stream
         desc = C.byref(self.params.desc)
-        _lib.call("rlks_ppo_gather", desc, C.byref(self.bufs), (self.seed * 1000003 + self.iteration) & (2**64 - 1),
-                  epoch, b * self.mb, self.mb, _lib.ptr(self.dyn), _lib.ptr(self.mbuf), s)
+        _lib.call("rlks_ppo_gather_grouped", desc, C.byref(self.bufs), self.perm_seed(), epoch, self.groups,
+                  self.group0, b * self.mb, self.mb, _lib.ptr(self.dyn), _lib.ptr(self.mbuf), s)
         _lib.call("rlks_ppo_grad", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat), _lib.ptr(self.dyn),
                   _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row), _lib.ptr(self.ws),
                   self.ws.numel(), s)
@@ -327,6 +383,63 @@ class PPO:
         self.timesteps_total += self.samples * self.world
 
     # ------------------------------------------------------------------ RLlib surface
+    def _episode_returns(self):
+        """returns of the episodes completed this iteration in completion order (all ranks, at
+        most RLKS_EPLOG_CAP per rank) and their total count"""
+        torch = self.torch
+        r, k, n = self.env.episode_log(clear=True)
+        if self.world == 1:
+            return r, n
+        cap = _lib.RLKS_EPLOG_CAP
+        mine = torch.zeros(2 * cap + 1, dtype=torch.float64, device=self.device)
+        mine[: len(r)] = torch.from_numpy(r)
+        mine[cap: cap + len(k)] = torch.from_numpy(k.astype(np.float64))  # keys < 2^53
+        mine[2 * cap] = float(n)
+        allv = torch.zeros(self.world, 2 * cap + 1, dtype=torch.float64, device=self.device)
+        allv[self.rank] = mine
+        self._allreduce(allv)
+        a = allv.cpu().numpy()
+        rets, keys, total = [], [], 0
+        for q in range(self.world):
+            nq = int(a[q, 2 * cap])
+            kq = min(nq, cap)
+            rets.append(a[q, :kq])
+            keys.append(a[q, cap: cap + kq])
+            total += nq
+        rets, keys = np.concatenate(rets), np.concatenate(keys)
+        return rets[np.argsort(keys, kind="stable")], total
+
+    def _reward_mean(self, ep_sum, n_ep):
+        """RLlib episode_reward_mean: the mean over this iteration's episodes, topped up with the
+        most recent earlier ones to metrics_num_episodes_for_smoothing (Algorithm.
+        _compile_iteration_results; RLlib third-party, parity unpinned)"""
+        window = self._ep_history.maxlen
+        rets, total = self._episode_returns()
+        # >= window episodes: the mean of all of them, from the device sums.  Past RLKS_EPLOG_CAP the
+        # log holds the first-logged episodes only, so the history kept for a later iteration with
+        # fewer than `window` episodes is then approximate (such a later iteration needs lanes that
+        # finish far out of step; all lanes of one rank reset together).
+        if total >= window or total > len(rets):
+            self._ep_history.extend(rets[-window:])
+            return float(ep_sum / total) if total else float("nan")
+        missing = window - total
+        hist = list(self._ep_history)[-missing:] if missing > 0 else []
+        vals = hist + list(rets)
+        self._ep_history.extend(rets)
+        return float(np.mean(vals)) if vals else float("nan")
+
+    def evaluate(self, episodes=None):
+        """greedy evaluation (RLlib evaluation workers, explore=False): `episodes` episodes, one
+        lane each (train_final.py:19 .evaluation(evaluation_interval=5, evaluation_duration=20))"""
+        from .evaluation import evaluate_lanes
+
+        n = int(episodes or self.config.evaluation_duration)
+        rets = evaluate_lanes(self.params, n, table=self.table, nodes=self.config.nodes,
+                              seed=(self.seed * 7919 + self.iteration) & 0xFFFFFFFF, device=self.device)
+        return {"episode_reward_mean": float(np.mean(rets)), "episode_reward_min": float(np.min(rets)),
+                "episode_reward_max": float(np.max(rets)), "episodes_this_iter": n,
+                "episode_len_mean": float(self.table.n_rows - 1)}
+
     def train(self):
         t0 = time.time()
         kl_before = float(self.dyn[_lib.RLKS_DYN_KL_COEFF].item())
@@ -337,6 +450,7 @@ class PPO:
         rows = st[:, _lib.RLKS_STAT_ROWS]
         n_ep = int(round(ep[1]))
         self.episodes_total += n_ep
+        reward_mean = self._reward_mean(ep[0], n_ep)
         learner = {
             "policy_loss": float(np.mean(st[:, _lib.RLKS_STAT_POLICY_LOSS] / rows)),
             "vf_loss": float(np.mean(st[:, _lib.RLKS_STAT_VF_LOSS] / rows)),
@@ -345,16 +459,22 @@ class PPO:
             "cur_kl_coeff": kl_before,
             "cur_lr": float(self.config.lr),
         }
-        return {
-            "episode_reward_mean": float(ep[0] / n_ep) if n_ep else float("nan"),
+        result = {
+            "episode_reward_mean": reward_mean,
+            "episode_reward_mean_this_iter": float(ep[0] / n_ep) if n_ep else float("nan"),
             "episodes_this_iter": n_ep,
             "episodes_total": self.episodes_total,
             "training_iteration": self.iteration,
             "timesteps_total": self.timesteps_total,
             "num_env_steps_sampled": self.timesteps_total,
-            "time_this_iter_s": time.time() - t0,
             "info": {"learner": {"default_policy": {"learner_stats": learner}}},
         }
+        # RLlib Algorithm.step(): evaluate when (iteration) % evaluation_interval == 0, after training
+        iv = self.config.evaluation_interval
+        if iv and self.iteration % int(iv) == 0:
+            result["evaluation"] = self.evaluate()
+        result["time_this_iter_s"] = time.time() - t0
+        return result
 
     def compute_actions(self, obs, explore=None):
         """batched actions for obs [n, D] (device or host); returns an int32 device tensor"""
@@ -377,41 +497,72 @@ class PPO:
         p /= p.sum()
         return int(np.random.choice(len(p), p=p))
 
+    def current_obs(self):
+        """the lanes' current observations [N, D] (device)"""
+        return self.buf["obs"][self.T] if self._carry else self.buf["obs"][0]
+
     def get_state(self):
+        """everything a resumed run needs: weights, Adam moments and step, KL coefficient, counters,
+        the smoothing window, and (checkpoint_env_state) the lanes' env state and current obs.
+        The per-epoch gather permutation is keyed by (seed, iteration), so it resumes too."""
         torch = self.torch
         steps = torch.zeros(self.N, dtype=torch.int32, device=self.device)
         eps = torch.zeros(self.N, dtype=torch.int32, device=self.device)
         _lib.call("rlks_env_lane_state", self.env.handle, _lib.ptr(steps), _lib.ptr(eps), self.stream)
-        return {
+        st = {
             "weights": self.params.state_dict(),
             "adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(),
             "adam_step": self.adam_step, "kl_coeff": float(self.dyn[_lib.RLKS_DYN_KL_COEFF].item()),
             "iteration": self.iteration, "timesteps_total": self.timesteps_total,
             "episodes_total": self.episodes_total, "lane_steps": steps.cpu(), "lane_episodes": eps.cpu(),
+            "episode_history": [float(x) for x in self._ep_history],
+            "rank": self.rank, "world": self.world,
         }
+        if self.config.checkpoint_env_state:
+            st["env_state"] = self.env.save_state().cpu()
+            st["current_obs"] = self.current_obs().detach().cpu().clone()
+        return st
 
     def save(self, checkpoint_dir=None):
-        """RLlib Algorithm.save(): writes <dir>/checkpoint_<iter:06d>/ and returns its path"""
+        """RLlib Algorithm.save(): writes <dir>/checkpoint_<iter:06d>/ and returns its path.
+        Files: state.pt (tensors, weights_only-loadable), algorithm_state.json (config + scalars),
+        table.npz (the env table's float64 bits) and, with checkpoint_env_state, env_state.bin
+        (raw device snapshot, rlks_env_save_state; rank-suffixed when world > 1)."""
         import torch
 
         base = Path(checkpoint_dir) if checkpoint_dir else Path.home() / "rlks_results" / "PPO"
         path = base / f"checkpoint_{self.iteration:06d}"
         path.mkdir(parents=True, exist_ok=True)
         st = self.get_state()
+        sfx = f".rank{self.rank}" if self.world > 1 else ""
         tensors = {f"weights/{k}": v for k, v in st.pop("weights").items()}
         tensors.update({k: st.pop(k) for k in ("adam_m", "adam_v", "lane_steps", "lane_episodes")})
-        torch.save(tensors, path / "state.pt")
-        meta = {"state": st, "config": self.config.to_dict()}
-        (path / "algorithm_state.json").write_text(json.dumps(meta, indent=1, default=str))
+        if "current_obs" in st:
+            tensors["current_obs"] = st.pop("current_obs")
+        env_state = st.pop("env_state", None)
+        if env_state is not None:
+            env_state.numpy().tofile(path / f"env_state{sfx}.bin")
+            st["env_state_bytes"] = int(env_state.numel())
+        torch.save(tensors, path / f"state{sfx}.pt")
+        if self.rank == 0:
+            self.table.save(path / "table.npz")
+            meta = {"state": st, "config": self.config.to_dict()}
+            (path / "algorithm_state.json").write_text(json.dumps(meta, indent=1, default=str))
         return str(path)
 
     def restore(self, checkpoint_path):
         import torch
 
         path = Path(checkpoint_path)
-        tensors = torch.load(path / "state.pt", weights_only=True)
+        sfx = f".rank{self.rank}" if self.world > 1 else ""
+        tensors = torch.load(path / f"state{sfx}.pt", weights_only=True)
         meta = json.loads((path / "algorithm_state.json").read_text())["state"]
-        self.params.load_state_dict({k[len("weights/"):]: v for k, v in tensors.items() if k.startswith("weights/")})
+        sd = {k[len("weights/"):]: v for k, v in tensors.items() if k.startswith("weights/")}
+        w = self.params.state_dict()
+        for k, v in w.items():
+            if tuple(sd[k].shape) != tuple(v.shape):
+                raise ValueError(f"checkpoint tensor {k} has shape {tuple(sd[k].shape)}, this policy {tuple(v.shape)}")
+        self.params.load_state_dict(sd)
         self.adam_m.copy_(tensors["adam_m"].to(self.device))
         self.adam_v.copy_(tensors["adam_v"].to(self.device))
         self.adam_step = int(meta["adam_step"])
@@ -419,20 +570,24 @@ class PPO:
         self.iteration = int(meta["iteration"])
         self.timesteps_total = int(meta["timesteps_total"])
         self.episodes_total = int(meta["episodes_total"])
+        self._ep_history.clear()
+        self._ep_history.extend(meta.get("episode_history", []))
+        es = path / f"env_state{sfx}.bin"
+        if es.exists() and "current_obs" in tensors:
+            self.env.load_state(np.fromfile(es, dtype=np.uint8))
+            self.buf["obs"][0].copy_(tensors["current_obs"].to(self.device))
+            self._carry = False
+            self.env.episode_log(clear=True)
 
     @classmethod
     def from_checkpoint(cls, checkpoint_path, config: PPOConfig | None = None, **kw):
+        from .tables import Table
+
         path = Path(checkpoint_path)
         if config is None:
-            d = json.loads((path / "algorithm_state.json").read_text())["config"]
-            config = PPOConfig()
-            for k, v in d.items():
-                if k == "lambda":
-                    config.lambda_ = v
-                elif k == "adam_betas":
-                    config.adam_betas = tuple(v)
-                elif k != "env" and hasattr(config, k):
-                    setattr(config, k, v)
+            config = PPOConfig.from_dict(json.loads((path / "algorithm_state.json").read_text())["config"])
+            if (path / "table.npz").exists():
+                config.table = Table.load(path / "table.npz")
         algo = cls(config=config, **kw)
         algo.restore(path)
         return algo

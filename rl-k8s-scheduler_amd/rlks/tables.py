@@ -47,6 +47,17 @@ class Table:
 
         return pd.DataFrame(self.raw, columns=self.columns)
 
+    def save(self, path) -> None:
+        """npz of the exact float64 bits (checkpoints); load with Table.load (no pickle)"""
+        np.savez(path, cost=self.cost, latency=self.latency, raw=self.raw,
+                 columns=np.array([str(c) for c in self.columns]), source=np.array(self.source))
+
+    @classmethod
+    def load(cls, path) -> "Table":
+        z = np.load(path, allow_pickle=False)
+        return cls(np.ascontiguousarray(z["cost"]), np.ascontiguousarray(z["latency"]),
+                   [str(c) for c in z["columns"]], z["raw"], str(z["source"]))
+
 
 def _from_columns(raw: np.ndarray, columns: list, source: str, clouds=CLOUDS) -> Table:
     idx = {c: i for i, c in enumerate(columns)}

@@ -1,0 +1,45 @@
+"""One rank of tests/test_gpu_multirank.py (started as a fresh child process, never exec'd from a
+process that touched the GPU): torch.distributed over gloo, every rank on device 0, the real PPO
+class; writes its parameters and per-iteration results to <out>/rank<r>.npz."""
+import json
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "rl-k8s-scheduler_amd")]
+
+
+def main():
+    out = Path(sys.argv[1])
+    N, T, mb, epochs, iters = (int(x) for x in sys.argv[2:7])
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rlks.ppo import PPO, PPOConfig
+
+        cfg = (PPOConfig().environment("K8sMultiCloudEnv").framework("torch")
+               .training(train_batch_size=N * T * world, sgd_minibatch_size=mb, num_sgd_iter=epochs, lr=3e-4,
+                         gamma=0.99)
+               .debugging(seed=13))
+        cfg.num_envs = N
+        cfg.rollout_fragment_length = T
+        algo = PPO(config=cfg, device=torch.device("cuda", 0))
+        assert (algo.rank, algo.world, algo.groups, algo.group0) == (rank, world, 1, rank)
+        results = [algo.train() for _ in range(iters)]
+        keep = ("episode_reward_mean", "episodes_this_iter", "timesteps_total")
+        res = [{k: r[k] for k in keep} | {"kl": r["info"]["learner"]["default_policy"]["learner_stats"]["kl"]}
+               for r in results]
+        np.savez(out / f"rank{rank}.npz", params=algo.params.flat.cpu().numpy(),
+                 kl_coeff=np.float32(algo.dyn[2].item()), results=np.array(json.dumps(res)))
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+"""The data-parallel path with the real PPO class in two processes: two ranks as
+fresh child processes, gloo, both on device 0 (this box has one GPU; the 8-GPU RCCL run is the
+driver's).  Checked:
+  - both ranks end with bit-identical parameters (every rank applies the same all-reduced gradient);
+  - the two-rank run equals a single-rank run over all 2N lanes with num_lane_groups = 2 (the same
+    minibatches, rlks_ppo_gather_grouped): parameters within 1e-5 of their norm and 1e-3 of the
+    update's norm (fp32 summation order differs: per-rank partial sums + all-reduce vs one sum), KL
+    coefficient, episode counts and episode_reward_mean (the lanes' f64 returns are the same)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+HERE = Path(__file__).resolve().parent
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_equal_one_rank_with_two_lane_groups(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from rlks.ppo import PPO, PPOConfig
+
+    N, T, mb, epochs, iters, world = 512, 128, 4096, 2, 2, 2
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, str(HERE / "multirank_worker.py"), str(tmp_path), str(N),
+                                       str(T), str(mb), str(epochs), str(iters)], env=env))
+    try:
+        for p in procs:
+            assert p.wait(timeout=100) == 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    ranks = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    assert np.array_equal(ranks[0]["params"], ranks[1]["params"])
+    res = [json.loads(str(z["results"])) for z in ranks]
+    assert res[0] == res[1]
+    # single rank over all lanes, two lane groups
+    d = torch.device("cuda", 0)
+    cfg = (PPOConfig().environment("K8sMultiCloudEnv").framework("torch")
+           .training(train_batch_size=N * T * world, sgd_minibatch_size=mb, num_sgd_iter=epochs, lr=3e-4, gamma=0.99)
+           .debugging(seed=13))
+    cfg.num_envs = N * world
+    cfg.rollout_fragment_length = T
+    cfg.num_lane_groups = world
+    algo = PPO(config=cfg, device=d)
+    p0 = algo.params.flat.cpu().numpy().astype(np.float64)
+    single = [algo.train() for _ in range(iters)]
+    p1 = algo.params.flat.cpu().numpy().astype(np.float64)
+    p2 = ranks[0]["params"].astype(np.float64)
+    dn = np.linalg.norm(p2 - p1)
+    print(f"||p_2rank - p_1rank|| / ||p|| = {dn / np.linalg.norm(p1):.2e}, / ||update|| = "
+          f"{dn / np.linalg.norm(p1 - p0):.2e}")
+    assert dn <= 1e-5 * np.linalg.norm(p1)
+    assert dn <= 1e-3 * np.linalg.norm(p1 - p0)
+    assert float(ranks[0]["kl_coeff"]) == float(algo.dyn[2].item())
+    for a, b in zip(res[0], single):
+        assert a["episodes_this_iter"] == b["episodes_this_iter"] and a["timesteps_total"] == b["timesteps_total"]
+        assert a["episode_reward_mean"] == pytest.approx(b["episode_reward_mean"], rel=1e-12)
+        assert a["kl"] == pytest.approx(b["info"]["learner"]["default_policy"]["learner_stats"]["kl"], rel=1e-3)
