@@ -1,18 +1,19 @@
 #!/usr/bin/env python3
 """Throughput benchmark: env-steps/s of batched rollout + PPO policy update (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "c2"): per GPU 4,096 envs on the reference 2-cloud
-price/latency table, T = 128 rollout steps per iteration (524,288 env-steps), GAE, then 10 SGD
-epochs of 65,536-row minibatches (8 per epoch) of RLlib's default PPO (FCNet [256, 256] tanh,
-separate value net, Adam lr 3e-4, gamma 0.99).  A "step" is one full PPO iteration.  Synthetic
-data (the env itself generates it); random-init weights; fp32 throughout.
+Workload (default "c4" = BASELINE.json configs[3], the config the metric's 1/2/4/8-GPU curve is
+quoted on): per GPU 131,072 envs on the reference 2-cloud price/latency table (1,048,576 at 8
+GPUs), T = 128 rollout steps per iteration (16.8M env-steps per GPU), GAE, then 10 SGD epochs of
+65,536-row minibatches (256 per epoch) of RLlib's default PPO (FCNet [256, 256] tanh, separate
+value net, Adam lr 3e-4, gamma 0.99).  A "step" is one full PPO iteration.  Synthetic data (the
+env itself generates it); random-init weights; fp32-accurate arithmetic throughout.
 
   python bench.py --gpus N --steps K --warmup W [--config c2|c3|c4|c5]
-  (--config picks another BASELINE.json workload — c3: 65,536 node-level envs x 8 clusters x 256
-   nodes; c4: 131,072 envs/GPU, the 8-GPU 1,048,576-env shard; c5: 64 x 1,024 nodes with bursty
-   arrivals and the [2048, 2048] policy on the generic-width path; the default is c2)
+  (--config picks another BASELINE.json workload — c2: 4,096 envs/GPU (configs[1]); c3: 65,536
+   node-level envs x 8 clusters x 256 nodes; c5: 64 x 1,024 nodes with the Locust-fitted MMPP
+   arrivals and the [2048, 2048] policy on the generic-width path; the default is c4)
   (N > 1: launched by torch.distributed.run; one rank per GPU over RCCL; weak scaling —
-   every rank owns its own 4,096 lanes, the global minibatch is 65,536 x N rows)
+   every rank owns its own 131,072 lanes, the global minibatch is 65,536 x N rows)
 
 Prints ONE JSON line on rank 0.  Also measures, with HIP events on the launch stream, the average
 duration of each kernel of the SGD step (roofline of the dominant one), of the env step kernel and
@@ -106,7 +107,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS), help="BASELINE.json workload")
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS), help="BASELINE.json workload")
     ap.add_argument("--envs", type=int, default=None, help="lanes per GPU (default: the config's)")
     ap.add_argument("--rollout", type=int, default=128)
     ap.add_argument("--minibatch", type=int, default=None, help="rows per GPU per SGD step (default: the config's)")
@@ -192,7 +193,7 @@ def kernel_timing(algo, torch, config="c2", reps=20):
     out["rollout"] = {"ms": ms, "env_steps_per_s": T * N / (ms * 1e-3), "tflops": flops / (ms * 1e-3) / 1e12}
     if config == "c3":
         out["k_node_step_c3"] = node_env_timing(algo, torch, timed)
-    if config != "c2":
+    if config not in ("c2", "c4"):
         return out
     # the standalone env step kernel at a size where HBM, not launch latency, bounds it
     from rlks import VecK8sMultiCloudEnv
@@ -269,11 +270,18 @@ def node_env_timing(algo, torch, timed, n=65536, C=8, nodes=256, depart_prob="st
     read_nodes = 8.0 * C * nodes
     algo_bytes = read_nodes + 8 * written + 12 * C + 4 * C + 4 + 8 + 4 + 16 + 8 + 1 + 1 + 4
     gbs = algo_bytes * n / (ms * 1e-3) / 1e9
+    # SURVEY.md §8(d)'s per-env-step figure counts the chosen cluster's first-fit scan only
+    # (256 x 8 B + 8 B + 72 B obs + the 41 B of the table env = 2,169 B at C = 8, N = 256); this
+    # kernel also realises every other cluster's per-pod departures each step, so
+    # both rates are reported
+    survey_bytes = nodes * 8 + 8 + (12 * C - 24) + ENV_BYTES_PER_STEP
     res = {"kernel": "k_node_step", "depart_prob": spec.depart_prob, "ms": ms, "ms_validated": ms_checked, "envs": n, "clusters": C,
            "nodes": nodes, "env_steps_per_s": n / (ms * 1e-3), "env_steps_per_s_validated": n / (ms_checked * 1e-3),
            "node_checks_per_step": checks, "placed_per_step": placed, "rejected_per_step": rejected,
            "departed_per_step": departed, "nodes_written_per_step": written,
-           "bytes_per_step": algo_bytes, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
+           "bytes_per_step": algo_bytes, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
+           "survey_bytes_per_step": survey_bytes,
+           "frac_hbm_survey_bytes": survey_bytes * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     # HBM bytes per launch from the committed PMC passes (tools/pmc_node_traffic.py), for the cache
     # policy this churn selects (csrc/env.hip: streaming when depart_prob x max pods < 0.02)
     pmc = pmc_traffic()
@@ -284,6 +292,15 @@ def node_env_timing(algo, torch, timed, n=65536, C=8, nodes=256, depart_prob="st
         res["traffic_source"] = pmc[key]["source"]
     venv.close()
     return res
+
+
+def cpu_threads() -> int:
+    """host threads for the CPU baseline: the CPUs this process may run on (its affinity mask),
+    capped by OMP_NUM_THREADS when set.  The GPU box sets OMP_NUM_THREADS to its per-GPU CPU share
+    (16), while os.cpu_count() there reports the whole machine's CPUs, most of them not this job's."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() else max(1, n)
 
 
 def pmc_traffic():
@@ -383,7 +400,7 @@ def main():
             if dom == "wide_grad":
                 roofline["note"] = "generic-width path: the whole SGD-step gradient (a sequence of split-fp16 GEMM launches)"
             pmc = pmc_traffic()
-            if pmc and args.config == "c2" and dom in pmc:
+            if pmc and args.config in ("c2", "c4") and dom in pmc:
                 roofline["traffic"] = pmc[dom]["hbm_bytes_per_launch"]
                 roofline["traffic_source"] = pmc["source"]
         cpu = None
@@ -393,8 +410,7 @@ def main():
 
             cc = preset["cpu"]
             c = time_cpu_iteration(n_envs=cc["n_envs"], T=cc["T"], minibatch=cc["minibatch"], epochs=args.epochs,
-                                   threads=min(16, os.cpu_count() or 1), table=table, nodes=nodes, hidden=H,
-                                   label=args.config)
+                                   threads=cpu_threads(), table=table, nodes=nodes, hidden=H, label=args.config)
             cpu = {"value": c["value"], "unit": "env-steps/s", "cores": c["cores"], "kind": "port",
                    "sample": c["sample"]}
         result = {
