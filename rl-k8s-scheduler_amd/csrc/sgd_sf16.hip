@@ -22,8 +22,8 @@
 //     Z1 = Xa W1a^T, dZ1 = dH1 (1 - H1^2)
 //     dW1a^T = Xa^T dZ1        B = dZ1 accumulator; row D of dW1a is db1
 //   F2 (k_sf_dw2): dW2 = dZ2^T H1 over the rows, H1 recomputed (rows in registers) as the B
-//     operand, dZ2^T tiles staged through LDS pre-split with the global max|dZ2| scale; db2 from
-//     the same loads.  Row splits write fp32 partials, summed in a fixed order by k_reduce.
+//     operand, dZ2^T tiles staged through registers into LDS pre-split with the global max|dZ2|
+//     scale; db2 from the same loads.  Row splits write fp32 partials, summed in a fixed order by k_reduce.
 //
 // Reference semantics: RLlib FCNet [256, 256] tanh, vf_share_layers=False, PPO loss as in
 // mlp_fwd.hip (train_ppo.py:9-31; RLlib third-party).
@@ -35,6 +35,7 @@ namespace rlks {
 
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
+using v4u = __attribute__((ext_vector_type(4))) unsigned;  // 16-byte staging register (a vector, not HIP's uint4 struct, so it stays in VGPRs)
 
 constexpr int SF_ROWS = 256;        // minibatch rows must be a multiple of this
 constexpr int SF_CH = 8192;         // halves per staged chunk (per hi / lo array)
@@ -198,25 +199,43 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
 }
 
 // ----------------------------------------------------------------------------- F1
-// Weight chunks staged by LDS-DMA (global_load_lds_dwordx4: each lane's 16 bytes land at
-// base + 16 * lane, so the swizzle is applied on the global side).  Chunk c < 8: w2p columns
-// [32c, 32c+32) of all 256 rows (Z2 loop); c >= 8: w2t rows [32(c-8), +32) (dH1 loop).  A chunk
-// is 2 x 1024 slots of 16 B (hi, lo) = 32 blocks of 64; wave w of W issues blocks (32/W) w + i.
+// Weight chunks staged through registers: a wave loads its share of chunk c + 1 at the start of
+// a step (global_load_dwordx4 into 32 / W x 16 B per lane) and writes it to the idle LDS buffer at
+// the end.  (LDS-DMA, global_load_lds, would save the registers, but while one is in flight the
+// compiler waits for every outstanding LDS read, lgkmcnt(0), before any LDS result is used, which
+// serialises the fragment pipeline below.)  Chunk c < 8: w2p columns [32c, 32c+32) of all 256
+// rows (Z2 loop, k-tile c); c >= 8: w2t columns [32(c-8), +32) of all 256 rows (dH1 loop, n-tile
+// c - 8).  Both are [256 rows][32 halves] images with 16-byte pieces XOR-swizzled by
+// (row >> 2) & 3, read by sf_frag.  A chunk is 2 x 1024 slots of 16 B (hi, lo) = 32 blocks of 64;
+// wave w of W moves blocks (32/W) w + i.
 template <int W>
-__device__ __forceinline__ void chunk_dma(const SfNet& N, _Float16* buf, int c, int w, int l) {
+__device__ __forceinline__ void chunk_load(const SfNet& N, int c, int w, int l, v4u (&v)[32 / W]) {
+  const bool p = c < 8;
+  const int col = 32 * (p ? c : c - 8);
 #pragma unroll
   for (int i = 0; i < 32 / W; ++i) {
     const int blk = (32 / W) * w + i, arr = blk >> 4, sig = (blk & 15) * 64 + l;
-    const _Float16* src;
-    if (c < 8) {
-      const int n = sig >> 2, pc = (sig & 3) ^ ((n >> 2) & 3);
-      src = (arr ? N.w2pl : N.w2ph) + n * HID + 32 * c + 8 * pc;
-    } else {
-      const int k = sig >> 5, pc = (sig & 31) ^ (k & 15);
-      src = (arr ? N.w2tl : N.w2th) + (32 * (c - 8) + k) * HID + 8 * pc;
-    }
-    _Float16* dst = buf + arr * SF_CH + (blk & 15) * 64 * 8;
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    const int row = sig >> 2, pc = (sig & 3) ^ ((row >> 2) & 3);
+    const _Float16* src = (p ? (arr ? N.w2pl : N.w2ph) : (arr ? N.w2tl : N.w2th)) + row * HID + col + 8 * pc;
+    v[i] = *reinterpret_cast<const v4u*>(src);
+  }
+}
+template <int W>
+__device__ __forceinline__ void chunk_store(_Float16* buf, int w, int l, const v4u (&v)[32 / W]) {
+#pragma unroll
+  for (int i = 0; i < 32 / W; ++i) {
+    const int blk = (32 / W) * w + i, arr = blk >> 4;
+    *reinterpret_cast<v4u*>(buf + arr * SF_CH + ((blk & 15) * 64 + l) * 8) = v[i];
+  }
+}
+// the (hi, lo) fragments of one 32-row block of a chunk for both k-steps s: lane (r, h) of row
+// `row` gets halves [16 s + 8 h, +8) of its 32
+__device__ __forceinline__ void sf_frag(const _Float16* buf, int row, int h, h8 (&f)[2][2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int off = row * 32 + 8 * ((2 * s + h) ^ ((row >> 2) & 3));
+    f[s][0] = *reinterpret_cast<const h8*>(buf + off);
+    f[s][1] = *reinterpret_cast<const h8*>(buf + SF_CH + off);
   }
 }
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -238,8 +257,8 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
   constexpr int NTHR = 64 * W;
   constexpr int KS = KD / 16;   // k-steps of the first layer
   // NG: accumulator row groups (8 rows each) holding the rows d <= D of dW1a^T.  Each k-tile's
-  // dW1a^T block goes to an LDS slot (double-buffered over k-tiles) and is summed over the W waves
-  // two k-tiles later, so no accumulator outlives its k-tile (registers stay below 512 for A = 8).
+  // dW1a^T block goes to an LDS slot (the epilogue reuses the chunk buffers) and is summed over the
+  // W waves there, so no accumulator outlives its k-tile.
   constexpr int DWR = 8 * NG;   // LDS rows per dW1a^T column
   const SfNet& N = g.n[NET];
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -248,14 +267,17 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
   float* sW3 = sB2 + HID;                            // [A_][HID]
   _Float16* sW1 = reinterpret_cast<_Float16*>(sW3 + A_ * HID);  // [2 hi/lo][HID k][KD] (swizzled)
   h8* sXT = reinterpret_cast<h8*>(sW1 + 2 * HID * KD);          // [W][2 s][2 hi/lo][64 lanes]
-  float* sDW = reinterpret_cast<float*>(sXT + W * 4 * 64);   // [2][W][32 k][DWR d]
 
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int D = g.D, stride = g.x_stride;
   const int tile = blockIdx.x * W + w, row0 = tile * 32;
   SF_STAMP(0);
 
-  chunk_dma<W>(N, sCh, 0, w, l);
+  {
+    v4u cv[32 / W];
+    chunk_load<W>(N, 0, w, l, cv);
+    chunk_store<W>(sCh, w, l, cv);
+  }
   for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i];
   for (int i = tid; i < A_ * HID; i += NTHR) sW3[i] = N.w3[i];
 
@@ -326,33 +348,53 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
   h1t_tile(0, bh, bl);
   for (int c = 0; c < 8; ++c) {
     const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
-    chunk_dma<W>(N, sCh + ((c + 1) & 1) * 2 * SF_CH, c + 1, w, l);
-    h8 fa[8][2][2];
+    v4u cv[32 / W];
+    chunk_load<W>(N, c + 1, w, l, cv);
+    // n-tile steps fenced by sched_barrier: step nt issues the LDS reads of n-tile nt + 1's W2
+    // fragments, then n-tile nt's six MFMAs, so every read has a whole step (192 MFMA cycles) to
+    // land and only two fragment sets are live (the register budget goes to the accumulators).
+    // The next k-tile's H1^T (kn = c + 1; the last is discarded) is computed in the MFMA shadows.
+    const int kn = c + 1 < 8 ? c + 1 : 7;
+    h8 fc[2][2], fn[2][2], nbh[2], nbl[2];
+    f32x16 z;
+    sf_frag(buf, r, h, fc);
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
-      const int n = 32 * nt + r;
+      if (nt < 7) sf_frag(buf, 32 * (nt + 1) + r, h, fn);
+      if (nt == 0) w1_frag(kn);
+#ifndef RLKS_Z2_NOFENCE
+      __builtin_amdgcn_sched_barrier(0);  // the reads issue before this step's MFMAs
+#endif
+      if (nt == 1) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) z = mma3(wh[ks], wl[ks], xh[ks], xl[ks], z);
+      }
+      if (nt >= 2 && nt < 6) {
+#pragma unroll
+        for (int q = 4 * (nt - 2); q < 4 * (nt - 1); ++q) z[q] = tanh_abs(z[q] * inv_z1);
+      }
+      if (nt == 6) {
+        split16(z, 0, SF_H1_SCALE, nbh[0], nbl[0]);
+        split16(z, 8, SF_H1_SCALE, nbh[1], nbl[1]);
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int off = n * 32 + 8 * ((2 * s + h) ^ ((n >> 2) & 3));
-        fa[nt][s][0] = *reinterpret_cast<const h8*>(buf + off);
-        fa[nt][s][1] = *reinterpret_cast<const h8*>(buf + SF_CH + off);
+        acc[nt] = mma(fc[s][1], bh[s], acc[nt]);
+        acc[nt] = mma(fc[s][0], bl[s], acc[nt]);
+        acc[nt] = mma(fc[s][0], bh[s], acc[nt]);
       }
-    }
-    h8 nbh[2], nbl[2];
-    h1t_tile(c + 1 < 8 ? c + 1 : 7, nbh, nbl);  // next tile's H1 (branch-free: the last is discarded)
-    // consecutive MFMAs on independent accumulators
+#ifndef RLKS_Z2_NOFENCE
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      if (nt < 7)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int nt = 0; nt < 8; ++nt) acc[nt] = mma(fa[nt][s][1], bh[s], acc[nt]);
-#pragma unroll
-      for (int nt = 0; nt < 8; ++nt) acc[nt] = mma(fa[nt][s][0], bl[s], acc[nt]);
-#pragma unroll
-      for (int nt = 0; nt < 8; ++nt) acc[nt] = mma(fa[nt][s][0], bh[s], acc[nt]);
+        for (int s = 0; s < 2; ++s) { fc[s][0] = fn[s][0]; fc[s][1] = fn[s][1]; }
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) { bh[s] = nbh[s]; bl[s] = nbl[s]; }
-    vm_drain();
+    chunk_store<W>(sCh + ((c + 1) & 1) * 2 * SF_CH, w, l, cv);
     __syncthreads();
   }
 
@@ -516,15 +558,7 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
   dmx = wave_max(dmx);
   if (l == 0) atomicMax(N.dzmax, __float_as_uint(dmx));
   const int edz = sf_exp(dmx);
-  h8 dzh[8][2], dzl[8][2];
-  {
-    const float sdz = pow2(edz);
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-      split16(acc[nt], 0, sdz, dzh[nt][0], dzl[nt][0]);
-      split16(acc[nt], 8, sdz, dzh[nt][1], dzl[nt][1]);
-    }
-  }
+  const float sdz = pow2(edz);
   {
     h8 a, b;
     split8(xtv, 0, sx, a, b);
@@ -535,23 +569,63 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
     sXT[(w * 4 + 3) * 64 + l] = b;
   }
   SF_STAMP(5);
-  // ---- dH1 = dZ2 W2 per 32-column k-tile; dZ1 = dH1 (1 - H1^2); dW1a^T = Xa^T dZ1
-  // dZ1 enters the split at 2^(e_dz + e_w2 - 23): |dH1 2^(e_dz + e_w2)| <= 256 2^15 2^15
+  // ---- dH1 = dZ2 W2, n-tile outer: chunk 8 + nt holds W2's n-tile nt (w2t columns) for every
+  // k-tile, the n-tile's dZ2^T accumulator is split into the A fragments just before its MFMAs,
+  // and all eight dH1 k-tile accumulators stay live (AGPRs) until the last n-tile.  Fragment
+  // reads run one k-tile step ahead of the MFMAs (sched_barrier fences), so only two fragment sets
+  // and one n-tile's dZ2 split are live instead of the whole split dZ2^T.
+  f32x16 dh[8];
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dh[kt][q] = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt) {
+    const int c = 8 + nt;
+    const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
+    v4u cv[32 / W];
+    if (nt < 7) chunk_load<W>(N, c + 1, w, l, cv);
+    h8 ah[2], al[2], fc[2][2], fn[2][2];
+    split16(acc[nt], 0, sdz, ah[0], al[0]);
+    split16(acc[nt], 8, sdz, ah[1], al[1]);
+    sf_frag(buf, r, h, fc);
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      if (kt < 7) sf_frag(buf, 32 * (kt + 1) + r, h, fn);
+      __builtin_amdgcn_sched_barrier(0);  // the reads issue before this step's MFMAs
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        dh[kt] = mma(al[s], fc[s][0], dh[kt]);
+        dh[kt] = mma(ah[s], fc[s][1], dh[kt]);
+        dh[kt] = mma(ah[s], fc[s][0], dh[kt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt < 7)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) { fc[s][0] = fn[s][0]; fc[s][1] = fn[s][1]; }
+    }
+    if (nt < 7) chunk_store<W>(sCh + ((c + 1) & 1) * 2 * SF_CH, w, l, cv);
+    __syncthreads();
+  }
+  SF_STAMP(6);
+  // ---- dZ1 = dH1 (1 - H1^2) -> dW1a^T = Xa^T dZ1 per k-tile; dZ1 enters the split at
+  // 2^(e_dz + e_w2 - 23): |dH1 2^(e_dz + e_w2)| <= 256 2^15 2^15.  Each wave's dW1a^T blocks go to
+  // LDS slots in the (now idle) chunk buffers, KPR k-tiles per round, and the workgroup sums them
+  // over the W waves in a fixed order after one barrier per round.
+  constexpr int SLOT = W * 32 * DWR;                       // floats per k-tile
+  constexpr int KPR = (2 * SF_CH) / SLOT >= 8 ? 8 : (2 * SF_CH) / SLOT;  // 64 KB of chunk buffers
+  static_assert(KPR >= 1 && 8 % KPR == 0, "dW1 epilogue slots");
+  float* sEp = reinterpret_cast<float*>(sCh);
   const int blk = blockIdx.x;
-  auto dw1_flush = [&](int kt) {  // elements (k = 32 kt + e / (D+1), d = e mod (D+1)), fixed wave order
+  auto dw1_flush = [&](int kt0) {  // k-tiles kt0 .. kt0 + KPR - 1: (k, d) elements, fixed wave order
     const int nd = D + 1;
-    auto one = [&](int e) {
-      const int kk = e / nd, d = e - kk * nd, k = 32 * kt + kk;
+    for (int e = tid; e < KPR * 32 * nd; e += NTHR) {
+      const int j = e / (32 * nd), e2 = e - j * 32 * nd, kk = e2 / nd, d = e2 - kk * nd, k = 32 * (kt0 + j) + kk;
       float s = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < W; ++ww) s += sDW[(((kt & 1) * W + ww) * 32 + kk) * DWR + d];
+      for (int ww = 0; ww < W; ++ww) s += sEp[j * SLOT + (ww * 32 + kk) * DWR + d];
       if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
       else N.part_b1[(size_t)blk * HID + k] = s;
-    };
-    if constexpr (32 * DWR <= NTHR) {  // one element per thread at most
-      if (tid < 32 * nd) one(tid);
-    } else {
-      for (int e = tid; e < 32 * nd; e += NTHR) one(e);
     }
   };
   const float sz1 = pow2(-23);
@@ -570,12 +644,11 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
       der[q] = 1.f - h1 * h1;
     }
   };
-  // dZ1 = dH1 (1 - H1^2) -> split -> dW1a^T = Xa^T dZ1 of k-tile kt (issued one iteration late so
-  // that it overlaps the next tile's MFMAs)
-  auto dw1_tile = [&](int kt, const f32x16& dh, const f32x16& der) {
+  // dZ1 -> split -> dW1a^T of k-tile kt into this wave's part of slot kt mod KPR
+  auto dw1_tile = [&](int kt, const f32x16& dhk, const f32x16& der) {
     f32x16 dz;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) dz[q] = dh[q] * der[q];
+    for (int q = 0; q < 16; ++q) dz[q] = dhk[q] * der[q];
     h8 zh[2], zl[2];
     split16(dz, 0, sz1, zh[0], zl[0]);
     split16(dz, 8, sz1, zh[1], zl[1]);
@@ -592,68 +665,28 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
     wacc2 = mma(x1h, zh[1], wacc2);
 #pragma unroll
     for (int q = 0; q < 16; ++q) wacc[q] += wacc2[q];
-    // rows d = 8g + 4h + 0..3 of column k: 16-byte stores into this wave's slot of k-tile kt
+    // rows d = 8g + 4h + 0..3 of column k: 16-byte stores
 #pragma unroll
     for (int gq = 0; gq < NG; ++gq) {
       float4 v = {wacc[4 * gq] * u1, wacc[4 * gq + 1] * u1, wacc[4 * gq + 2] * u1, wacc[4 * gq + 3] * u1};
-      *reinterpret_cast<float4*>(sDW + (((kt & 1) * W + w) * 32 + r) * DWR + 8 * gq + 4 * h) = v;
+      *reinterpret_cast<float4*>(sEp + (kt % KPR) * SLOT + (w * 32 + r) * DWR + 8 * gq + 4 * h) = v;
     }
   };
-  f32x16 der, dprev, derprev;
+  // software-pipelined: the next k-tile's derivative (MFMAs + tanh) overlaps this one's dW1a
+  f32x16 der;
   h1_der(0, der);
 #pragma unroll
-  for (int q = 0; q < 16; ++q) { dprev[q] = 0.f; derprev[q] = 0.f; }
-  for (int c = 8; c < 16; ++c) {
-    const int kt = c - 8;
-    const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
-    // branch-free body: at c = 15 chunk 15 is re-fetched into the idle buffer
-    chunk_dma<W>(N, sCh + ((c + 1) & 1) * 2 * SF_CH, c + 1 < 16 ? c + 1 : 15, w, l);
-    h8 fb[8][2][2];
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int off = r * HID + 8 * ((4 * nt + 2 * s + h) ^ (r & 15));
-        fb[nt][s][0] = *reinterpret_cast<const h8*>(buf + off);
-        fb[nt][s][1] = *reinterpret_cast<const h8*>(buf + SF_CH + off);
-      }
-    // four independent accumulation chains (n-tile mod 4), MFMAs interleaved across them
-    f32x16 dc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) dc[i][q] = 0.f;
-#pragma unroll
-    for (int g2 = 0; g2 < 2; ++g2)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dc[i] = mma(dzl[4 * g2 + i][s], fb[4 * g2 + i][s][0], dc[i]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dc[i] = mma(dzh[4 * g2 + i][s], fb[4 * g2 + i][s][1], dc[i]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dc[i] = mma(dzh[4 * g2 + i][s], fb[4 * g2 + i][s][0], dc[i]);
-      }
+  for (int kt = 0; kt < 8; ++kt) {
     f32x16 nder;
-    h1_der(kt + 1 < 8 ? kt + 1 : 7, nder);
-    // tail of k-tile kt - 1; at kt = 0 it runs on zeros into slot 1, rewritten before its flush
-    dw1_tile((kt + 7) & 7, dprev, derprev);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      dprev[q] = (dc[0][q] + dc[1][q]) + (dc[2][q] + dc[3][q]);
-      derprev[q] = der[q];
-      der[q] = nder[q];
+    if (kt < 7) h1_der(kt + 1, nder);
+    dw1_tile(kt, dh[kt], der);
+    if (kt % KPR == KPR - 1) {
+      __syncthreads();
+      dw1_flush(kt + 1 - KPR);
+      if (kt < 7) __syncthreads();  // slots free for the next round
     }
-    if (kt > 1) dw1_flush(kt - 2);
-    vm_drain();
-    __syncthreads();
+    if (kt < 7) der = nder;
   }
-  dw1_tile(7, dprev, derprev);
-  dw1_flush(6);
-  __syncthreads();
-  SF_STAMP(6);
-  // ---- workgroup epilogue: the last k-tile's fixed-order sum over the W waves
-  dw1_flush(7);
   SF_STAMP(7);
 }
 
@@ -674,8 +707,6 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   const SfNet& N = g.n[net];
   extern __shared__ __attribute__((aligned(16))) float lds[];
   _Float16* sA = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][HID n][32 m perm]
-  // fp32 dZ2^T tiles landed by LDS-DMA: [2 slots][2048 float4] (float4 f = tid + 512 i of a tile)
-  float4* sStage = reinterpret_cast<float4*>(sA + 2 * 2 * SF_CH);
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int D = g.D, stride = g.x_stride;
   const int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
@@ -694,30 +725,29 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   }
 
   float db2[4] = {0.f, 0.f, 0.f, 0.f};
-  // tile t's 32 KB into stage slot (t - t0) & 1: each lane's 16 bytes land at the wave's base +
-  // 16 lane, i.e. at float4 index tid + 512 i (no register round trip, no compiler-inserted wait)
+  // dZ2^T tile t (32 KB) staged through registers: thread tid loads float4 f = tid + 512 i
+  // (row n = f >> 3, rows m 4 (f & 7) .. +3) one tile ahead, and splits it into an MFMA buffer at
+  // the end of the step.  (LDS-DMA would make the compiler wait for every outstanding LDS read,
+  // lgkmcnt(0), before each fragment's use while a DMA is in flight.)
+  using v4f = __attribute__((ext_vector_type(4))) float;
+  v4f dv[4];
   auto load = [&](int t) {
-    float4* dst = sStage + ((t - t0) & 1) * 2048;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds(N.dz2t + (size_t)t * HID * 32 + (size_t)(tid + 512 * i) * 4,
-                                       (__attribute__((address_space(3))) void*)(dst + 512 * i + 64 * w), 16, 0, 0);
+      dv[i] = *reinterpret_cast<const v4f*>(N.dz2t + (size_t)t * HID * 32 + (size_t)(tid + 512 * i) * 4);
   };
-  // split tile t (stage slot) into the MFMA buffer `buf`
-  auto store = [&](int t, int buf) {
+  auto store = [&](int buf) {
     _Float16* b = sA + buf * 2 * SF_CH;
-    const float4* src = sStage + ((t - t0) & 1) * 2048;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = tid + 512 * i, n = f >> 3, c = f & 7;
-      const float4 v = src[f];
-      db2[i] += (v.x + v.y) + (v.z + v.w);
-      const float vv[4] = {v.x, v.y, v.z, v.w};
+      const v4f v = dv[i];
+      db2[i] += (v[0] + v[1]) + (v[2] + v[3]);
       h4 hi, lo;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         _Float16 a, bb;
-        split1(vv[j] * sg, a, bb);
+        split1(v[j] * sg, a, bb);
         hi[j] = a;
         lo[j] = bb;
       }
@@ -734,13 +764,7 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
 
-  load(t0);
-  if (t0 + 1 < t1) load(t0 + 1);
-  vm_drain();
-  __syncthreads();
-  store(t0, 0);
-  __syncthreads();
-  // X rows of the next tile are loaded one iteration ahead (their latency hides behind the MFMAs)
+  // X rows of the next tile are loaded one step ahead (their latency hides behind the MFMAs)
   float xnext[KS * 8];
   auto load_x = [&](int t) {
     const float* xr = g.x + (size_t)(t * 32 + r) * stride;
@@ -752,39 +776,50 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
         xnext[ks * 8 + j] = d < D ? xr[d] : (d == D ? 1.f : 0.f);
       }
   };
+  // H1 tile (rows m in registers, columns k = 32w + r on lanes) of the X rows in xnext, as the B
+  // operand; then xnext <- the rows of tile tn
+  auto h1 = [&](int tn, h8 (&bh)[2], h8 (&bl)[2]) {
+    float xv[KS * 8];
+#pragma unroll
+    for (int i = 0; i < KS * 8; ++i) xv[i] = xnext[i];
+    load_x(tn);
+    float xm = 0.f;
+#pragma unroll
+    for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
+    const float sx = pow2(sf_exp(wave_max(xm)));
+    f32x16 z;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      h8 a, b;
+      split8(xv, ks * 8, sx, a, b);
+      z = mma3(a, b, wh[ks], wl[ks], z);
+    }
+    const float inv_z1 = inv_w1 / sx;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
+    split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
+    split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
+  };
+
+  // Software pipeline: step t runs tile t's 48 MFMAs and, in their shadow, splits tile t + 1's
+  // dZ2^T (loaded during step t - 1) into the other LDS buffer, loads tile t + 2's and computes
+  // tile t + 1's H1.  The VALU work of a step thus overlaps the same wave's MFMAs instead of
+  // following them: both waves of a SIMD meet at every barrier, so they cannot hide each
+  // other's VALU phases.
+  h8 bh[2], bl[2];
+  load(t0);
+  store(0);
+  if (t0 + 1 < t1) load(t0 + 1);
   load_x(t0);
+  h1(t0 + 1 < t1 ? t0 + 1 : t0, bh, bl);
+  __syncthreads();
   for (int t = t0; t < t1; ++t) {
     const int buf = (t - t0) & 1;
-    // tile t + 2 into the stage slot tile t left (split into `buf` before the last barrier); it
-    // lands while this tile's MFMAs run
-    if (t + 2 < t1) load(t + 2);
-    // H1 tile (rows m in registers, columns k = 32w + r on lanes) as the B operand
-    h8 bh[2], bl[2];
-    {
-      float xv[KS * 8];
-#pragma unroll
-      for (int i = 0; i < KS * 8; ++i) xv[i] = xnext[i];
-      load_x(t + 1 < t1 ? t + 1 : t);
-      float xm = 0.f;
-#pragma unroll
-      for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
-      const float sx = pow2(sf_exp(wave_max(xm)));
-      f32x16 z;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) z[q] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        h8 a, b;
-        split8(xv, ks * 8, sx, a, b);
-        z = mma3(a, b, wh[ks], wl[ks], z);
-      }
-      const float inv_z1 = inv_w1 / sx;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
-      split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
-      split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
-    }
+    const bool more = t + 1 < t1;
     const _Float16* b = sA + buf * 2 * SF_CH;
+    h8 nbh[2], nbl[2];
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
       const int n = 32 * nt + r;
@@ -795,10 +830,12 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
         const h8 al = *reinterpret_cast<const h8*>(b + SF_CH + off);
         acc[nt] = mma3(ah, al, bh[s], bl[s], acc[nt]);
       }
+      if (nt == 1 && more) store(buf ^ 1);                     // tile t + 1 -> other buffer
+      if (nt == 3 && t + 2 < t1) load(t + 2);                   // tile t + 2 -> registers
+      if (nt == 4) h1(t + 2 < t1 ? t + 2 : t + 1 < t1 ? t + 1 : t, nbh, nbl);  // tile t + 1's H1
     }
-    // tile t + 1 (landed during the previous iteration) split into the other MFMA buffer
-    if (t + 1 < t1) store(t + 1, buf ^ 1);
-    vm_drain();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) { bh[s] = nbh[s]; bl[s] = nbl[s]; }
     __syncthreads();
   }
   float* out = N.part_w2 + (size_t)blockIdx.x * HID * HID;
@@ -826,8 +863,7 @@ extern "C" int rlks_dbg_sf_stamps(unsigned long long* host) {
 
 size_t sf_f1_lds_bytes(int A_, int NG, int KD, int W) {
   return (size_t)2 * 2 * SF_CH * sizeof(_Float16) + (size_t)(HID + A_ * HID) * sizeof(float) +
-         (size_t)2 * HID * KD * sizeof(_Float16) + (size_t)W * 4 * 64 * 16 +
-         (size_t)2 * W * 32 * 8 * NG * sizeof(float);
+         (size_t)2 * HID * KD * sizeof(_Float16) + (size_t)W * 4 * 64 * 16;
 }
 
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
@@ -863,7 +899,7 @@ int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s) {
 }
 
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {
-  const size_t lds = (size_t)2 * 2 * SF_CH * sizeof(_Float16) + (size_t)2 * 2048 * 16;  // + fp32 stage
+  const size_t lds = (size_t)2 * 2 * SF_CH * sizeof(_Float16);
   if (sf_kd(a.D) == 16) hipLaunchKernelGGL(k_sf_dw2<16>, dim3(splits, 2), dim3(512), lds, s, a);
   else hipLaunchKernelGGL(k_sf_dw2<32>, dim3(splits, 2), dim3(512), lds, s, a);
   RLKS_LAUNCHED();
