@@ -54,6 +54,9 @@ def flops_per_row(name, D=6, H=256, A=2):
         "k_dh1": 2 * 2 * H * H + 2 * 2 * D * H,     # dH1 = dZ2 W2 and dW1 = dZ1^T X, both nets
         # split-fp16 F1 (sgd_sf16.hip): forward + head backward + dH1 = dZ2 W2 + dW1 = dZ1^T X, both nets
         "k_sf_fwdbwd": sum(fwd(An) + head(An) + 2 * H * H + 2 * D * H for An in (A, 1)),
+        # the same F1 as two kernels: forward + head backward (F1a), dH1 = dZ2 W2 + dW1 = dZ1^T X (F1b)
+        "k_sf_fwd": sum(fwd(An) + head(An) for An in (A, 1)),
+        "k_sf_bwd": 2 * (2 * H * H + 2 * D * H),
         "k_sf_dw2": 2 * 2 * H * H,                  # dW2 = dZ2^T H1, both nets
         # generic-width path (wide_mlp.hip): the whole gradient (forward, head, dW2, dH1, dW1), both nets
         "wide_grad": sum(fwd(An) + head(An) + 4 * H * H + 2 * D * H for An in (A, 1)),
@@ -97,7 +100,8 @@ def env_setup(name):
                          init_occupancy=0.5)
 
 
-ROOFLINE_KERNELS = ("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1", "k_sf_fwdbwd", "k_sf_dw2", "wide_grad")
+ROOFLINE_KERNELS = ("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1", "k_sf_fwdbwd", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2",
+                    "wide_grad")
 ENV_BYTES_PER_STEP = 4 + 8 + 24 + 4 + 1  # action, step r/w, obs, reward, done
 GAE_BYTES_PER_STEP = 17                  # r, V, done in; A, vtarg out
 
@@ -150,8 +154,12 @@ def kernel_timing(algo, torch, config="c2", reps=20):
         peak, peak_name = SF16_PEAK_TFLOPS, "frac_sf16_mfma"
     elif algo.precision == "sf16":
         phase(_lib.RLKS_PHASE_ALL)()  # weight splits + dZ2 in place for the per-phase timings
-        phases = (("k_sf_prep", _lib.RLKS_PHASE_PREP),
-                  ("k_sf_fwdbwd", _lib.RLKS_PHASE_FWD_PI | _lib.RLKS_PHASE_FWD_VF),
+        if _lib.lib().rlks_sf_f1_split():  # F1 as k_sf_fwd + k_sf_bwd: each timed alone, and the pair
+            f1 = (("k_sf_fwd", _lib.RLKS_PHASE_F1A), ("k_sf_bwd", _lib.RLKS_PHASE_F1B),
+                  ("f1_total", _lib.RLKS_PHASE_FWD_PI | _lib.RLKS_PHASE_FWD_VF))
+        else:
+            f1 = (("k_sf_fwdbwd", _lib.RLKS_PHASE_FWD_PI | _lib.RLKS_PHASE_FWD_VF),)
+        phases = (("k_sf_prep", _lib.RLKS_PHASE_PREP), *f1,
                   ("k_sf_dw2", _lib.RLKS_PHASE_DW2), ("k_reduce", _lib.RLKS_PHASE_REDUCE))
         peak, peak_name = SF16_PEAK_TFLOPS, "frac_sf16_mfma"
     else:
@@ -165,6 +173,9 @@ def kernel_timing(algo, torch, config="c2", reps=20):
             tf = flops_per_row(name, D, H, A) * algo.mb / (ms * 1e-3) / 1e12
             rec.update({"tflops": tf, peak_name: tf / peak, "frac_fp32_mfma_peak": tf / FP32_MFMA_PEAK_TFLOPS})
         out[name] = rec
+    if "f1_total" in out:
+        tf = flops_per_row("k_sf_fwdbwd", D, H, A) * algo.mb / (out["f1_total"]["ms"] * 1e-3) / 1e12
+        out["f1_total"].update({"tflops": tf, peak_name: tf / peak})
     ms = timed(lambda: _lib.call("rlks_ppo_grad", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(),
                                  algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None,
                                  algo.ws.data_ptr(), algo.ws.numel(), s.cuda_stream), n=reps if H <= 256 else 3)

@@ -230,9 +230,15 @@ int rlks_ppo_grad(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, cons
 #define RLKS_PHASE_FWD_PI 16 /* F1 of the policy net only (profiling) */
 #define RLKS_PHASE_FWD_VF 32 /* F1 of the value net only (profiling) */
 #define RLKS_PHASE_PREP 64   /* split-fp16: weight split/permute (implied by RLKS_PHASE_FWD) */
+#define RLKS_PHASE_F1A 128   /* split-fp16, split F1: k_sf_fwd only, both nets (profiling) */
+#define RLKS_PHASE_F1B 256   /* split-fp16, split F1: k_sf_bwd only, both nets (profiling) */
 int rlks_ppo_grad_phases(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
                          const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
                          void* workspace_dev, int64_t workspace_bytes, int phases, void* stream);
+
+/* 1 when the split-fp16 F1 runs as the k_sf_fwd + k_sf_bwd pair (the default; RLKS_F1_SPLIT=0 selects
+ * the fused one-wave-per-SIMD k_sf_fwdbwd), 0 otherwise.  Profiling / reporting only. */
+int rlks_sf_f1_split(void);
 
 /* torch.optim.Adam step (lerp form of exp_avg, bias-corrected), in place on n floats */
 int rlks_adam_step(float* params_dev, const float* grad_dev, float* m_dev, float* v_dev, int64_t n,

@@ -296,6 +296,7 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     const int An = net == 0 ? A : 1;
     SfNet& n = w.n[net];
     n.dz2t = (float*)take(4LL * M * HID);
+    n.tile_edz = (int*)take(4LL * tiles);
     n.part_w1 = (float*)take(4LL * w.blocks * HID * D);
     n.part_b1 = (float*)take(4LL * w.blocks * HID);
     n.part_w3 = (float*)take(4LL * tiles * An * HID);
@@ -515,6 +516,10 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
   // F1 (forward, loss, dZ2, dH1 -> dW1 / db1, dW3 / db3) per net; F2 (dW2, db2) for both
   if (f_pi || f_vf)
     if (int rc = launch_sf_f1(a, f_pi ? 0 : 1, (f_pi && f_vf) ? 2 : 1, A, s)) return rc;
+  // split F1 halves alone, both nets (profiling: each reads what a full F1 left in the workspace)
+  if (!(f_pi || f_vf) && (phases & (RLKS_PHASE_F1A | RLKS_PHASE_F1B)))
+    if (int rc = launch_sf_f1(a, 0, 2, A, s, (phases & RLKS_PHASE_F1A ? 1 : 0) | (phases & RLKS_PHASE_F1B ? 2 : 0)))
+      return rc;
   if (phases & RLKS_PHASE_DW2)
     if (int rc = launch_sf_dw2(a, w.splits, s)) return rc;
   if (!(phases & RLKS_PHASE_REDUCE)) return RLKS_OK;
@@ -627,6 +632,8 @@ int rlks_ppo_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float
                   void* stream) {
   return rlks_ppo_grad_phases(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, stream);
 }
+
+int rlks_sf_f1_split(void) { return sf_f1_split() ? 1 : 0; }
 
 int rlks_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                    float eps, int step, void* stream) {

@@ -31,6 +31,7 @@ struct SfNet {
   const float* sc;
   unsigned* dzmax;
   float* dz2t;  // [M/32][HID][32]
+  int* tile_edz;  // [M/32] split F1: each tile's dZ2 split exponent (F1a -> F1b)
   float *part_w1, *part_b1;                 // [F1 blocks][...]
   float *part_w3, *part_b3, *part_stat;     // [tiles of 32 rows][...]
   float *part_w2, *part_b2;                                   // [splits][...]
@@ -71,9 +72,14 @@ struct SfRollArgs {
 int launch_sf_roll(const SfRollArgs& a, int mode, hipStream_t s);
 
 size_t sf_f1_lds_bytes(int A_, int NG, int KD, int W);
+#ifndef RLKS_F1_SPLIT_DEFAULT
+#define RLKS_F1_SPLIT_DEFAULT 1
+#endif
+bool sf_f1_split();
 int sf_kd(int D);
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
-int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s);  // needs M % 256 == 0
+// halves (split F1 only): 1 = k_sf_fwd, 2 = k_sf_bwd, 3 = both; the fused kernel ignores it
+int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int halves = 3);  // needs M % 256 == 0
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
 
 }  // namespace rlks

@@ -28,6 +28,7 @@
 // Reference semantics: RLlib FCNet [256, 256] tanh, vf_share_layers=False, PPO loss as in
 // mlp_fwd.hip (train_ppo.py:9-31; RLlib third-party).
 #include <cmath>
+#include <cstdlib>
 
 #include "sgd_sf16.h"
 
@@ -240,13 +241,80 @@ __device__ __forceinline__ void sf_frag(const _Float16* buf, int row, int h, h8 
 }
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// PPO loss of one row (RLlib ppo_torch_policy semantics): d loss / d logits (pi) or
+// d loss / d value (vf), scaled by 1 / global rows, and the row's [policy loss, vf loss, kl,
+// entropy] terms
+template <int A_, int NET>
+__device__ __forceinline__ void sf_loss(const SfArgs& g, const float (&out)[A_], int row, float (&dl)[A_],
+                                        float (&st)[4]) {
+  const int D = g.D;
+  const float* rec = g.x + (size_t)row * g.x_stride;
+  const float inv_count = g.dyn[RLKS_DYN_INV_COUNT];
+  const int Ap = g.A_pi;
+  st[0] = st[1] = st[2] = st[3] = 0.f;
+  if (NET == 0) {
+    const float* lo = rec + D;
+    const float adv = (rec[D + Ap] - g.dyn[RLKS_DYN_ADV_MEAN]) * g.dyn[RLKS_DYN_ADV_INVSTD];
+    const float logp_old = rec[D + Ap + 2];
+    const int act = (int)rec[D + Ap + 3];
+    float mx = out[0], mo = lo[0];
+#pragma unroll
+    for (int a = 1; a < A_; ++a) { mx = fmaxf(mx, out[a]); mo = fmaxf(mo, lo[a]); }
+    float se = 0.f, so = 0.f;
+#pragma unroll
+    for (int a = 0; a < A_; ++a) { se += expf(out[a] - mx); so += expf(lo[a] - mo); }
+    const float lse = mx + logf(se), lso = mo + logf(so);
+    float p[A_], lp[A_], po[A_];
+    float kl = 0.f, ent = 0.f, lpa = 0.f;
+#pragma unroll
+    for (int a = 0; a < A_; ++a) {
+      lp[a] = out[a] - lse;
+      p[a] = expf(lp[a]);
+      const float lpo = lo[a] - lso;
+      po[a] = expf(lpo);
+      kl += po[a] * (lpo - lp[a]);
+      ent -= p[a] * lp[a];
+      lpa = (a == act) ? lp[a] : lpa;
+    }
+    const float ratio = expf(lpa - logp_old);
+    const float lo_c = 1.f - g.co.clip_param, hi_c = 1.f + g.co.clip_param;
+    const float rc = fminf(fmaxf(ratio, lo_c), hi_c);
+    const float s1 = adv * ratio, s2 = adv * rc;
+    // torch.min backward splits ties evenly; torch.clamp passes the gradient on [lo, hi]
+    const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+    const float inr = (ratio >= lo_c && ratio <= hi_c) ? 1.f : 0.f;
+    const float dr = -adv * (w1 + (1.f - w1) * inr) * ratio;
+    const float klc = g.dyn[RLKS_DYN_KL_COEFF];
+#pragma unroll
+    for (int a = 0; a < A_; ++a) {
+      float d = dr * ((a == act ? 1.f : 0.f) - p[a]);
+      d += klc * (p[a] - po[a]);
+      d += g.co.entropy_coeff * p[a] * (lp[a] + ent);
+      dl[a] = d * inv_count;
+    }
+    st[0] = -fminf(s1, s2);
+    st[2] = kl;
+    st[3] = ent;
+  } else {
+    const float diff = out[0] - rec[D + Ap + 1];
+    const float sq = diff * diff;
+    st[1] = fminf(sq, g.co.vf_clip_param);
+    dl[0] = (sq <= g.co.vf_clip_param) ? g.co.vf_loss_coeff * 2.f * diff * inv_count : 0.f;
+  }
+}
+
 #ifdef RLKS_STAMPS
 // diagnostic build only (tools/stamps.sh): per-wave phase clocks of F1, [net][tile][phase]
 __device__ unsigned long long g_sf_stamps[2][4096][8];
 #define SF_STAMP(i) \
   if (l == 0 && tile < 4096) g_sf_stamps[NET][tile][i] = __builtin_amdgcn_s_memtime()
+// loop-internal clocks: Z2 chunk 3 (top, after the MFMA steps, after the barrier) and dH1 n-tile 3
+__device__ unsigned long long g_sf_stamps2[2][4096][8];
+#define SF_STAMP2(i) \
+  if (l == 0 && tile < 4096) g_sf_stamps2[NET][tile][i] = __builtin_amdgcn_s_memtime()
 #else
 #define SF_STAMP(i)
+#define SF_STAMP2(i)
 #endif
 
 // W waves per workgroup, one 32-row tile each; one wave per SIMD (waves_per_eu 1) so that every
@@ -354,6 +422,7 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
     // fragments, then n-tile nt's six MFMAs, so every read has a whole step (192 MFMA cycles) to
     // land and only two fragment sets are live (the register budget goes to the accumulators).
     // The next k-tile's H1^T (kn = c + 1; the last is discarded) is computed in the MFMA shadows.
+    if (c == 3) SF_STAMP2(0);
     const int kn = c + 1 < 8 ? c + 1 : 7;
     h8 fc[2][2], fn[2][2], nbh[2], nbl[2];
     f32x16 z;
@@ -394,8 +463,11 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) { bh[s] = nbh[s]; bl[s] = nbl[s]; }
+    if (c == 3) SF_STAMP2(1);
     chunk_store<W>(sCh + ((c + 1) & 1) * 2 * SF_CH, w, l, cv);
+    if (c == 3) SF_STAMP2(2);
     __syncthreads();
+    if (c == 3) SF_STAMP2(3);
   }
 
   SF_STAMP(2);
@@ -441,61 +513,9 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
 
   // ---- PPO loss for row m = row0 + r (both half-waves compute it; stats from h = 0)
   float dl[A_];
-  float st_pl = 0.f, st_vf = 0.f, st_kl = 0.f, st_ent = 0.f;
-  {
-    const float* rec = g.x + (size_t)(row0 + r) * stride;
-    const float inv_count = g.dyn[RLKS_DYN_INV_COUNT];
-    const int Ap = g.A_pi;
-    if (NET == 0) {
-      const float* lo = rec + D;
-      const float adv = (rec[D + Ap] - g.dyn[RLKS_DYN_ADV_MEAN]) * g.dyn[RLKS_DYN_ADV_INVSTD];
-      const float logp_old = rec[D + Ap + 2];
-      const int act = (int)rec[D + Ap + 3];
-      float mx = out[0], mo = lo[0];
-#pragma unroll
-      for (int a = 1; a < A_; ++a) { mx = fmaxf(mx, out[a]); mo = fmaxf(mo, lo[a]); }
-      float se = 0.f, so = 0.f;
-#pragma unroll
-      for (int a = 0; a < A_; ++a) { se += expf(out[a] - mx); so += expf(lo[a] - mo); }
-      const float lse = mx + logf(se), lso = mo + logf(so);
-      float p[A_], lp[A_], po[A_];
-      float kl = 0.f, ent = 0.f, lpa = 0.f;
-#pragma unroll
-      for (int a = 0; a < A_; ++a) {
-        lp[a] = out[a] - lse;
-        p[a] = expf(lp[a]);
-        const float lpo = lo[a] - lso;
-        po[a] = expf(lpo);
-        kl += po[a] * (lpo - lp[a]);
-        ent -= p[a] * lp[a];
-        lpa = (a == act) ? lp[a] : lpa;
-      }
-      const float ratio = expf(lpa - logp_old);
-      const float lo_c = 1.f - g.co.clip_param, hi_c = 1.f + g.co.clip_param;
-      const float rc = fminf(fmaxf(ratio, lo_c), hi_c);
-      const float s1 = adv * ratio, s2 = adv * rc;
-      // torch.min backward splits ties evenly; torch.clamp passes the gradient on [lo, hi]
-      const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
-      const float inr = (ratio >= lo_c && ratio <= hi_c) ? 1.f : 0.f;
-      const float dr = -adv * (w1 + (1.f - w1) * inr) * ratio;
-      const float klc = g.dyn[RLKS_DYN_KL_COEFF];
-#pragma unroll
-      for (int a = 0; a < A_; ++a) {
-        float d = dr * ((a == act ? 1.f : 0.f) - p[a]);
-        d += klc * (p[a] - po[a]);
-        d += g.co.entropy_coeff * p[a] * (lp[a] + ent);
-        dl[a] = d * inv_count;
-      }
-      st_pl = -fminf(s1, s2);
-      st_kl = kl;
-      st_ent = ent;
-    } else {
-      const float diff = out[0] - rec[D + Ap + 1];
-      const float sq = diff * diff;
-      st_vf = fminf(sq, g.co.vf_clip_param);
-      dl[0] = (sq <= g.co.vf_clip_param) ? g.co.vf_loss_coeff * 2.f * diff * inv_count : 0.f;
-    }
-  }
+  float stv[4];
+  sf_loss<A_, NET>(g, out, row0 + r, dl, stv);
+  const float st_pl = stv[0], st_vf = stv[1], st_kl = stv[2], st_ent = stv[3];
 
   SF_STAMP(3);
   // ---- per-tile partials straight to HBM: dW3[a][n] = sum_m dl[m][a] H2[m][n] (half-wave
@@ -529,11 +549,13 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
   // ---- dZ2^T = (dl W3) (1 - H2^2): to HBM (F2), tile max |dZ2| (this wave's split + F2's scale)
   float dmx = 0.f;
   {
-    float* dst = N.dz2t + (size_t)tile * HID * 32 + r;
+    // one base per n-tile, so every store of the n-tile takes an immediate offset (< 4 KB)
+    float* dst0 = N.dz2t + (size_t)tile * HID * 32 + 4 * h * 32 + r;
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt)
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
+        float* dst = dst0 + (size_t)nt * 32 * 32 + (size_t)8 * gq * 32;
         const int n0 = 32 * nt + 8 * gq + 4 * h;
         float wv[A_][4];
 #pragma unroll
@@ -551,7 +573,7 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
           const float dz = gsum * (1.f - h2 * h2);
           acc[nt][q] = dz;
           dmx = fmaxf(dmx, fabsf(dz));
-          dst[(size_t)(n0 + i) * 32] = dz;
+          dst[i * 32] = dz;
         }
       }
   }
@@ -584,6 +606,7 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
     const int c = 8 + nt;
     const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
     v4u cv[32 / W];
+    if (nt == 3) SF_STAMP2(4);
     if (nt < 7) chunk_load<W>(N, c + 1, w, l, cv);
     h8 ah[2], al[2], fc[2][2], fn[2][2];
     split16(acc[nt], 0, sdz, ah[0], al[0]);
@@ -604,8 +627,11 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) { fc[s][0] = fn[s][0]; fc[s][1] = fn[s][1]; }
     }
+    if (nt == 3) SF_STAMP2(5);
     if (nt < 7) chunk_store<W>(sCh + ((c + 1) & 1) * 2 * SF_CH, w, l, cv);
+    if (nt == 3) SF_STAMP2(6);
     __syncthreads();
+    if (nt == 3) SF_STAMP2(7);
   }
   SF_STAMP(6);
   // ---- dZ1 = dH1 (1 - H1^2) -> dW1a^T = Xa^T dZ1 per k-tile; dZ1 enters the split at
@@ -688,6 +714,440 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
     if (kt < 7) der = nder;
   }
   SF_STAMP(7);
+}
+
+// ----------------------------------------------------------------------------- split F1
+// The fused F1 needs ~460 registers (the Z2^T / dZ2^T accumulators plus the eight dH1 k-tile
+// accumulators), so it runs one wave per SIMD and its ~9k VALU instructions per tile (tanh and
+// splits, head, dW3, dZ2, dZ1) cannot hide behind another wave's MFMAs.  Split at the dZ2 hand-off
+// (which F2 needs in HBM anyway), each half fits 256 registers and ~50-80 KB of LDS, so two
+// independent workgroups share every CU and each SIMD interleaves two waves in different phases:
+//   F1a (k_sf_fwd): Z1, Z2^T = W2 H1^T, head, loss, dW3 / db3 / stats, dZ2^T -> HBM, tile scale;
+//   F1b (k_sf_bwd): dH1 = dZ2 W2 (dZ2^T n-tiles from HBM, W2 chunks per k-half), dZ1, dW1a.
+// W2 chunks are single-buffered: a step computes from LDS while its successor is loaded into
+// registers, then barrier / store / barrier.
+// Half-chunk of the Z2 loop: w2p rows n in [128 p, +128), columns [32 c, +32) -> [128][32] image;
+// of the dH1 loop: w2t rows k in [128 p, +128), columns [32 nt, +32).  1024 slots of 16 B (hi,
+// lo): 16 blocks of 64 lanes, wave w of W moves blocks (16 / W) w + i.
+template <int W>
+__device__ __forceinline__ void half_load(const _Float16* hi, const _Float16* lo, int p, int col, int w, int l,
+                                          v4u (&v)[16 / W]) {
+#pragma unroll
+  for (int i = 0; i < 16 / W; ++i) {
+    const int blk = (16 / W) * w + i, arr = blk >> 3, sig = (blk & 7) * 64 + l;
+    const int row = sig >> 2, pc = (sig & 3) ^ ((row >> 2) & 3);
+    v[i] = *reinterpret_cast<const v4u*>((arr ? lo : hi) + (128 * p + row) * HID + col + 8 * pc);
+  }
+}
+template <int W>
+__device__ __forceinline__ void half_store(_Float16* buf, int w, int l, const v4u (&v)[16 / W]) {
+  constexpr int HALF = SF_CH / 2;  // halves per [128][32] image
+#pragma unroll
+  for (int i = 0; i < 16 / W; ++i) {
+    const int blk = (16 / W) * w + i, arr = blk >> 3;
+    *reinterpret_cast<v4u*>(buf + arr * HALF + ((blk & 7) * 64 + l) * 8) = v[i];
+  }
+}
+// the same half-chunk by LDS-DMA (no staging registers; the split kernels run two waves per SIMD,
+// which hide the LDS waits the DMA brings with it)
+template <int W>
+__device__ __forceinline__ void half_dma(const _Float16* hi, const _Float16* lo, int p, int col, _Float16* buf, int w,
+                                         int l) {
+  constexpr int HALF = SF_CH / 2;
+#pragma unroll
+  for (int i = 0; i < 16 / W; ++i) {
+    const int blk = (16 / W) * w + i, arr = blk >> 3, sig = (blk & 7) * 64 + l;
+    const int row = sig >> 2, pc = (sig & 3) ^ ((row >> 2) & 3);
+    const _Float16* src = (arr ? lo : hi) + (128 * p + row) * HID + col + 8 * pc;
+    _Float16* dst = buf + arr * HALF + (blk & 7) * 64 * 8;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void half_frag(const _Float16* buf, int row, int h, h8 (&f)[2][2]) {
+  constexpr int HALF = SF_CH / 2;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int off = row * 32 + 8 * ((2 * s + h) ^ ((row >> 2) & 3));
+    f[s][0] = *reinterpret_cast<const h8*>(buf + off);
+    f[s][1] = *reinterpret_cast<const h8*>(buf + HALF + off);
+  }
+}
+
+template <int A_, int NET, int KD, int W>
+__device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
+  constexpr int NTHR = 64 * W;
+  constexpr int KS = KD / 16;
+  constexpr int HALF = SF_CH / 2;
+  const SfNet& N = g.n[NET];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  _Float16* sCh = reinterpret_cast<_Float16*>(lds);             // [2 buf][2 hi/lo][128][32] (32 KB)
+  float* sB2 = lds + SF_CH;                                     // [HID]
+  float* sW3 = sB2 + HID;                                       // [A_][HID]
+  _Float16* sW1 = reinterpret_cast<_Float16*>(sW3 + A_ * HID);  // [2 hi/lo][HID k][KD] (swizzled)
+
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int D = g.D, stride = g.x_stride;
+  const int tile = blockIdx.x * W + w, row0 = tile * 32;
+
+  half_dma<W>(N.w2ph, N.w2pl, 0, 0, sCh, w, l);
+  for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i];
+  for (int i = tid; i < A_ * HID; i += NTHR) sW3[i] = N.w3[i];
+  float xv[KS * 8];
+  const float* xr = g.x + (size_t)(row0 + r) * stride;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[ks * 8 + j] = xa_elem(xr, 16 * ks + 8 * h + j, D);
+  float xm = 0.f;
+#pragma unroll
+  for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
+  const float sx = pow2(sf_exp(wave_max(xm)));
+  h8 xh[KS], xl[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) split8(xv, ks * 8, sx, xh[ks], xl[ks]);
+  const float inv_z1 = N.sc[1] / sx;
+  for (int p = tid; p < 2 * HID * KD / 8; p += NTHR) {
+    const int arr = p / (HID * KD / 8), q = p - arr * (HID * KD / 8), k = q / (KD / 8), pc = q - k * (KD / 8);
+    const v4u v = *reinterpret_cast<const v4u*>((arr ? N.w1l : N.w1h) + k * KD + 8 * pc);
+    *reinterpret_cast<v4u*>(sW1 + arr * HID * KD + k * KD + 8 * (pc ^ ((k >> 3) & 1))) = v;
+  }
+  h8 wh[KS], wl[KS];
+  auto w1_frag = [&](int kt) {
+    const int k = 32 * kt + r;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int off = k * KD + 8 * ((2 * ks + h) ^ ((k >> 3) & 1));
+      wh[ks] = *reinterpret_cast<const h8*>(sW1 + off);
+      wl[ks] = *reinterpret_cast<const h8*>(sW1 + HID * KD + off);
+    }
+  };
+  auto h1t = [&](int kt, h8 (&bh)[2], h8 (&bl)[2]) {
+    w1_frag(kt);
+    f32x16 z;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) z = mma3(wh[ks], wl[ks], xh[ks], xl[ks], z);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
+    split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
+    split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
+  };
+  vm_drain();
+  __syncthreads();
+
+  // ---- Z2^T = W2 H1^T: 16 steps (k-tile c, n-half p) of 24 MFMAs over double-buffered
+  // half-chunks; H1^T of k-tile c is computed at the start of its first step
+  f32x16 acc[8];
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
+  h8 bh[2], bl[2];
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {  // step 2c + p reads buffer p; the next half-chunk -> buffer p ^ 1
+      if (!(c == 7 && p == 1)) half_dma<W>(N.w2ph, N.w2pl, p ^ 1, 32 * (c + p), sCh + (p ^ 1) * SF_CH, w, l);
+      if (p == 0) h1t(c, bh, bl);
+      const _Float16* buf = sCh + p * SF_CH;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h8 fc[2][2];
+        half_frag(buf, 32 * j + r, h, fc);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          acc[4 * p + j] = mma(fc[s][1], bh[s], acc[4 * p + j]);
+          acc[4 * p + j] = mma(fc[s][0], bl[s], acc[4 * p + j]);
+          acc[4 * p + j] = mma(fc[s][0], bh[s], acc[4 * p + j]);
+        }
+      }
+      vm_drain();
+      __syncthreads();
+    }
+  }
+
+  // ---- H2^T = tanh(Z2^T + b2), head out[a] = b3 + sum_n W3[a][n] H2[n]
+  const float inv_z2 = N.sc[3] / SF_H1_SCALE;
+  float out[A_];
+#pragma unroll
+  for (int a = 0; a < A_; ++a) out[a] = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int n0 = 32 * nt + 8 * gq + 4 * h;
+      const float4 bb = *reinterpret_cast<const float4*>(sB2 + n0);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+      float wv[A_][4];
+#pragma unroll
+      for (int a = 0; a < A_; ++a) {
+        const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
+        wv[a][0] = t.x; wv[a][1] = t.y; wv[a][2] = t.z; wv[a][3] = t.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = 4 * gq + i;
+        const float h2 = tanh_abs(fmaf(acc[nt][q], inv_z2, bv[i]));
+        acc[nt][q] = h2;
+#pragma unroll
+        for (int a = 0; a < A_; ++a) out[a] = fmaf(h2, wv[a][i], out[a]);
+      }
+    }
+#pragma unroll
+  for (int a = 0; a < A_; ++a) out[a] += __shfl_xor(out[a], 32, 64) + N.b3[a];
+  float dl[A_];
+  float st[4];
+  sf_loss<A_, NET>(g, out, row0 + r, dl, st);
+  // ---- dW3 (half-wave reduce), db3, loss stats
+#pragma unroll
+  for (int a = 0; a < A_; ++a)
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = dl[a] * acc[nt][q];
+      const float t = half_wave_reduce16(v, l);
+      if ((l & 1) == 0) N.part_w3[((size_t)tile * A_ + a) * HID + 32 * nt + acc_row((l >> 1) & 15, l)] = t;
+    }
+  {
+    float sv[A_ + 4];
+#pragma unroll
+    for (int a = 0; a < A_; ++a) sv[a] = h ? 0.f : dl[a];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sv[A_ + i] = h ? 0.f : st[i];
+#pragma unroll
+    for (int i = 0; i < A_ + 4; ++i) {
+      const float t = wave_sum(sv[i]);
+      if (l == 0) {
+        if (i < A_) N.part_b3[(size_t)tile * A_ + i] = t;
+        else N.part_stat[(size_t)tile * 4 + i - A_] = t;
+      }
+    }
+  }
+  // ---- dZ2^T = (dl W3) (1 - H2^2) -> HBM; the tile's split exponent for F1b, max for F2
+  float dmx = 0.f;
+  {
+    // one base per n-tile, so every store of the n-tile takes an immediate offset (< 4 KB)
+    float* dst0 = N.dz2t + (size_t)tile * HID * 32 + 4 * h * 32 + r;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        float* dst = dst0 + (size_t)nt * 32 * 32 + (size_t)8 * gq * 32;
+        const int n0 = 32 * nt + 8 * gq + 4 * h;
+        float wv[A_][4];
+#pragma unroll
+        for (int a = 0; a < A_; ++a) {
+          const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
+          wv[a][0] = t.x; wv[a][1] = t.y; wv[a][2] = t.z; wv[a][3] = t.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = 4 * gq + i;
+          float gsum = 0.f;
+#pragma unroll
+          for (int a = 0; a < A_; ++a) gsum = fmaf(dl[a], wv[a][i], gsum);
+          const float h2 = acc[nt][q];
+          const float dz = gsum * (1.f - h2 * h2);
+          dmx = fmaxf(dmx, fabsf(dz));
+          dst[i * 32] = dz;
+        }
+      }
+  }
+  dmx = wave_max(dmx);
+  if (l == 0) {
+    atomicMax(N.dzmax, __float_as_uint(dmx));
+    N.tile_edz[tile] = sf_exp(dmx);
+  }
+}
+
+template <int A_, int KD, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sf_fwd(SfArgs g) {
+  if (blockIdx.y + g.net0 == 0) sf_fwd_body<A_, 0, KD, W>(g);
+  else sf_fwd_body<1, 1, KD, W>(g);
+}
+
+template <int NET, int KD, int NG, int W>
+__device__ __forceinline__ void sf_bwd_body(const SfArgs& g) {
+  constexpr int NTHR = 64 * W;
+  constexpr int KS = KD / 16;
+  constexpr int DWR = 8 * NG;
+  constexpr int SLOT = W * 32 * DWR;                           // floats per k-tile of dW1a^T partials
+  constexpr int KPR = SF_CH / SLOT >= 4 ? 4 : SF_CH / SLOT;   // k-tiles per flush round (32-KB buffers)
+  static_assert(KPR >= 1 && 4 % KPR == 0, "dW1 epilogue slots");
+  const SfNet& N = g.n[NET];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  _Float16* sCh = reinterpret_cast<_Float16*>(lds);             // [2 buf][2 hi/lo][128][32] (32 KB)
+  _Float16* sW1 = reinterpret_cast<_Float16*>(lds + SF_CH);    // [2 hi/lo][HID k][KD] (swizzled)
+  h8* sXT = reinterpret_cast<h8*>(sW1 + 2 * HID * KD);          // [W][2 s][2 hi/lo][64 lanes]
+  float* sEp = lds;                                             // epilogue slots (the chunk buffers)
+
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int D = g.D, stride = g.x_stride;
+  const int tile = blockIdx.x * W + w, row0 = tile * 32, blk = blockIdx.x;
+
+  half_dma<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
+  float xv[KS * 8];
+  const float* xr = g.x + (size_t)(row0 + r) * stride;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[ks * 8 + j] = xa_elem(xr, 16 * ks + 8 * h + j, D);
+  float xm = 0.f;
+#pragma unroll
+  for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
+  const int ex = sf_exp(wave_max(xm));
+  const float sx = pow2(ex);
+  h8 xh[KS], xl[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) split8(xv, ks * 8, sx, xh[ks], xl[ks]);
+  const float inv_z1 = N.sc[1] / sx;
+  {  // Xa^T for dW1a^T = Xa^T dZ1 (lane row d = r, m = perm(s, h, j))
+    float xtv[16];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xtv[s * 8 + j] = xa_elem(g.x + (size_t)(row0 + sf_perm(s, h, j)) * stride, r, D);
+    h8 a, b;
+    split8(xtv, 0, sx, a, b);
+    sXT[(w * 4 + 0) * 64 + l] = a;
+    sXT[(w * 4 + 1) * 64 + l] = b;
+    split8(xtv, 8, sx, a, b);
+    sXT[(w * 4 + 2) * 64 + l] = a;
+    sXT[(w * 4 + 3) * 64 + l] = b;
+  }
+  for (int p = tid; p < 2 * HID * KD / 8; p += NTHR) {
+    const int arr = p / (HID * KD / 8), q = p - arr * (HID * KD / 8), k = q / (KD / 8), pc = q - k * (KD / 8);
+    const v4u v = *reinterpret_cast<const v4u*>((arr ? N.w1l : N.w1h) + k * KD + 8 * pc);
+    *reinterpret_cast<v4u*>(sW1 + arr * HID * KD + k * KD + 8 * (pc ^ ((k >> 3) & 1))) = v;
+  }
+  h8 wh[KS], wl[KS];
+  auto w1_frag = [&](int kt) {
+    const int k = 32 * kt + r;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int off = k * KD + 8 * ((2 * ks + h) ^ ((k >> 3) & 1));
+      wh[ks] = *reinterpret_cast<const h8*>(sW1 + off);
+      wl[ks] = *reinterpret_cast<const h8*>(sW1 + HID * KD + off);
+    }
+  };
+  const int edz = N.tile_edz[tile];
+  const float sdz = pow2(edz);
+  const float sz1 = pow2(-23);
+  const float u1 = pow2(23 - ex - edz - (int)N.sc[5]);
+  // dZ2^T n-tile nt of this wave's rows in accumulator form (register q <-> row n = acc_row(q, l)):
+  // one base address and constant offsets
+  const float* dzsrc = N.dz2t + (size_t)tile * HID * 32 + 4 * h * 32 + r;
+  auto dz_load = [&](int nt, float (&v)[16]) {
+    const float* b = dzsrc + (size_t)nt * 32 * 32;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = b[((q & 3) + 8 * (q >> 2)) * 32];
+  };
+  vm_drain();
+  __syncthreads();
+
+  // ---- two passes over the k-halves p: dH1 k-tiles 4p .. 4p+3 accumulate over the 8 n-tiles
+  // (24 MFMAs per n-tile step; half-chunks double-buffered), then their dZ1 and dW1a^T
+#pragma unroll 1
+  for (int p = 0; p < 2; ++p) {
+    f32x16 dh[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dh[j][q] = 0.f;
+    float dzc[16], dzn[16];
+    dz_load(0, dzc);
+    for (int nt = 0; nt < 8; ++nt) {
+      if (nt < 7) {
+        half_dma<W>(N.w2th, N.w2tl, p, 32 * (nt + 1), sCh + ((nt + 1) & 1) * SF_CH, w, l);
+        dz_load(nt + 1, dzn);
+      }
+      const _Float16* buf = sCh + (nt & 1) * SF_CH;
+      h8 ah[2], al[2];
+      split8(dzc, 0, sdz, ah[0], al[0]);
+      split8(dzc, 8, sdz, ah[1], al[1]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h8 fc[2][2];
+        half_frag(buf, 32 * j + r, h, fc);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          dh[j] = mma(al[s], fc[s][0], dh[j]);
+          dh[j] = mma(ah[s], fc[s][1], dh[j]);
+          dh[j] = mma(ah[s], fc[s][0], dh[j]);
+        }
+      }
+      vm_drain();
+      __syncthreads();
+      if (nt < 7)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dzc[q] = dzn[q];
+    }
+    // ---- dZ1 = dH1 (1 - H1^2) -> dW1a^T of k-tiles 4p + j; sums over the W waves in the chunk
+    // buffers (free now), KPR k-tiles per round
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kt = 4 * p + j;
+      w1_frag(kt);
+      f32x16 z;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) z = mma3(xh[ks], xl[ks], wh[ks], wl[ks], z);
+      f32x16 dz;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float h1 = tanh_abs(z[q] * inv_z1);
+        dz[q] = dh[j][q] * (1.f - h1 * h1);
+      }
+      h8 zh[2], zl[2];
+      split16(dz, 0, sz1, zh[0], zl[0]);
+      split16(dz, 8, sz1, zh[1], zl[1]);
+      f32x16 wacc, wacc2;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) { wacc[q] = 0.f; wacc2[q] = 0.f; }
+      const h8 x0h = sXT[(w * 4 + 0) * 64 + l], x0l = sXT[(w * 4 + 1) * 64 + l];
+      const h8 x1h = sXT[(w * 4 + 2) * 64 + l], x1l = sXT[(w * 4 + 3) * 64 + l];
+      wacc = mma(x0l, zh[0], wacc);
+      wacc2 = mma(x1l, zh[1], wacc2);
+      wacc = mma(x0h, zl[0], wacc);
+      wacc2 = mma(x1h, zl[1], wacc2);
+      wacc = mma(x0h, zh[0], wacc);
+      wacc2 = mma(x1h, zh[1], wacc2);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) wacc[q] += wacc2[q];
+#pragma unroll
+      for (int gq = 0; gq < NG; ++gq) {
+        float4 v = {wacc[4 * gq] * u1, wacc[4 * gq + 1] * u1, wacc[4 * gq + 2] * u1, wacc[4 * gq + 3] * u1};
+        *reinterpret_cast<float4*>(sEp + (j % KPR) * SLOT + (w * 32 + r) * DWR + 8 * gq + 4 * h) = v;
+      }
+      if (j % KPR == KPR - 1) {
+        __syncthreads();
+        const int nd = D + 1, kt0 = kt + 1 - KPR;
+        for (int e = tid; e < KPR * 32 * nd; e += NTHR) {
+          const int jj = e / (32 * nd), e2 = e - jj * 32 * nd, kk = e2 / nd, d = e2 - kk * nd;
+          const int k = 32 * (kt0 + jj) + kk;
+          float sum = 0.f;
+#pragma unroll
+          for (int ww = 0; ww < W; ++ww) sum += sEp[jj * SLOT + (ww * 32 + kk) * DWR + d];
+          if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = sum;
+          else N.part_b1[(size_t)blk * HID + k] = sum;
+        }
+        __syncthreads();
+      }
+    }
+    if (p == 0) {  // the second pass's first half-chunk (the buffers held the epilogue slots)
+      half_dma<W>(N.w2th, N.w2tl, 1, 0, sCh, w, l);
+      vm_drain();
+      __syncthreads();
+    }
+  }
+}
+
+template <int KD, int NG, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sf_bwd(SfArgs g) {
+  if (blockIdx.y + g.net0 == 0) sf_bwd_body<0, KD, NG, W>(g);
+  else sf_bwd_body<1, KD, NG, W>(g);
 }
 
 // both nets in one grid (blockIdx.y + net0): the hardware backfills CUs across the two nets
@@ -859,11 +1319,24 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
 extern "C" int rlks_dbg_sf_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sf_stamps), sizeof(g_sf_stamps)) == hipSuccess ? 0 : 1;
 }
+extern "C" int rlks_dbg_sf_stamps2(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sf_stamps2), sizeof(g_sf_stamps2)) == hipSuccess ? 0 : 1;
+}
 #endif
 
 size_t sf_f1_lds_bytes(int A_, int NG, int KD, int W) {
   return (size_t)2 * 2 * SF_CH * sizeof(_Float16) + (size_t)(HID + A_ * HID) * sizeof(float) +
          (size_t)2 * HID * KD * sizeof(_Float16) + (size_t)W * 4 * 64 * 16;
+}
+
+// F1 as two kernels (F1a k_sf_fwd + F1b k_sf_bwd, two workgroups per CU) or the fused one-wave-
+// per-SIMD kernel: RLKS_F1_SPLIT=0 / 1 overrides the default
+bool sf_f1_split() {
+  static const int v = [] {
+    const char* e = getenv("RLKS_F1_SPLIT");
+    return e ? atoi(e) : RLKS_F1_SPLIT_DEFAULT;
+  }();
+  return v != 0;
 }
 
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
@@ -875,10 +1348,25 @@ int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
 }
 
 template <int A_, int KD, int NG>
-static int launch_f1_net(SfArgs a, int net0, int nets, hipStream_t s) {
+static int launch_f1_net(SfArgs a, int net0, int nets, hipStream_t s, int halves) {
   constexpr int W = SF_F1_W;
   a.net0 = net0;
   const dim3 grid(a.M / (32 * W), nets);
+  if (sf_f1_split()) {
+    const size_t lds_a = (size_t)2 * SF_CH * sizeof(_Float16) + (size_t)(1 + A_) * HID * sizeof(float) +
+                         (size_t)2 * HID * KD * sizeof(_Float16);
+    const size_t lds_b = (size_t)2 * SF_CH * sizeof(_Float16) + (size_t)2 * HID * KD * sizeof(_Float16) +
+                         (size_t)W * 4 * 64 * 16;
+    if (halves & 1) {
+      hipLaunchKernelGGL((k_sf_fwd<A_, KD, W>), grid, dim3(64 * W), lds_a, s, a);
+      RLKS_LAUNCHED();
+    }
+    if (halves & 2) {
+      hipLaunchKernelGGL((k_sf_bwd<KD, NG, W>), grid, dim3(64 * W), lds_b, s, a);
+      RLKS_LAUNCHED();
+    }
+    return RLKS_OK;
+  }
   hipLaunchKernelGGL((k_sf_fwdbwd<A_, KD, NG, W>), grid, dim3(64 * W), sf_f1_lds_bytes(A_, NG, KD, W), s, a);
   RLKS_LAUNCHED();
   return RLKS_OK;
@@ -887,13 +1375,13 @@ static int launch_f1_net(SfArgs a, int net0, int nets, hipStream_t s) {
 // obs_dim = 3 x clusters: C = 2, 4, 8 -> D = 6, 12, 24 (D + 1 <= 8, 16, 32)
 int sf_kd(int D) { return D + 1 <= 16 ? 16 : 32; }
 
-int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s) {
+int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int halves) {
   RLKS_REQUIRE(a.M % SF_ROWS == 0, RLKS_ERR_ARG, "split-fp16 SGD step: rows must be a multiple of 256");
   RLKS_REQUIRE(a.D == 3 * A, RLKS_ERR_UNSUPPORTED, "split-fp16 SGD step expects obs_dim = 3 x n_actions");
   switch (A) {
-    case 2: return launch_f1_net<2, 16, 1>(a, net0, nets, s);
-    case 4: return launch_f1_net<4, 16, 2>(a, net0, nets, s);
-    case 8: return launch_f1_net<8, 32, 4>(a, net0, nets, s);
+    case 2: return launch_f1_net<2, 16, 1>(a, net0, nets, s, halves);
+    case 4: return launch_f1_net<4, 16, 2>(a, net0, nets, s, halves);
+    case 8: return launch_f1_net<8, 32, 4>(a, net0, nets, s, halves);
     default: return fail(RLKS_ERR_UNSUPPORTED, "split-fp16 head is built for 2, 4 or 8 actions");
   }
 }

@@ -21,7 +21,7 @@ RLKS_DYN_SIZE = 8
 RLKS_DYN_ADV_MEAN, RLKS_DYN_ADV_INVSTD, RLKS_DYN_KL_COEFF, RLKS_DYN_INV_COUNT = 0, 1, 2, 3
 RLKS_STAT_SIZE = 8
 RLKS_PHASE_FWD, RLKS_PHASE_DW2, RLKS_PHASE_DH1, RLKS_PHASE_REDUCE, RLKS_PHASE_ALL = 1, 2, 4, 8, 15
-RLKS_PHASE_FWD_PI, RLKS_PHASE_FWD_VF, RLKS_PHASE_PREP = 16, 32, 64
+RLKS_PHASE_FWD_PI, RLKS_PHASE_FWD_VF, RLKS_PHASE_PREP, RLKS_PHASE_F1A, RLKS_PHASE_F1B = 16, 32, 64, 128, 256
 RLKS_PRECISION_FP32, RLKS_PRECISION_SF16, RLKS_PRECISION_WIDE = 0, 1, 2
 RLKS_STAT_POLICY_LOSS, RLKS_STAT_VF_LOSS, RLKS_STAT_KL, RLKS_STAT_ENTROPY, RLKS_STAT_ROWS = 0, 1, 2, 3, 4
 RLKS_EPLOG_CAP = 128
@@ -115,6 +115,7 @@ SIGNATURES = {
     "rlks_ppo_grad_phases": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _I, _P],
     "rlks_adam_step": [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _I, _P],
     "rlks_kl_update": [_P, _P, _F, _P],
+    "rlks_sf_f1_split": [],
 }
 _RESTYPES = {"rlks_last_error": C.c_char_p, "rlks_version": C.c_char_p}
 

@@ -85,6 +85,16 @@ def main():
         for i, name in enumerate(PHASES):
             print(f"  {name:18s} median {np.median(dt[:, i]):8.0f}  p90 {np.percentile(dt[:, i], 90):8.0f}"
                   f"  share {np.median(dt[:, i]) / np.median(tot):.2f}")
+    fn = getattr(_lib.lib(), "rlks_dbg_sf_stamps2", None)
+    if fn is not None:
+        st2 = np.zeros((2, 4096, 8), np.uint64)
+        assert fn(st2.ctypes.data_as(C.c_void_p)) == 0
+        for net in range(2):
+            s = st2[net, :tiles].astype(np.int64)
+            print(f"net {net} loop internals (one step): Z2 MFMA steps {np.median(s[:, 1] - s[:, 0]):.0f}, "
+                  f"chunk store {np.median(s[:, 2] - s[:, 1]):.0f}, barrier {np.median(s[:, 3] - s[:, 2]):.0f}; "
+                  f"dH1 MFMA steps {np.median(s[:, 5] - s[:, 4]):.0f}, chunk store {np.median(s[:, 6] - s[:, 5]):.0f}, "
+                  f"barrier {np.median(s[:, 7] - s[:, 6]):.0f}")
 
 
 if __name__ == "__main__":
