@@ -103,6 +103,9 @@ def env_setup(name):
 ROOFLINE_KERNELS = ("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1", "k_sf_fwdbwd", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2",
                     "wide_grad")
 ENV_BYTES_PER_STEP = 4 + 8 + 24 + 4 + 1  # action, step r/w, obs, reward, done
+# what the 2-cloud step kernel must move per env-step: action 4, step r/w 8, episode 4 (Philox
+# counter), obs 24, reward 8 (the reference's float64), terminated 1
+ENV_STEP_BYTES = 4 + 8 + 4 + 24 + 8 + 1
 GAE_BYTES_PER_STEP = 17                  # r, V, done in; A, vtarg out
 
 
@@ -206,22 +209,35 @@ def kernel_timing(algo, torch, config="c2", reps=20):
         out["k_node_step_c3"] = node_env_timing(algo, torch, timed)
     if config not in ("c2", "c4"):
         return out
-    # the standalone env step kernel at a size where HBM, not launch latency, bounds it
+    # the standalone env step kernel at a size where HBM, not launch latency, bounds it: the plain
+    # gymnasium step contract (trusted actions, no episode-return bookkeeping) through the ABI on
+    # preallocated buffers, and VecK8sMultiCloudEnv.step as a whole (status memset + k_validate +
+    # step with episode returns, info["step"] and final observations)
     from rlks import VecK8sMultiCloudEnv
 
     big = 1 << 24
-    venv = VecK8sMultiCloudEnv(big, table=algo.table, seed=1, device=algo.device)
-    venv.reset()
-    acts = torch.randint(0, 2, (big,), dtype=torch.int32, device=algo.device)
-    ms = timed(lambda: venv.step(acts), n=10)
-    alg = ENV_BYTES_PER_STEP * big / (ms * 1e-3) / 1e9
-    # bytes the kernel actually moves per lane: action 4, step 4+4, episode 4, ep_ret 8+8,
-    # obs 24, reward f64 8, terminated 1, truncated 1, step_out 4
-    moved = 70 * big / (ms * 1e-3) / 1e9
-    out["k_env_step_16M"] = {"ms": ms, "lanes": big, "GBps_algorithmic": alg, "frac_hbm": alg / HBM_PEAK_GBS,
-                             "GBps_moved": moved, "env_steps_per_s": big / (ms * 1e-3)}
-    venv.close()
-    del venv, acts
+    res = {"lanes": big}
+    for track in (False, True):
+        venv = VecK8sMultiCloudEnv(big, table=algo.table, seed=1, device=algo.device, track_returns=track)
+        venv.reset()
+        acts = torch.randint(0, 2, (big,), dtype=torch.int32, device=algo.device)
+        if not track:
+            ms = timed(lambda: _lib.call("rlks_env_step", venv.handle, acts.data_ptr(), venv.obs.data_ptr(),
+                                         venv.reward.data_ptr(), None, venv.terminated.data_ptr(), None, None,
+                                         venv.final_obs.data_ptr(), None, s.cuda_stream), n=20)
+            alg = ENV_STEP_BYTES * big / (ms * 1e-3) / 1e9
+            res.update({"ms": ms, "kernel": "k_env_step2", "bytes_per_step": ENV_STEP_BYTES,
+                        "GBps": alg, "frac_hbm": alg / HBM_PEAK_GBS, "env_steps_per_s": big / (ms * 1e-3),
+                        "GBps_survey_bytes": ENV_BYTES_PER_STEP * big / (ms * 1e-3) / 1e9})
+        else:
+            ms = timed(lambda: venv.step(acts), n=10)
+            # + ep_ret 8 + 8, step_out 4, the validation pass's action read 4
+            moved = ENV_STEP_BYTES + 24
+            res["vecenv_step"] = {"ms": ms, "bytes_per_step": moved,
+                                  "GBps": moved * big / (ms * 1e-3) / 1e9, "env_steps_per_s": big / (ms * 1e-3)}
+        venv.close()
+        del venv, acts
+    out["k_env_step_16M"] = res
     out["k_node_step_c3"] = node_env_timing(algo, torch, timed)
     out["k_node_step_c3_churn"] = node_env_timing(algo, torch, timed, depart_prob=0.02)
     return out

@@ -44,7 +44,8 @@ typedef struct rlks_env_cfg {
   int32_t noise_mode;    /* RLKS_NOISE_* */
   int32_t autoreset;     /* 1: terminated lanes reset inside step (vector-env semantics) */
   int32_t env_offset;    /* global id of lane 0 (multi-GPU shard base; Philox counter word 0) */
-  int32_t reserved0;
+  int32_t skip_returns;  /* 1: no episode-return bookkeeping in the step (ep_ret / ret_sum / ep_cnt /
+                            episode log untouched): the plain gymnasium step contract */
   uint64_t seed;         /* Philox key; also the default MT seed when none is given */
   double cpu_lo;         /* random.uniform(0.1, 0.8) (:87) */
   double cpu_hi;

@@ -29,7 +29,7 @@ _lib = None
 class EnvCfg(C.Structure):  # mirror of rlks_env_cfg (include/rlks_types.h)
     _fields_ = [
         ("n_envs", C.c_int32), ("n_rows", C.c_int32), ("n_clouds", C.c_int32), ("max_steps", C.c_int32),
-        ("noise_mode", C.c_int32), ("autoreset", C.c_int32), ("env_offset", C.c_int32), ("reserved0", C.c_int32),
+        ("noise_mode", C.c_int32), ("autoreset", C.c_int32), ("env_offset", C.c_int32), ("skip_returns", C.c_int32),
         ("seed", C.c_uint64), ("cpu_lo", C.c_double), ("cpu_hi", C.c_double), ("w_cost", C.c_double),
         ("w_lat", C.c_double), ("scale", C.c_double),
         ("nodes_per_cluster", C.c_int32), ("pod_cpu_m", C.c_int32), ("pod_mem_mi", C.c_int32),

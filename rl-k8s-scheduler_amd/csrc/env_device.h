@@ -50,7 +50,7 @@ constexpr int ENV_BLOCK = 256;
 constexpr int MAX_TABLE_BYTES = 128 * 1024;  // LDS budget for the staged tables (gfx950: 160 KB per workgroup)
 
 struct EnvView {
-  int N, T, C, max_steps, noise_mode, autoreset, env_offset;
+  int N, T, C, max_steps, noise_mode, autoreset, env_offset, track_returns;
   uint32_t k0, k1;
   double cpu_lo, span, w_cost, w_lat, scale;
   int32_t* step;
@@ -79,6 +79,7 @@ inline EnvView view(const rlks_env* e) {
   EnvView v;
   v.N = e->cfg.n_envs; v.T = e->cfg.n_rows; v.C = e->cfg.n_clouds; v.max_steps = e->cfg.max_steps;
   v.noise_mode = e->cfg.noise_mode; v.autoreset = e->cfg.autoreset; v.env_offset = e->cfg.env_offset;
+  v.track_returns = e->cfg.skip_returns ? 0 : 1;
   v.k0 = (uint32_t)e->cfg.seed; v.k1 = (uint32_t)(e->cfg.seed >> 32);
   v.cpu_lo = e->cfg.cpu_lo; v.span = e->span; v.w_cost = e->cfg.w_cost; v.w_lat = e->cfg.w_lat;
   v.scale = e->cfg.scale;
@@ -210,6 +211,18 @@ __device__ __forceinline__ void emit_obs(const EnvView& v, const double* s_tab, 
   }
 }
 
+// episode return bookkeeping (PPO result episode_reward_mean)
+__device__ __forceinline__ void track_return(const EnvView& v, int lane, int ep, double reward, bool done) {
+  double ret = v.ep_ret[lane] + reward;
+  if (done) {
+    v.ret_sum[lane] += ret;
+    v.ep_cnt[lane] += 1;
+    eplog_append(v, lane, ep, ret);
+    ret = 0.0;
+  }
+  v.ep_ret[lane] = ret;
+}
+
 struct StepOut {
   double reward;
   int step;
@@ -241,15 +254,7 @@ __device__ __forceinline__ StepOut step_lane(const EnvView& v, const double* s_t
     return r;
   }
   emit_obs(v, s_tab, lane, t, ep, o);
-  // episode return bookkeeping (PPO result episode_reward_mean)
-  double ret = v.ep_ret[lane] + r.reward;
-  if (r.done) {
-    v.ret_sum[lane] += ret;
-    v.ep_cnt[lane] += 1;
-    eplog_append(v, lane, ep, ret);
-    ret = 0.0;
-  }
-  v.ep_ret[lane] = ret;
+  if (v.track_returns) track_return(v, lane, ep, r.reward, r.done);
   if (r.done && v.autoreset) {
     const int D = 3 * C;
     if (final_o)

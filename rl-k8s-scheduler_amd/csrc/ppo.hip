@@ -163,19 +163,59 @@ struct GatherArgs {
   float* mb;
 };
 
-// one thread per record element (row i = e / stride, field j): the record stores are fully
-// coalesced and each row's fields are read contiguously; the row's permuted source index is
-// recomputed per element (a few dozen ALU ops against a scattered 4-byte load).  Rows
-// [k rows_g, (k+1) rows_g) come from lane group k: its permutation p -> (t = p / Ng, lane
-// k Ng + p mod Ng).
+// source index t * N + n of minibatch row i: rows [k rows_g, (k+1) rows_g) come from lane group
+// k, whose permutation p -> (t = p / Ng, lane k Ng + p mod Ng)
+__device__ __forceinline__ int64_t gather_src(const GatherArgs& g, uint32_t i) {
+  const uint32_t k = i / (uint32_t)g.rows_g, ii = i - k * (uint32_t)g.rows_g;
+  const uint64_t p = perm_apply(g.perm[k], (uint64_t)(g.row0g + ii));
+  uint64_t t, nl;
+  if (p >> 32) {
+    t = p / (uint64_t)g.Ng;
+    nl = p - t * (uint64_t)g.Ng;
+  } else {  // 32-bit division (every train batch below 2^32 rows per group)
+    const uint32_t t32 = (uint32_t)p / (uint32_t)g.Ng;
+    t = t32;
+    nl = (uint32_t)p - t32 * (uint32_t)g.Ng;
+  }
+  return (int64_t)(t * (uint64_t)g.b.N + (uint64_t)k * g.Ng + nl);
+}
+
+// narrow records (stride 12 / 20 / 36: 2, 4 or 8 clouds): one thread per row computes the row's permuted source
+// once, loads its fields (obs and logits contiguous, four scalars) and writes the record as
+// 16-byte stores; consecutive threads write consecutive records
+template <int S>
+__global__ __launch_bounds__(256) void k_gather_rows(GatherArgs g) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint32_t)g.rows) return;
+  const int64_t tn = gather_src(g, i);
+  const int D = g.D, A = g.A;
+  float rec[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    float v = 0.f;
+    if (j < D) v = g.b.obs[tn * D + j];
+    else if (j < D + A) v = g.b.logits[tn * A + (j - D)];
+    else if (j == D + A) v = g.b.adv[tn];
+    else if (j == D + A + 1) v = g.b.vtarg[tn];
+    else if (j == D + A + 2) v = g.b.logp[tn];
+    else if (j == D + A + 3) v = (float)g.b.actions[tn];
+    rec[j] = v;
+  }
+  float4* dst = reinterpret_cast<float4*>(g.mb + (size_t)i * S);
+#pragma unroll
+  for (int q = 0; q < S / 4; ++q) {
+    dst[q] = make_float4(rec[4 * q], rec[4 * q + 1], rec[4 * q + 2], rec[4 * q + 3]);
+  }
+}
+
+// wide records: one thread per record element (row i = e / stride, field j), so the record
+// stores are fully coalesced and each row's fields are read contiguously; the row's permuted
+// source index is recomputed per element
 __global__ void k_gather(GatherArgs g) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (uint32_t)g.rows * (uint32_t)g.stride) return;
   const uint32_t i = e / (uint32_t)g.stride, j = e - i * (uint32_t)g.stride;
-  const uint32_t k = i / (uint32_t)g.rows_g, ii = i - k * (uint32_t)g.rows_g;
-  const uint64_t p = perm_apply(g.perm[k], (uint64_t)(g.row0g + ii));
-  const uint64_t t = p / (uint64_t)g.Ng, nl = p - t * (uint64_t)g.Ng;
-  const int64_t tn = (int64_t)(t * (uint64_t)g.b.N + (uint64_t)k * g.Ng + nl);  // = t * N + n
+  const int64_t tn = gather_src(g, i);
   const int D = g.D, A = g.A;
   float v = 0.f;
   if ((int)j < D) v = g.b.obs[tn * D + j];
@@ -265,7 +305,10 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   const int KD = sf_kd(D), tiles = M / 32;
   w.blocks = M / (32 * SF_F1_W);  // F1 workgroups of SF_F1_W x 32 rows
   w.splits = 1;
-  while (w.splits * 2 <= 128 && tiles % (w.splits * 2) == 0) w.splits *= 2;
+#ifndef RLKS_F2_MAX_SPLITS
+#define RLKS_F2_MAX_SPLITS 128
+#endif
+  while (w.splits * 2 <= RLKS_F2_MAX_SPLITS && tiles % (w.splits * 2) == 0) w.splits *= 2;
   w.tiles_per_split = tiles > 0 ? tiles / w.splits : 0;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -459,7 +502,12 @@ int rlks_ppo_gather_grouped(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, 
   g.mb = mb;
   RLKS_REQUIRE((int64_t)rows * g.stride < (int64_t)1 << 31, RLKS_ERR_UNSUPPORTED,
                "rlks_ppo_gather: at most 2^31 record elements per call");
-  hipLaunchKernelGGL(k_gather, dim3(cdiv(rows * g.stride, 256)), dim3(256), 0, (hipStream_t)stream, g);
+  const dim3 rg(cdiv(rows, 256));
+  if (g.stride == 12) hipLaunchKernelGGL(k_gather_rows<12>, rg, dim3(256), 0, (hipStream_t)stream, g);
+  else if (g.stride == 20) hipLaunchKernelGGL(k_gather_rows<20>, rg, dim3(256), 0, (hipStream_t)stream, g);
+  else if (g.stride == 36) hipLaunchKernelGGL(k_gather_rows<36>, rg, dim3(256), 0, (hipStream_t)stream, g);
+  else
+    hipLaunchKernelGGL(k_gather, dim3(cdiv(rows * g.stride, 256)), dim3(256), 0, (hipStream_t)stream, g);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }

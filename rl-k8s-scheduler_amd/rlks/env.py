@@ -65,9 +65,10 @@ def seed_key_words(seed: int) -> list:
 
 
 def make_cfg(n_envs, table, *, noise="philox", seed=0, autoreset=True, env_offset=0, max_steps=None,
-             nodes=None):
+             nodes=None, track_returns=True):
     """rlks_env_cfg for `n_envs` lanes over `table`; `nodes` (a NodeSpec) enables the node-level
-    extension"""
+    extension; track_returns=False drops the per-lane episode-return bookkeeping
+    (episode_stats / episode_log stay empty) and leaves the plain gymnasium step"""
     cfg = _lib.EnvCfg()
     cfg.n_envs = int(n_envs)
     cfg.n_rows = table.n_rows
@@ -76,6 +77,7 @@ def make_cfg(n_envs, table, *, noise="philox", seed=0, autoreset=True, env_offse
     cfg.noise_mode = _lib.RLKS_NOISE_MT19937 if noise == "mt19937" else _lib.RLKS_NOISE_PHILOX
     cfg.autoreset = int(bool(autoreset))
     cfg.env_offset = int(env_offset)
+    cfg.skip_returns = 0 if track_returns else 1
     cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     cfg.cpu_lo, cfg.cpu_hi = 0.1, 0.8          # random.uniform(0.1, 0.8) (:87)
     cfg.w_cost, cfg.w_lat, cfg.scale = 0.6, 0.4, 100.0  # 100 * (0.6*cost + 0.4*latency) (:122)
@@ -348,7 +350,7 @@ class VecK8sMultiCloudEnv:
     """
 
     def __init__(self, num_envs, *, table=None, seed=0, noise="philox", autoreset=True, env_offset=0,
-                 device=None, data_path=None, nodes: NodeSpec | None = None):
+                 device=None, data_path=None, nodes: NodeSpec | None = None, track_returns=True):
         torch = _torch()
         self.table = table if table is not None else load_table(data_path)
         self.nodes = nodes
@@ -359,7 +361,7 @@ class VecK8sMultiCloudEnv:
         self.observation_space = Box(0.0, 1.0, (self.obs_dim,), np.float32)
         self.max_steps = self.table.n_rows - 1
         self.cfg = make_cfg(num_envs, self.table, noise=noise, seed=seed, autoreset=autoreset, env_offset=env_offset,
-                            nodes=nodes)
+                            nodes=nodes, track_returns=track_returns)
         self.dev = DeviceEnv(self.cfg, self.table, device, nodes)
         d = self.dev.device
         self.device = d
@@ -368,7 +370,7 @@ class VecK8sMultiCloudEnv:
         self.obs = torch.zeros(N, self.obs_dim, dtype=torch.float32, device=d)
         self.reward = torch.zeros(N, dtype=torch.float64, device=d)
         self.terminated = torch.zeros(N, dtype=torch.uint8, device=d)
-        self.truncated = torch.zeros(N, dtype=torch.uint8, device=d)
+        self.truncated = torch.zeros(N, dtype=torch.uint8, device=d)  # TimeLimit(100) never fires: stays 0
         self.steps = torch.zeros(N, dtype=torch.int32, device=d)
         self.final_obs = torch.zeros(N, self.obs_dim, dtype=torch.float32, device=d)
         self._stats = torch.zeros(2, dtype=torch.float64, device=d)
@@ -402,7 +404,7 @@ class VecK8sMultiCloudEnv:
         torch = _torch()
         a = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
         _lib.call("rlks_env_step", self.handle, _lib.ptr(a), _lib.ptr(self.obs), _lib.ptr(self.reward), None,
-                  _lib.ptr(self.terminated), _lib.ptr(self.truncated), _lib.ptr(self.steps),
+                  _lib.ptr(self.terminated), None, _lib.ptr(self.steps),
                   _lib.ptr(self.final_obs), _lib.ptr(self._status), self.dev.stream)
         return self.obs, self.reward, self.terminated, self.truncated, {"step": self.steps,
                                                                          "final_observation": self.final_obs,

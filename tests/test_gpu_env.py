@@ -166,6 +166,37 @@ def test_vec_env_matches_oracle(golden_cost_lat, noise, n, steps):
     venv.check_status()
 
 
+def test_lean_step_contract_matches_oracle(golden_cost_lat):
+    """the plain gymnasium step (k_env_step2 through the ABI with trusted actions, no truncated /
+    step / status outputs, no episode-return bookkeeping) is bit-exact vs the C oracle, including
+    final observations of auto-reset lanes, and leaves the episode accumulators empty"""
+    from rlks import VecK8sMultiCloudEnv, _lib
+
+    d = _dev()
+    cost, lat = golden_cost_lat
+    n, steps = 4099, 230  # a ragged last workgroup; two auto-resets per lane
+    venv = VecK8sMultiCloudEnv(n, seed=77, env_offset=5, device=d, track_returns=False)
+    ora = oracle.OracleEnv(oracle.make_cfg(n, 100, 2, noise_mode=0, seed=77, autoreset=1, env_offset=5), cost, lat)
+    np.testing.assert_array_equal(venv.reset().cpu().numpy().view(np.uint32), ora.reset().view(np.uint32))
+    rng = np.random.default_rng(11)
+    stream = torch.cuda.current_stream(d).cuda_stream
+    for _ in range(steps):
+        a = rng.integers(0, 2, n).astype(np.int32)
+        acts = torch.from_numpy(a).to(d)
+        _lib.call("rlks_env_step", venv.handle, acts.data_ptr(), venv.obs.data_ptr(), venv.reward.data_ptr(), None,
+                  venv.terminated.data_ptr(), None, None, venv.final_obs.data_ptr(), None, stream)
+        eo, er, et, es, ef, st = ora.step(a)
+        np.testing.assert_array_equal(venv.obs.cpu().numpy().view(np.uint32), eo.view(np.uint32))
+        np.testing.assert_array_equal(venv.reward.cpu().numpy().view(np.uint64), er.view(np.uint64))
+        np.testing.assert_array_equal(venv.terminated.cpu().numpy(), et)
+        tm = et.astype(bool)
+        np.testing.assert_array_equal(venv.final_obs.cpu().numpy()[tm].view(np.uint32), ef[tm].view(np.uint32))
+    steps_now, eps_now = venv.lane_state()
+    assert int(eps_now.min()) == int(eps_now.max()) and bool((steps_now == steps - 2 * 99).all())
+    s = venv.episode_stats(clear=True).cpu().numpy()
+    assert s[0] == 0.0 and s[1] == 0.0
+
+
 def test_vec_env_invalid_action_steps_nothing():
     from rlks import VecK8sMultiCloudEnv
 

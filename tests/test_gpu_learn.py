@@ -34,8 +34,12 @@ def close(x, ref, rtol=1e-5):
 
 
 # ----------------------------------------------------------------------------- GAE
-@pytest.mark.parametrize("T,N,gamma,lam", [(128, 4096, 0.99, 1.0), (64, 1000, 0.995, 0.95), (17, 5, 0.9, 0.0)])
+@pytest.mark.parametrize("T,N,gamma,lam", [(128, 4096, 0.99, 1.0), (64, 1000, 0.995, 0.95), (17, 5, 0.9, 0.0),
+                                           (256, 333, 0.99, 1.0), (200, 65, 0.99, 0.9), (1, 40, 0.99, 1.0),
+                                           (300, 70, 0.99, 1.0), (4000, 1, 0.99, 1.0), (128, 131072, 0.99, 1.0)])
 def test_gae_matches_oracle(T, N, gamma, lam):
+    """reverse-scan GAE (T <= 256: 8 / 16-step segments, partial last segment, ragged lane groups)
+    and the serial recurrence (T > 256, c1's 4,000-step single lane) vs the float64 oracle"""
     from rlks import _lib
 
     d = _dev()
@@ -243,36 +247,48 @@ def test_adam_matches_torch():
     np.testing.assert_allclose(pt.cpu().numpy(), ep, rtol=2.5e-7, atol=1e-5 * 3e-4)
 
 
-def test_gather_is_a_permutation_per_epoch():
+@pytest.mark.parametrize("D,A,T,N", [(6, 2, 128, 4096), (12, 4, 16, 1024), (24, 8, 8, 2048), (192, 64, 4, 512)])
+def test_gather_is_a_permutation_per_epoch(D, A, T, N):
+    """every epoch's minibatches are a permutation of the train batch, and every record holds its
+    source sample's fields (obs, logits, adv, vtarg, logp, action, zero padding) — the row-parallel
+    gather (records of 12 / 20 / 36 floats) and the element-parallel one (wide records)"""
     from rlks import _lib
-    from rlks.policy import PolicyParams
 
     d = _dev()
-    T, N = 128, 4096
     S = T * N
+    g = torch.Generator(device=d).manual_seed(D)
     f32 = dict(dtype=torch.float32, device=d)
-    bufs_t = {"obs": torch.zeros(T + 1, N, 6, **f32), "logits": torch.zeros(T, N, 2, **f32),
-              "values": torch.zeros(T + 1, N, **f32), "actions": torch.zeros(T, N, dtype=torch.int32, device=d),
-              "logp": torch.zeros(T, N, **f32), "rewards": torch.zeros(T, N, **f32),
-              "dones": torch.zeros(T, N, dtype=torch.uint8, device=d),
-              "adv": torch.arange(S, dtype=torch.float64, device=d).float().view(T, N), "vtarg": torch.zeros(T, N, **f32)}
-    bufs_t["vtarg"].copy_(torch.arange(S, device=d).view(T, N).float().remainder(4096))
-    b = bufs_t
+    b = {"obs": torch.rand(T + 1, N, D, generator=g, **f32), "logits": torch.randn(T, N, A, generator=g, **f32),
+         "values": torch.zeros(T + 1, N, **f32),
+         "actions": torch.randint(0, A, (T, N), generator=g, dtype=torch.int32, device=d),
+         "logp": torch.randn(T, N, generator=g, **f32), "rewards": torch.zeros(T, N, **f32),
+         "dones": torch.zeros(T, N, dtype=torch.uint8, device=d),
+         "adv": torch.arange(S, dtype=torch.float64, device=d).float().view(T, N),
+         "vtarg": torch.randn(T, N, generator=g, **f32)}
     rb = _lib.RolloutBufs(*[b[k].data_ptr() for k in ("obs", "logits", "values", "actions", "logp", "rewards",
                                                        "dones", "adv", "vtarg")], T, N)
-    desc = _lib.MlpDesc(6, 256, 2, 0)
+    desc = _lib.MlpDesc(D, 256, A, 0)
     stride = _lib.lib().rlks_minibatch_stride(C.byref(desc))
     dyn = torch.tensor([0, 1, 0.2, 1, 0, 0, 0, 0], **f32)
     out = torch.zeros(S, stride, **f32)
+    mb = min(S, 65536)
     seen = []
     for epoch in range(2):
-        for row0 in range(0, S, 65536):
-            _lib.call("rlks_ppo_gather", C.byref(desc), C.byref(rb), 77, epoch, row0, 65536, dyn.data_ptr(),
+        out.fill_(-7.0)
+        for row0 in range(0, S, mb):
+            _lib.call("rlks_ppo_gather", C.byref(desc), C.byref(rb), 77, epoch, row0, mb, dyn.data_ptr(),
                       out[row0:].data_ptr(), None)
-        idx = out[:, 8].double()
+        idx = out[:, D + A].double()
         # adv column carries the sample id (exact in fp32 below 2^24)
         assert torch.equal(torch.sort(idx).values, torch.arange(S, dtype=torch.float64, device=d))
         seen.append(idx.clone())
+        t, n = idx.long() // N, idx.long() % N
+        assert torch.equal(out[:, :D], b["obs"][t, n])
+        assert torch.equal(out[:, D:D + A], b["logits"][t, n])
+        assert torch.equal(out[:, D + A + 1], b["vtarg"][t, n])
+        assert torch.equal(out[:, D + A + 2], b["logp"][t, n])
+        assert torch.equal(out[:, D + A + 3], b["actions"][t, n].float())
+        assert bool((out[:, D + A + 4:] == 0).all())
     assert not torch.equal(seen[0], seen[1])
 
 
