@@ -183,6 +183,24 @@ def kernel_timing(algo, torch, config="c2", reps=20):
                                  algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None,
                                  algo.ws.data_ptr(), algo.ws.numel(), s.cuda_stream), n=reps if H <= 256 else 3)
     out["sgd_grad_total"] = {"ms": ms}
+    # the per-SGD-step minibatch gather (a new epoch's permutation on every call, so that the
+    # rows are not cache-resident from the previous call) and the once-per-iteration record pack
+    ep = [100]
+
+    def gather():
+        ep[0] += 1
+        if algo.packed is not None:
+            _lib.call("rlks_ppo_gather_packed", desc, algo.packed.data_ptr(), algo.T, algo.N, 1, ep[0], 1, 0, 0,
+                      algo.mb, algo.mbuf.data_ptr(), s.cuda_stream)
+        else:
+            _lib.call("rlks_ppo_gather", desc, C.byref(algo.bufs), 1, ep[0], 0, algo.mb, algo.dyn.data_ptr(),
+                      algo.mbuf.data_ptr(), s.cuda_stream)
+
+    out["k_gather" if algo.packed is None else "k_gather_packed"] = {"ms": timed(gather), "rows": algo.mb}
+    if algo.packed is not None:
+        out["k_pack"] = {"ms": timed(lambda: _lib.call("rlks_ppo_pack", desc, C.byref(algo.bufs),
+                                                       algo.packed.data_ptr(), s.cuda_stream), n=5),
+                         "samples": algo.T * algo.N}
     if algo.precision == "wide":
         tf = flops_per_row("wide_grad", D, H, A) * algo.mb / (ms * 1e-3) / 1e12
         out["wide_grad"] = {"ms": ms, "tflops": tf, peak_name: tf / peak, "frac_fp32_mfma_peak": tf / FP32_MFMA_PEAK_TFLOPS}

@@ -211,6 +211,15 @@ int rlks_ppo_gather(const rlks_mlp_desc* desc, const rlks_rollout_bufs* bufs, ui
 int rlks_ppo_gather_grouped(const rlks_mlp_desc* desc, const rlks_rollout_bufs* bufs, uint64_t perm_seed,
                             int epoch, int groups, int group0, int64_t row0, int rows, const float* dyn_dev,
                             float* mb_dev, void* stream);
+/* Floats per sample record of rlks_ppo_pack: the minibatch record padded to a 64-byte multiple
+ * (16 / 32 / 48 for obs 6 / 12 / 24); 0 for shapes the packed path does not cover. */
+int rlks_packed_stride(const rlks_mlp_desc* desc);
+/* The rollout's T*N samples as records [T*N][rlks_packed_stride] in rollout order (after GAE):
+ * one aligned record per sample, so that each minibatch row is one random line read. */
+int rlks_ppo_pack(const rlks_mlp_desc* desc, const rlks_rollout_bufs* bufs, float* packed_dev, void* stream);
+/* rlks_ppo_gather_grouped from packed records: the same rows, permutation and record bytes. */
+int rlks_ppo_gather_packed(const rlks_mlp_desc* desc, const float* packed_dev, int T, int N, uint64_t perm_seed,
+                           int epoch, int groups, int group0, int64_t row0, int rows, float* mb_dev, void* stream);
 
 /* Gradient of the RLlib PPO loss (mean over `rows`*world rows via dyn[INV_COUNT]) w.r.t. the
  * flat parameters -> grad_dev (padded_count floats).  stats_dev (double[RLKS_STAT_SIZE]) gets

@@ -161,6 +161,8 @@ struct GatherArgs {
   int64_t row0g;          // first row of this minibatch within each group's permutation
   int rows, rows_g, Ng, D, A, stride;
   float* mb;
+  const float* packed;    // rlks_ppo_pack records [T N][pstride] (gather_packed), else null
+  int pstride;
 };
 
 // source index t * N + n of minibatch row i: rows [k rows_g, (k+1) rows_g) come from lane group
@@ -225,6 +227,48 @@ __global__ void k_gather(GatherArgs g) {
   else if ((int)j == D + A + 2) v = g.b.logp[tn];
   else if ((int)j == D + A + 3) v = (float)g.b.actions[tn];
   g.mb[(size_t)e] = v;
+}
+
+// Sample records in rollout order, one 64-byte-aligned record per sample (c2 / c4: exactly one
+// 64-byte line), so that a minibatch gather reads one line per row instead of one line from each
+// of the six rollout arrays (obs, logits, adv, vtarg, logp, action): one thread per sample, 16-byte
+// streaming stores.
+template <int PS>
+__global__ __launch_bounds__(256) void k_pack(rlks_rollout_bufs b, int D, int A, float* __restrict__ packed) {
+  constexpr int TPR = PS / 4;  // threads per record, thread q writes floats [4q, 4q + 4)
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tn = e / TPR;
+  const int q = (int)(e % TPR);
+  if (tn >= (int64_t)b.T * b.N) return;
+  float rec[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int j = 4 * q + c;
+    float v = 0.f;
+    if (j < D) v = b.obs[tn * D + j];
+    else if (j < D + A) v = b.logits[tn * A + (j - D)];
+    else if (j == D + A) v = b.adv[tn];
+    else if (j == D + A + 1) v = b.vtarg[tn];
+    else if (j == D + A + 2) v = b.logp[tn];
+    else if (j == D + A + 3) v = (float)b.actions[tn];
+    rec[c] = v;
+  }
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(f32x4{rec[0], rec[1], rec[2], rec[3]}, reinterpret_cast<f32x4*>(packed + tn * PS) + q);
+}
+
+// minibatch rows from packed records: PS / 4 consecutive threads per row, thread q moving the
+// record's 16-byte piece q, so that every load instruction reads whole 64-byte lines (one line
+// per row for PS = 16) and the stores are contiguous
+template <int S, int PS>
+__global__ __launch_bounds__(256) void k_gather_packed(GatherArgs g) {
+  constexpr int TPR = PS / 4;
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = e / TPR, q = e % TPR;
+  if (i >= (uint32_t)g.rows) return;
+  const int64_t tn = gather_src(g, i);
+  const float4 v = reinterpret_cast<const float4*>(g.packed + tn * PS)[q];
+  if (4 * q < (uint32_t)S) reinterpret_cast<float4*>(g.mb + (size_t)i * S)[q] = v;
 }
 
 static Perm make_perm(uint64_t seed, int epoch, uint64_t S) {
@@ -474,20 +518,15 @@ int rlks_ppo_gather(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, uint64_t
   return rlks_ppo_gather_grouped(d, b, perm_seed, epoch, 1, 0, row0, rows, dyn, mb, stream);
 }
 
-int rlks_ppo_gather_grouped(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, uint64_t perm_seed, int epoch,
-                            int groups, int group0, int64_t row0, int rows, const float* dyn, float* mb,
-                            void* stream) {
-  RLKS_REQUIRE(d && b && mb && rows >= 0, RLKS_ERR_ARG, "rlks_ppo_gather: bad argument");
-  RLKS_REQUIRE(groups >= 1 && groups <= MAX_GROUPS && group0 >= 0 && b->N % groups == 0 && rows % groups == 0 &&
+static int gather_args(const rlks_mlp_desc* d, int T, int N, uint64_t perm_seed, int epoch, int groups, int group0,
+                       int64_t row0, int rows, float* mb, GatherArgs& g) {
+  RLKS_REQUIRE(groups >= 1 && groups <= MAX_GROUPS && group0 >= 0 && N % groups == 0 && rows % groups == 0 &&
                    row0 % groups == 0, RLKS_ERR_ARG,
                "rlks_ppo_gather: groups must divide the lanes, the rows and row0 (at most 64 groups)");
-  (void)dyn;  // advantages are standardised inside the loss kernel from dyn
-  const int Ng = b->N / groups;
-  const uint64_t Sg = (uint64_t)b->T * (uint64_t)Ng;
+  const int Ng = N / groups;
+  const uint64_t Sg = (uint64_t)T * (uint64_t)Ng;
   RLKS_REQUIRE(row0 >= 0 && (uint64_t)(row0 + rows) / groups <= Sg, RLKS_ERR_ARG, "rlks_ppo_gather: rows out of range");
-  if (rows == 0) return RLKS_OK;
-  GatherArgs g{};
-  g.b = *b;
+  g = GatherArgs{};
   // group k's key: perm_seed for global group 0 (the single-group gather), else perm_seed offset by
   // an odd 64-bit multiple of the global group id
   for (int k = 0; k < groups; ++k)
@@ -502,12 +541,66 @@ int rlks_ppo_gather_grouped(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, 
   g.mb = mb;
   RLKS_REQUIRE((int64_t)rows * g.stride < (int64_t)1 << 31, RLKS_ERR_UNSUPPORTED,
                "rlks_ppo_gather: at most 2^31 record elements per call");
+  return RLKS_OK;
+}
+
+int rlks_ppo_gather_grouped(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, uint64_t perm_seed, int epoch,
+                            int groups, int group0, int64_t row0, int rows, const float* dyn, float* mb,
+                            void* stream) {
+  RLKS_REQUIRE(d && b && mb && rows >= 0, RLKS_ERR_ARG, "rlks_ppo_gather: bad argument");
+  (void)dyn;  // advantages are standardised inside the loss kernel from dyn
+  GatherArgs g;
+  if (int rc = gather_args(d, b->T, b->N, perm_seed, epoch, groups, group0, row0, rows, mb, g)) return rc;
+  if (rows == 0) return RLKS_OK;
+  g.b = *b;
   const dim3 rg(cdiv(rows, 256));
   if (g.stride == 12) hipLaunchKernelGGL(k_gather_rows<12>, rg, dim3(256), 0, (hipStream_t)stream, g);
   else if (g.stride == 20) hipLaunchKernelGGL(k_gather_rows<20>, rg, dim3(256), 0, (hipStream_t)stream, g);
   else if (g.stride == 36) hipLaunchKernelGGL(k_gather_rows<36>, rg, dim3(256), 0, (hipStream_t)stream, g);
   else
     hipLaunchKernelGGL(k_gather, dim3(cdiv(rows * g.stride, 256)), dim3(256), 0, (hipStream_t)stream, g);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_packed_stride(const rlks_mlp_desc* d) {
+  if (!d) return 0;
+  const int s = mb_stride(d->obs_dim, d->n_actions);
+  return s == 12 ? 16 : s == 20 ? 32 : s == 36 ? 48 : 0;
+}
+
+int rlks_ppo_pack(const rlks_mlp_desc* d, const rlks_rollout_bufs* b, float* packed, void* stream) {
+  RLKS_REQUIRE(d && b && packed && b->T > 0 && b->N > 0, RLKS_ERR_ARG, "rlks_ppo_pack: bad argument");
+  const int ps = rlks_packed_stride(d);
+  RLKS_REQUIRE(ps > 0, RLKS_ERR_UNSUPPORTED, "rlks_ppo_pack: records of 2, 4 or 8 clouds (obs 6 / 12 / 24) only");
+  const int64_t n = (int64_t)b->T * b->N;
+  const dim3 grid(cdiv(n * (ps / 4), 256));
+  hipStream_t s = (hipStream_t)stream;
+  const int D = d->obs_dim, A = d->n_actions;
+  if (ps == 16) hipLaunchKernelGGL(k_pack<16>, grid, dim3(256), 0, s, *b, D, A, packed);
+  else if (ps == 32) hipLaunchKernelGGL(k_pack<32>, grid, dim3(256), 0, s, *b, D, A, packed);
+  else hipLaunchKernelGGL(k_pack<48>, grid, dim3(256), 0, s, *b, D, A, packed);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_ppo_gather_packed(const rlks_mlp_desc* d, const float* packed, int T, int N, uint64_t perm_seed, int epoch,
+                           int groups, int group0, int64_t row0, int rows, float* mb, void* stream) {
+  RLKS_REQUIRE(d && packed && mb && rows >= 0 && T > 0 && N > 0, RLKS_ERR_ARG, "rlks_ppo_gather_packed: bad argument");
+  const int ps = rlks_packed_stride(d);
+  RLKS_REQUIRE(ps > 0, RLKS_ERR_UNSUPPORTED, "rlks_ppo_gather_packed: records of 2, 4 or 8 clouds only");
+  GatherArgs g;
+  if (int rc = gather_args(d, T, N, perm_seed, epoch, groups, group0, row0, rows, mb, g)) return rc;
+  if (rows == 0) return RLKS_OK;
+  g.b.T = T;
+  g.b.N = N;
+  g.packed = packed;
+  g.pstride = ps;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 rg(cdiv((int64_t)rows * ps / 4, 256));
+  if (g.stride == 12) hipLaunchKernelGGL((k_gather_packed<12, 16>), rg, dim3(256), 0, s, g);
+  else if (g.stride == 20) hipLaunchKernelGGL((k_gather_packed<20, 32>), rg, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((k_gather_packed<36, 48>), rg, dim3(256), 0, s, g);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }

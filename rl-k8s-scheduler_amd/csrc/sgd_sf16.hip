@@ -29,6 +29,7 @@
 // mlp_fwd.hip (train_ppo.py:9-31; RLlib third-party).
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "sgd_sf16.h"
 
@@ -38,6 +39,9 @@ using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
 using v4u = __attribute__((ext_vector_type(4))) unsigned;  // 16-byte staging register (a vector, not HIP's uint4 struct, so it stays in VGPRs)
 
+#ifndef RLKS_F2_PHASES
+#define RLKS_F2_PHASES 1
+#endif
 constexpr int SF_ROWS = 256;        // minibatch rows must be a multiple of this
 constexpr int SF_CH = 8192;         // halves per staged chunk (per hi / lo array)
 constexpr float SF_H1_SCALE = 16384.f;  // tanh outputs (|h| < 1) scaled by 2^14
@@ -1275,11 +1279,18 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   load_x(t0);
   h1(t0 + 1 < t1 ? t0 + 1 : t0, bh, bl);
   __syncthreads();
-  for (int t = t0; t < t1; ++t) {
+  // Waves 4-7 share SIMDs with waves 0-3 (wave i runs on SIMD i mod 4) and run the same step
+  // with the VALU blocks moved (H1 first, the tile split late): the two waves of a SIMD are then
+  // in complementary phases between barriers, and one's VALU issues under the other's MFMAs.
+  auto step = [&](auto PH, int t) {
+    constexpr int ph = decltype(PH)::value;
+    constexpr int NT_STORE = ph ? 5 : 1, NT_LOAD = ph ? 6 : 3, NT_H1 = ph ? -1 : 4;
     const int buf = (t - t0) & 1;
     const bool more = t + 1 < t1;
     const _Float16* b = sA + buf * 2 * SF_CH;
     h8 nbh[2], nbl[2];
+    const int th = t + 2 < t1 ? t + 2 : t + 1 < t1 ? t + 1 : t;
+    if (NT_H1 < 0) h1(th, nbh, nbl);  // tile t + 1's H1
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
       const int n = 32 * nt + r;
@@ -1290,14 +1301,20 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
         const h8 al = *reinterpret_cast<const h8*>(b + SF_CH + off);
         acc[nt] = mma3(ah, al, bh[s], bl[s], acc[nt]);
       }
-      if (nt == 1 && more) store(buf ^ 1);                     // tile t + 1 -> other buffer
-      if (nt == 3 && t + 2 < t1) load(t + 2);                   // tile t + 2 -> registers
-      if (nt == 4) h1(t + 2 < t1 ? t + 2 : t + 1 < t1 ? t + 1 : t, nbh, nbl);  // tile t + 1's H1
+      if (nt == NT_STORE && more) store(buf ^ 1);              // tile t + 1 -> other buffer
+      if (nt == NT_LOAD && t + 2 < t1) load(t + 2);            // tile t + 2 -> registers
+      if (nt == NT_H1) h1(th, nbh, nbl);                       // tile t + 1's H1
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) { bh[s] = nbh[s]; bl[s] = nbl[s]; }
     __syncthreads();
-  }
+  };
+#if RLKS_F2_PHASES
+  if (w & 4)
+    for (int t = t0; t < t1; ++t) step(std::integral_constant<int, 1>{}, t);
+  else
+#endif
+    for (int t = t0; t < t1; ++t) step(std::integral_constant<int, 0>{}, t);
   float* out = N.part_w2 + (size_t)blockIdx.x * HID * HID;
 #ifdef RLKS_F2_NOSTORE  // timing experiment only: the partials are not written
   if (acc[0][0] != 12345.f) return;

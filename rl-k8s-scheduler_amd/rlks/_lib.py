@@ -110,6 +110,9 @@ SIGNATURES = {
     "rlks_ppo_gather": [C.POINTER(MlpDesc), C.POINTER(RolloutBufs), C.c_uint64, _I, _I64, _I, _P, _P, _P],
     "rlks_ppo_gather_grouped": [C.POINTER(MlpDesc), C.POINTER(RolloutBufs), C.c_uint64, _I, _I, _I, _I64, _I, _P,
                                 _P, _P],
+    "rlks_packed_stride": [C.POINTER(MlpDesc)],
+    "rlks_ppo_pack": [C.POINTER(MlpDesc), C.POINTER(RolloutBufs), _P, _P],
+    "rlks_ppo_gather_packed": [C.POINTER(MlpDesc), _P, _I, _I, C.c_uint64, _I, _I, _I, _I64, _I, _P, _P],
     "rlks_ppo_workspace_bytes": [C.POINTER(MlpDesc), _I, C.POINTER(_I64)],
     "rlks_ppo_grad": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _P],
     "rlks_ppo_grad_phases": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _I, _P],

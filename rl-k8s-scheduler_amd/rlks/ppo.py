@@ -283,6 +283,10 @@ class PPO:
                                          b["dones"].data_ptr(), b["adv"].data_ptr(), b["vtarg"].data_ptr(), T, N)
             self.stride = _lib.lib().rlks_minibatch_stride(C.byref(self.params.desc))
             self.mbuf = torch.zeros(self.mb, self.stride, **f32)
+            # one aligned record per sample (rlks_ppo_pack after GAE): a minibatch row is then one
+            # random line read instead of six (2 / 4 / 8 clouds; the wide path gathers directly)
+            ps = _lib.lib().rlks_packed_stride(C.byref(self.params.desc))
+            self.packed = torch.empty(T * N, ps, **f32) if ps else None
             # one workspace for the SGD step and the rollout (split weights; wide: N-row activations)
             wsb, wsr = C.c_int64(), C.c_int64()
             _lib.call("rlks_ppo_workspace_bytes", C.byref(self.params.desc), self.mb, C.byref(wsb))
@@ -338,6 +342,8 @@ class PPO:
                   _lib.ptr(self.adv_sums), s)
         self._allreduce(self.adv_sums)
         _lib.call("rlks_adv_finalize", _lib.ptr(self.adv_sums), _lib.ptr(self.dyn), s)
+        if self.packed is not None:
+            _lib.call("rlks_ppo_pack", C.byref(self.params.desc), C.byref(self.bufs), _lib.ptr(self.packed), s)
 
     def perm_seed(self, iteration=None):
         """key of this iteration's minibatch permutations (resumes with the iteration counter)"""
@@ -347,8 +353,12 @@ class PPO:
     def sgd_step(self, epoch, b, stat_row):
         s = self.stream
         desc = C.byref(self.params.desc)
-        _lib.call("rlks_ppo_gather_grouped", desc, C.byref(self.bufs), self.perm_seed(), epoch, self.groups,
-                  self.group0, b * self.mb, self.mb, _lib.ptr(self.dyn), _lib.ptr(self.mbuf), s)
+        if self.packed is not None:
+            _lib.call("rlks_ppo_gather_packed", desc, _lib.ptr(self.packed), self.T, self.N, self.perm_seed(), epoch,
+                      self.groups, self.group0, b * self.mb, self.mb, _lib.ptr(self.mbuf), s)
+        else:
+            _lib.call("rlks_ppo_gather_grouped", desc, C.byref(self.bufs), self.perm_seed(), epoch, self.groups,
+                      self.group0, b * self.mb, self.mb, _lib.ptr(self.dyn), _lib.ptr(self.mbuf), s)
         _lib.call("rlks_ppo_grad", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat), _lib.ptr(self.dyn),
                   _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row), _lib.ptr(self.ws),
                   self.ws.numel(), s)

@@ -292,6 +292,43 @@ def test_gather_is_a_permutation_per_epoch(D, A, T, N):
     assert not torch.equal(seen[0], seen[1])
 
 
+@pytest.mark.parametrize("D,A,T,N,groups", [(6, 2, 128, 4096, 1), (6, 2, 16, 1024, 4), (12, 4, 16, 1024, 2),
+                                             (24, 8, 8, 2048, 1)])
+def test_packed_gather_equals_direct_gather(D, A, T, N, groups):
+    """rlks_ppo_pack + rlks_ppo_gather_packed writes exactly the records of rlks_ppo_gather_grouped
+    (same permutation per lane group, same fields), bit for bit"""
+    from rlks import _lib
+
+    d = _dev()
+    S = T * N
+    g = torch.Generator(device=d).manual_seed(D + groups)
+    f32 = dict(dtype=torch.float32, device=d)
+    b = {"obs": torch.randn(T + 1, N, D, generator=g, **f32), "logits": torch.randn(T, N, A, generator=g, **f32),
+         "values": torch.zeros(T + 1, N, **f32),
+         "actions": torch.randint(0, A, (T, N), generator=g, dtype=torch.int32, device=d),
+         "logp": torch.randn(T, N, generator=g, **f32), "rewards": torch.zeros(T, N, **f32),
+         "dones": torch.zeros(T, N, dtype=torch.uint8, device=d), "adv": torch.randn(T, N, generator=g, **f32),
+         "vtarg": torch.randn(T, N, generator=g, **f32)}
+    rb = _lib.RolloutBufs(*[b[k].data_ptr() for k in ("obs", "logits", "values", "actions", "logp", "rewards",
+                                                       "dones", "adv", "vtarg")], T, N)
+    desc = _lib.MlpDesc(D, 256, A, 0)
+    stride = _lib.lib().rlks_minibatch_stride(C.byref(desc))
+    ps = _lib.lib().rlks_packed_stride(C.byref(desc))
+    assert ps % 16 == 0 and ps >= stride
+    packed = torch.full((S, ps), -3.0, **f32)
+    _lib.call("rlks_ppo_pack", C.byref(desc), C.byref(rb), packed.data_ptr(), None)
+    rows = min(S, 8192)
+    ref = torch.zeros(rows, stride, **f32)
+    got = torch.full((rows, stride), -5.0, **f32)
+    for epoch, row0 in ((0, 0), (3, rows), (9, S - rows)):
+        _lib.call("rlks_ppo_gather_grouped", C.byref(desc), C.byref(rb), 1234, epoch, groups, 1, row0, rows, None,
+                  ref.data_ptr(), None)
+        _lib.call("rlks_ppo_gather_packed", C.byref(desc), packed.data_ptr(), T, N, 1234, epoch, groups, 1, row0,
+                  rows, got.data_ptr(), None)
+        assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+    assert bool((packed[:, stride:] == 0).all())
+
+
 # ----------------------------------------------------------------------------- end to end
 def test_ppo_iteration_parity_and_surface(tmp_path):
     """one iteration at the c2 size (4,096 lanes x 128 steps): the fused rollout's env transitions
