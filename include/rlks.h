@@ -252,6 +252,16 @@ int rlks_sf_f1_split(void);
 /* torch.optim.Adam step (lerp form of exp_avg, bias-corrected), in place on n floats */
 int rlks_adam_step(float* params_dev, const float* grad_dev, float* m_dev, float* v_dev, int64_t n,
                    float lr, float beta1, float beta2, float eps, int step, void* stream);
+/* One SGD step on one rank: the PPO gradient of the minibatch (as rlks_ppo_grad; `grad` still
+ * receives it) with Adam (as rlks_adam_step, step `step`) applied inside the gradient reduction,
+ * which also leaves the new weights' max |w| for the next step's operand split (prev_fused = 1 on
+ * the step after a fused one: the weight-max pass is skipped, with a device-side check that falls
+ * back to scanning the weights).  Replaces rlks_ppo_grad + rlks_adam_step when no gradient
+ * all-reduce sits between them; other precisions run exactly those two calls. */
+int rlks_ppo_sgd_step(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, float* params_dev,
+                      const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
+                      float* adam_m_dev, float* adam_v_dev, int64_t n_params, float lr, float beta1, float beta2,
+                      float eps, int step, int prev_fused, void* workspace, int64_t ws_bytes, void* stream);
 
 /* RLlib update_kl: kl = stats_sum[0] / stats_sum[1]; x1.5 if kl > 2*target, x0.5 if < target/2 */
 int rlks_kl_update(float* dyn_dev, const double* kl_sum_count_dev, float kl_target, void* stream);

@@ -24,13 +24,41 @@ struct RedTask {
   int64_t pstride;
   int P, len, G, V;
   int blk0;
+  int mslot;         // fused Adam: -1, or the max |w| slot (net * 2 + 0: W2, + 1: W1a) of the output
+  int mbase;         // first entry of this task's blocks in the slot
 };
 constexpr int MAX_TASKS = 20;
+// torch.optim.Adam (single-tensor path) on element i: exp_avg.lerp_(g, 1-b1); exp_avg_sq =
+// b2*v + (1-b2)*g*g; p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps).  Shared by
+// k_adam and the fused reduce so that both paths compute the same bits.
+struct AdamCo {
+  float w1, b2, omb2, step_size, bc2_sqrt, eps;
+};
+__device__ __forceinline__ float adam_elem(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                           int64_t i, float gi, const AdamCo& c) {
+  const float mi = m[i] + c.w1 * (gi - m[i]);
+  const float vi = c.b2 * v[i] + c.omb2 * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / c.bc2_sqrt + c.eps;
+  const float pn = p[i] - c.step_size * (mi / denom);
+  p[i] = pn;
+  return pn;
+}
+
 struct RedArgs {
   RedTask t[MAX_TASKS];
   int ntasks;
   double* stats;     // optional: stats[4] = rows, stats[5..7] = 0 (the sums come from tasks)
   double rows;
+  // fused Adam (p != null): every parameter-gradient output element is also applied to its
+  // parameter (index = out - grad), and the new |w| maxima of W2 / W1a go to the split's slots
+  float *p, *m, *v;
+  const float* grad;
+  AdamCo co;
+  float* slot[4];     // [net * 2 + 0] W2, [net * 2 + 1] W1a: per-block max entries (task mbase + block)
+  unsigned* tag[2];   // set to tag_val: the slots hold the maxima of Adam step tag_val
+  unsigned tag_val;
 };
 
 __global__ __launch_bounds__(256) void k_reduce(RedArgs g) {
@@ -54,34 +82,77 @@ __global__ __launch_bounds__(256) void k_reduce(RedArgs g) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) sh[j][threadIdx.x] = s[j];
   __syncthreads();
+  float wmax = 0.f;
   if (grp == 0) {
-    for (int j = 0; j < T.V; ++j) {
-      const int i = T.V * iv + j;
-      if (i >= T.len) break;
-      double t = 0.0;
-      for (int q = 0; q < T.G; ++q) t += sh[j][q * opb + o];
-      if (T.out64) T.out64[i] = t;
-      else T.out[i] = (float)t;
+    double t[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < T.V; ++j)
+      for (int q = 0; q < T.G; ++q) t[j] += sh[j][q * opb + o];
+    const int i0 = T.V * iv;
+    if (T.out64) {
+      for (int j = 0; j < T.V && i0 + j < T.len; ++j) T.out64[i0 + j] = t[j];
+    } else if (T.V == 4 && i0 + 3 < T.len) {
+      const float4 gv = make_float4((float)t[0], (float)t[1], (float)t[2], (float)t[3]);
+      *reinterpret_cast<float4*>(T.out + i0) = gv;
+      if (g.p) {  // Adam on the four parameters (16-byte aligned: tensors start on 64-float boundaries)
+        const int64_t pi = (T.out - g.grad) + i0;
+        float4 pv = *reinterpret_cast<const float4*>(g.p + pi), mv = *reinterpret_cast<const float4*>(g.m + pi),
+               vv = *reinterpret_cast<const float4*>(g.v + pi);
+        float* pp = &pv.x; float* mm = &mv.x; float* vq = &vv.x;
+        const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          wmax = fmaxf(wmax, fabsf(adam_elem(pp, mm, vq, j, gg[j], g.co)));
+        }
+        *reinterpret_cast<float4*>(g.p + pi) = pv;
+        *reinterpret_cast<float4*>(g.m + pi) = mv;
+        *reinterpret_cast<float4*>(g.v + pi) = vv;
+      }
+    } else {
+      for (int j = 0; j < T.V && i0 + j < T.len; ++j) {
+        T.out[i0 + j] = (float)t[j];
+        if (g.p) wmax = fmaxf(wmax, fabsf(adam_elem(g.p, g.m, g.v, (T.out - g.grad) + i0 + j, (float)t[j], g.co)));
+      }
     }
+  }
+  if (g.p && T.mslot >= 0) {  // block-uniform: this block's max |w_new| -> the slot
+    __shared__ float smax[4];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, off, 64));
+    if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = wmax;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      g.slot[T.mslot][T.mbase + (int)blockIdx.x - T.blk0] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
   }
   if (g.stats && blockIdx.x == 0 && threadIdx.x == 0) {
     g.stats[RLKS_STAT_ROWS] = g.rows;
     g.stats[5] = g.stats[6] = g.stats[7] = 0.0;
+  }
+  if (g.p && blockIdx.x == 0 && threadIdx.x == 0) {
+    *g.tag[0] = g.tag_val;
+    *g.tag[1] = g.tag_val;
   }
 }
 
 struct Reducer {
   RedArgs a{};
   int blocks = 0;
-  void add(const float* part, float* out, double* out64, int64_t pstride, int P, int len) {
+  int mnext[4] = {0, 0, 0, 0};  // next free entry per max slot
+  void add(const float* part, float* out, double* out64, int64_t pstride, int P, int len, int mslot = -1) {
     RedTask& t = a.t[a.ntasks++];
+    t.mslot = mslot;
+    t.mbase = 0;
     int G = 1;
     while (G < 256 && G * 16 < P) G *= 2;
     const bool vec = len % 4 == 0 && pstride % 4 == 0 && ((uintptr_t)part & 15) == 0;
     t.part = part; t.out = out; t.out64 = out64; t.pstride = pstride; t.P = P; t.len = len; t.G = G;
     t.V = vec ? 4 : 1;
     t.blk0 = blocks;
-    blocks += (int)cdiv(cdiv(len, t.V), 256 / G);
+    const int nb = (int)cdiv(cdiv(len, t.V), 256 / G);
+    blocks += nb;
+    if (mslot >= 0) {
+      t.mbase = mnext[mslot];
+      mnext[mslot] += nb;
+    }
   }
 };
 
@@ -101,17 +172,10 @@ __global__ void k_stats_finish(double* __restrict__ st, const double* __restrict
 // torch.optim.Adam (single-tensor path): exp_avg.lerp_(g, 1-b1); exp_avg_sq = b2*v + (1-b2)*g*g;
 // p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                       float* __restrict__ v, int64_t n, float w1, float b2, float omb2, float step_size,
-                       float bc2_sqrt, float eps) {
+                       float* __restrict__ v, int64_t n, AdamCo co) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float gi = g[i];
-  const float mi = m[i] + w1 * (gi - m[i]);
-  const float vi = b2 * v[i] + omb2 * gi * gi;
-  m[i] = mi;
-  v[i] = vi;
-  const float denom = sqrtf(vi) / bc2_sqrt + eps;
-  p[i] = p[i] - step_size * (mi / denom);
+  (void)adam_elem(p, m, v, i, g[i], co);
 }
 
 // RLlib PPO update_kl
@@ -340,6 +404,7 @@ struct SfWs {
   SfNetW w[2];
   SfNet n[2];
   double* stat64;
+  float* pmax_roll[2];  // the rollout's weight-max slots (the SGD steps' pmax keeps its parity state)
   int64_t bytes, weight_bytes;
   int blocks, splits, tiles_per_split;
 };
@@ -373,7 +438,9 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     W.w2rh = (_Float16*)take(2LL * HID * HID);
     W.w2rl = (_Float16*)take(2LL * HID * HID);
     W.sc = (float*)take(4 * 8);
-    W.pmax = (float*)take(4 * 32);
+    W.pmax = (float*)take(4LL * 4 * SF_PMAX);
+    W.tag = (unsigned*)take(4 * 2);
+    w.pmax_roll[net] = (float*)take(4LL * 4 * SF_PMAX);
     W.dzmax = (unsigned*)take(4);
     n.w1h = W.w1h; n.w1l = W.w1l; n.w2ph = W.w2ph; n.w2pl = W.w2pl; n.w2th = W.w2th; n.w2tl = W.w2tl;
     n.sc = W.sc; n.dzmax = W.dzmax;
@@ -397,14 +464,23 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   return w;
 }
 
-static int sf_prep(const rlks_mlp_desc* d, const SfWs& w, const float* params, hipStream_t s) {
+// Weight splits for the split-fp16 kernels.  rollout: also the rollout's fragment-order copy of W2,
+// with the max |w| slots of its own.  SGD step: `parity` selects the max slots (see SfPrepArgs);
+// skip_wmax when the previous fused SGD step left this step's maxima there.
+static int sf_prep(const rlks_mlp_desc* d, const SfWs& w, const float* params, hipStream_t s, bool rollout,
+                   int parity = 0, bool skip_wmax = false, unsigned expect_tag = 0) {
   const int D = d->obs_dim;
   const Layout L = make_layout(D, HID, d->n_actions);
   SfPrepArgs pa{};
   pa.D = D;
   pa.KD = sf_kd(D);
+  pa.parity = rollout ? 0 : parity;
+  pa.skip_wmax = rollout ? 0 : (skip_wmax ? 1 : 0);
+  pa.write_roll = rollout ? 1 : 0;
+  pa.expect_tag = expect_tag;
   for (int net = 0; net < 2; ++net) {
     pa.n[net] = w.w[net];
+    if (rollout) pa.n[net].pmax = w.pmax_roll[net];
     const NetPtrs P = net_ptrs_host(params, L, net);
     pa.n[net].w1 = P.w1; pa.n[net].b1 = P.b1; pa.n[net].w2 = P.w2;
   }
@@ -439,7 +515,7 @@ static int node_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* para
   const Layout L = make_layout(D, HID, A);
   SfRollArgs r{};
   if (w) {
-    if (int rc = sf_prep(d, *w, params, s)) return rc;
+    if (int rc = sf_prep(d, *w, params, s, true)) return rc;
     for (int net = 0; net < 2; ++net) {
       const NetPtrs P = net_ptrs_host(params, L, net);
       r.n[net] = SfRollNet{w->w[net].w1h, w->w[net].w1l, w->w[net].w2rh, w->w[net].w2rl, P.b2, P.w3, P.b3, w->w[net].sc};
@@ -635,17 +711,29 @@ int rlks_ppo_workspace_bytes(const rlks_mlp_desc* d, int rows, int64_t* bytes) {
   return RLKS_OK;
 }
 
+// SGD step with Adam fused into the gradient reduction (single rank: no gradient all-reduce between
+// them).  step: the Adam step performed (1-based); prev_fused: the previous SGD step on these
+// parameters was fused, so its reduce left this step's weight maxima in the split's slots.
+struct FusedAdam {
+  float *p, *m, *v;
+  AdamCo co;
+  int step, prev_fused;
+};
+
 static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
                    const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes, int phases,
-                   hipStream_t s) {
+                   hipStream_t s, const FusedAdam* fa = nullptr) {
   RLKS_REQUIRE(M > 0 && M % 256 == 0, RLKS_ERR_ARG, "rlks_ppo_grad: split-fp16 rows must be a positive multiple of 256");
   const int D = d->obs_dim, A = d->n_actions, H = HID;
   const SfWs w = sf_ws_layout(D, A, M, (char*)workspace);
   RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_ppo_grad: workspace too small");
   const Layout L = make_layout(D, H, A);
   const bool f_pi = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_PI), f_vf = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_VF);
-  if (phases & (RLKS_PHASE_FWD | RLKS_PHASE_PREP))
-    if (int rc = sf_prep(d, w, params, s)) return rc;
+  if (phases & (RLKS_PHASE_FWD | RLKS_PHASE_PREP)) {
+    const int parity = fa ? ((fa->step - 1) & 1) : 0;
+    if (int rc = sf_prep(d, w, params, s, false, parity, fa && fa->prev_fused, fa ? (unsigned)fa->step : 0u))
+      return rc;
+  }
   SfArgs a{};
   a.x = mb; a.x_stride = mb_stride(D, A); a.M = M; a.D = D; a.A_pi = A;
   a.tiles_per_split = w.tiles_per_split; a.co = *co; a.dyn = dyn;
@@ -669,9 +757,9 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     const int An = net == 0 ? A : 1;
     const int64_t* o = L.off + 6 * net;
     const SfNet& n = w.n[net];
-    R.add(n.part_w1, grad + o[0], nullptr, (int64_t)H * D, w.blocks, H * D);
-    R.add(n.part_b1, grad + o[1], nullptr, H, w.blocks, H);
-    R.add(n.part_w2, grad + o[2], nullptr, (int64_t)H * H, w.splits, H * H);
+    R.add(n.part_w1, grad + o[0], nullptr, (int64_t)H * D, w.blocks, H * D, 2 * net + 1);
+    R.add(n.part_b1, grad + o[1], nullptr, H, w.blocks, H, 2 * net + 1);
+    R.add(n.part_w2, grad + o[2], nullptr, (int64_t)H * H, w.splits, H * H, 2 * net);
     R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
     R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, M / 32, An * H);
     R.add(n.part_b3, grad + o[5], nullptr, An, M / 32, An);
@@ -684,6 +772,21 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     R.add(w.n[0].part_stat + 3, nullptr, stats + RLKS_STAT_ENTROPY, 4, tiles, 1);
     R.a.stats = stats;
     R.a.rows = (double)M;
+  }
+  if (fa) {  // Adam on every parameter as its gradient is summed; W2 / W1a maxima -> the next prep
+    for (int k = 0; k < 4; ++k)
+      RLKS_REQUIRE(R.mnext[k] <= SF_PMAX, RLKS_ERR_UNSUPPORTED, "rlks_ppo_sgd_step: too many reduce blocks per weight");
+    R.a.p = fa->p; R.a.m = fa->m; R.a.v = fa->v; R.a.grad = grad; R.a.co = fa->co;
+    const int par = fa->step & 1;
+    for (int net = 0; net < 2; ++net) {
+      R.a.slot[2 * net] = w.w[net].pmax + (par * 2 + 0) * SF_PMAX;
+      R.a.slot[2 * net + 1] = w.w[net].pmax + (par * 2 + 1) * SF_PMAX;
+    }
+    // the slots are complete when the reduce is (the next prep is a later launch): mark them as
+    // this step's
+    R.a.tag[0] = w.w[0].tag + par;
+    R.a.tag[1] = w.w[1].tag + par;
+    R.a.tag_val = (unsigned)fa->step + 1u;  // tag of step s = s + 1 (0: none), expected by step s + 1's prep
   }
   hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
   RLKS_LAUNCHED();
@@ -776,16 +879,36 @@ int rlks_ppo_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float
 
 int rlks_sf_f1_split(void) { return sf_f1_split() ? 1 : 0; }
 
+static AdamCo adam_co(float lr, float beta1, float beta2, float eps, int step) {
+  const double bc1 = 1.0 - std::pow((double)beta1, step);
+  const double bc2 = 1.0 - std::pow((double)beta2, step);
+  return AdamCo{1.f - beta1, beta2, 1.f - beta2, (float)(lr / bc1), (float)std::sqrt(bc2), eps};
+}
+
 int rlks_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                    float eps, int step, void* stream) {
   RLKS_REQUIRE(p && g && m && v && n >= 0 && step >= 1, RLKS_ERR_ARG, "rlks_adam_step: bad argument");
   if (n == 0) return RLKS_OK;
-  const double bc1 = 1.0 - std::pow((double)beta1, step);
-  const double bc2 = 1.0 - std::pow((double)beta2, step);
-  hipLaunchKernelGGL(k_adam, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, 1.f - beta1,
-                     beta2, 1.f - beta2, (float)(lr / bc1), (float)std::sqrt(bc2), eps);
+  hipLaunchKernelGGL(k_adam, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                     adam_co(lr, beta1, beta2, eps, step));
   RLKS_LAUNCHED();
   return RLKS_OK;
+}
+
+int rlks_ppo_sgd_step(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, float* params, const float* dyn,
+                      const float* mb, int M, float* grad, double* stats, float* adam_m, float* adam_v, int64_t n_params,
+                      float lr, float beta1, float beta2, float eps, int step, int prev_fused, void* workspace,
+                      int64_t ws_bytes, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(co && params && dyn && mb && grad && adam_m && adam_v && workspace && step >= 1, RLKS_ERR_ARG,
+               "rlks_ppo_sgd_step: bad argument");
+  if (d->precision != RLKS_PRECISION_SF16 || is_wide(d)) {  // unfused: gradient, then Adam
+    if (int rc = rlks_ppo_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, stream)) return rc;
+    return rlks_adam_step(params, grad, adam_m, adam_v, n_params, lr, beta1, beta2, eps, step, stream);
+  }
+  FusedAdam fa{params, adam_m, adam_v, adam_co(lr, beta1, beta2, eps, step), step, prev_fused ? 1 : 0};
+  return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
+                 &fa);
 }
 
 int rlks_kl_update(float* dyn, const double* kc, float target, void* stream) {
@@ -860,7 +983,7 @@ int rlks_rollout_ws(rlks_env* env, const rlks_mlp_desc* d, const float* params, 
     RLKS_REQUIRE(cfg.autoreset, RLKS_ERR_ARG, "rlks_rollout_ws: node-level rollout needs autoreset lanes");
     return node_rollout(env, d, params, b, explore, &w, s);
   }
-  if (int rc = sf_prep(d, w, params, s)) return rc;
+  if (int rc = sf_prep(d, w, params, s, true)) return rc;
   const Layout L = make_layout(D, HID, A);
   SfRollArgs a{};
   for (int net = 0; net < 2; ++net) {

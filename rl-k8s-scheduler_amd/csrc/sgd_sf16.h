@@ -8,6 +8,7 @@ namespace rlks {
 #define RLKS_F1_W 4
 #endif
 constexpr int SF_F1_W = RLKS_F1_W;  // waves per F1 workgroup (one per SIMD); 32 rows each
+constexpr int SF_PMAX = 1024;       // weight-max entries per (parity, kind)
 }  // namespace rlks
 
 namespace rlks {
@@ -17,12 +18,20 @@ struct SfNetW {
   _Float16 *w1h, *w1l, *w2ph, *w2pl, *w2th, *w2tl;
   _Float16 *w2rh, *w2rl;  // rollout: w2p in wave-fragment order [q 4][kt 8][s 2][i 2][64 lanes][8]
   float* sc;          // [8]: s_w1, 1/s_w1, s_w2, 1/s_w2, e_w1, e_w2
-  float* pmax;        // [32] per-block max |w| (16 over W2, 16 over W1a)
+  float* pmax;        // [2 parity][2 kind: W2, W1a][SF_PMAX] per-block max |w| (k_sf_wmax: entries
+                      // 0..15 of each kind; the fused reduce: one entry per reduce block)
+  unsigned* tag;      // [2 parity]: the Adam step whose fused reduce filled pmax[parity] (0: none)
   unsigned* dzmax;    // zeroed here (F1 atomicMax)
 };
+// parity: which half of pmax holds this prep's maxima; the split zeroes the other half, which the
+// fused reduce + Adam of the coming SGD step fills (one entry per reduce block, no atomics) for the
+// next prep.  skip_wmax: the maxima are already there (the previous SGD step was fused).
 struct SfPrepArgs {
   SfNetW n[2];
   int D, KD;
+  int parity, skip_wmax, write_roll;
+  unsigned expect_tag;  // skip_wmax: pmax[parity] is valid only if tag[parity] == expect_tag; else
+                        // every split block scans the weights for their maxima itself
 };
 
 struct SfNet {

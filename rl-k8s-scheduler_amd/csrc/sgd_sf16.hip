@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void k_sf_wmax(SfPrepArgs g) {
     if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
     __syncthreads();
   }
-  if (tid == 0) N.pmax[b] = red[0];
+  if (tid == 0) N.pmax[(g.parity * 2 + (b < 16 ? 0 : 1)) * SF_PMAX + (b & 15)] = red[0];
 }
 
 // pass 2: grid (2 nets, 64 blocks) x 256 threads, 4 elements of W2 (both orders) per thread and
@@ -158,10 +158,47 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
   const SfNetW& N = g.n[blockIdx.x];
   const int D = g.D, KD = g.KD, tid = threadIdx.x;
   float m2 = 0.f, m1 = 0.f;
+  if (g.skip_wmax && N.tag[g.parity] != g.expect_tag) {  // stale slots: this block scans the weights
+    __shared__ float red[2][256];
+    for (int e = tid; e < HID * HID; e += 256) m2 = fmaxf(m2, fabsf(N.w2[e]));
+    for (int e = tid; e < HID * (D + 1); e += 256) {
+      const int k = e / (D + 1), d = e - k * (D + 1);
+      m1 = fmaxf(m1, fabsf(d < D ? N.w1[k * D + d] : N.b1[k]));
+    }
+    red[0][tid] = m2;
+    red[1][tid] = m1;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (tid < o) {
+        red[0][tid] = fmaxf(red[0][tid], red[0][tid + o]);
+        red[1][tid] = fmaxf(red[1][tid], red[1][tid + o]);
+      }
+      __syncthreads();
+    }
+    m2 = red[0][0];
+    m1 = red[1][0];
+  } else if (!g.skip_wmax) {  // k_sf_wmax's 16 block maxima per kind
+    const float* pm = N.pmax + g.parity * 2 * SF_PMAX;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    m2 = fmaxf(m2, N.pmax[i]);
-    m1 = fmaxf(m1, N.pmax[16 + i]);
+    for (int i = 0; i < 16; ++i) {
+      m2 = fmaxf(m2, pm[i]);
+      m1 = fmaxf(m1, pm[SF_PMAX + i]);
+    }
+  } else {  // the fused reduce's per-block maxima (unused entries are zero)
+    __shared__ float red2[2][4];
+    const float4* pm = reinterpret_cast<const float4*>(N.pmax + g.parity * 2 * SF_PMAX);
+    const float4 a = pm[tid], c = pm[SF_PMAX / 4 + tid];
+    m2 = fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w));
+    m1 = fmaxf(fmaxf(c.x, c.y), fmaxf(c.z, c.w));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
+      m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
+    }
+    if ((tid & 63) == 0) { red2[0][tid >> 6] = m2; red2[1][tid >> 6] = m1; }
+    __syncthreads();
+    m2 = fmaxf(fmaxf(red2[0][0], red2[0][1]), fmaxf(red2[0][2], red2[0][3]));
+    m1 = fmaxf(fmaxf(red2[1][0], red2[1][1]), fmaxf(red2[1][2], red2[1][3]));
   }
   const int e1 = sf_exp(m1), e2 = sf_exp(m2);
   const float s1 = pow2(e1), s2 = pow2(e2);
@@ -178,7 +215,7 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
     split1(N.w2[src * HID + row] * s2, a, b);  // w2t[k = row][n perm]
     N.w2th[i] = a;
     N.w2tl[i] = b;
-    if (N.w2rh) {  // rollout copy: i = ((((q 8 + kt) 2 + s) 2 + ii) 64 + lane) 8 + j -> w2p[n][32kt+16s+8h+j]
+    if (g.write_roll) {  // rollout copy: i = ((((q 8 + kt) 2 + s) 2 + ii) 64 + lane) 8 + j -> w2p[n][32kt+16s+8h+j]
       const int j = i & 7, lane = (i >> 3) & 63, ii = (i >> 9) & 1, ss = (i >> 10) & 1, kt = (i >> 11) & 7,
                 q = i >> 14;
       const int n = 32 * (2 * q + ii) + (lane & 31), kk = 32 * kt + 16 * ss + 8 * (lane >> 5) + j;
@@ -201,6 +238,11 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
     N.sc[2] = s2; N.sc[3] = 1.f / s2; N.sc[5] = (float)e2;
     *N.dzmax = 0u;
   }
+  if (blockIdx.y == 0) {  // the other parity's entries: the coming fused reduce writes some of them
+    float4* z = reinterpret_cast<float4*>(N.pmax + (g.parity ^ 1) * 2 * SF_PMAX);
+    for (int i = tid; i < 2 * SF_PMAX / 4; i += 256) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (blockIdx.y == 0 && tid == 0) N.tag[g.parity ^ 1] = 0u;
 }
 
 // ----------------------------------------------------------------------------- F1
@@ -1360,8 +1402,10 @@ bool sf_f1_split() {
 }
 
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_sf_wmax, dim3(2, 32), dim3(256), 0, s, a);
-  RLKS_LAUNCHED();
+  if (!a.skip_wmax) {
+    hipLaunchKernelGGL(k_sf_wmax, dim3(2, 32), dim3(256), 0, s, a);
+    RLKS_LAUNCHED();
+  }
   hipLaunchKernelGGL(k_sf_split, dim3(2, 64), dim3(256), 0, s, a);
   RLKS_LAUNCHED();
   return RLKS_OK;

@@ -307,6 +307,8 @@ class PPO:
         # they are obs[T] of the previous rollout (moved to obs[0] when the next one starts, so the
         # update can still read obs[0..T-1])
         self._carry = False
+        # the previous SGD step was a fused one on the current parameters (rlks_ppo_sgd_step)
+        self._fused_prev = False
         self._ep_history = collections.deque(maxlen=max(1, int(cfg.metrics_num_episodes_for_smoothing)))
         self.iteration = 0
         self.timesteps_total = 0
@@ -353,18 +355,26 @@ class PPO:
     def sgd_step(self, epoch, b, stat_row):
         s = self.stream
         desc = C.byref(self.params.desc)
+        beta1, beta2 = self.config.adam_betas
         if self.packed is not None:
             _lib.call("rlks_ppo_gather_packed", desc, _lib.ptr(self.packed), self.T, self.N, self.perm_seed(), epoch,
                       self.groups, self.group0, b * self.mb, self.mb, _lib.ptr(self.mbuf), s)
         else:
             _lib.call("rlks_ppo_gather_grouped", desc, C.byref(self.bufs), self.perm_seed(), epoch, self.groups,
                       self.group0, b * self.mb, self.mb, _lib.ptr(self.dyn), _lib.ptr(self.mbuf), s)
+        self.adam_step += 1
+        if self.world == 1:  # no all-reduce between gradient and Adam: one fused launch sequence
+            _lib.call("rlks_ppo_sgd_step", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat), _lib.ptr(self.dyn),
+                      _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row), _lib.ptr(self.adam_m),
+                      _lib.ptr(self.adam_v), self.params.padded, float(self.config.lr), float(beta1), float(beta2),
+                      float(self.config.adam_eps), self.adam_step, int(self._fused_prev), _lib.ptr(self.ws),
+                      self.ws.numel(), s)
+            self._fused_prev = True
+            return
         _lib.call("rlks_ppo_grad", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat), _lib.ptr(self.dyn),
                   _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row), _lib.ptr(self.ws),
                   self.ws.numel(), s)
         self._allreduce(self.grad)
-        self.adam_step += 1
-        beta1, beta2 = self.config.adam_betas
         _lib.call("rlks_adam_step", _lib.ptr(self.params.flat), _lib.ptr(self.grad), _lib.ptr(self.adam_m),
                   _lib.ptr(self.adam_v), self.params.padded, float(self.config.lr), float(beta1), float(beta2),
                   float(self.config.adam_eps), self.adam_step, s)
@@ -573,6 +583,7 @@ class PPO:
             if tuple(sd[k].shape) != tuple(v.shape):
                 raise ValueError(f"checkpoint tensor {k} has shape {tuple(sd[k].shape)}, this policy {tuple(v.shape)}")
         self.params.load_state_dict(sd)
+        self._fused_prev = False
         self.adam_m.copy_(tensors["adam_m"].to(self.device))
         self.adam_v.copy_(tensors["adam_v"].to(self.device))
         self.adam_step = int(meta["adam_step"])

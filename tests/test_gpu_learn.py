@@ -329,6 +329,55 @@ def test_packed_gather_equals_direct_gather(D, A, T, N, groups):
     assert bool((packed[:, stride:] == 0).all())
 
 
+@pytest.mark.parametrize("A", [2, 8])
+def test_fused_sgd_step_equals_grad_then_adam(A):
+    """rlks_ppo_sgd_step (Adam inside the gradient reduction, the next step's weight maxima from
+    its slots) gives the parameters, Adam moments and gradients of rlks_ppo_grad + rlks_adam_step,
+    bit for bit, over consecutive steps -- including a first step that claims prev_fused with no
+    fused predecessor (the device-side tag check falls back to scanning the weights)"""
+    from rlks import _lib
+    from rlks.policy import PolicyParams
+
+    d = _dev()
+    D, M = 3 * A, 2048
+    desc = _lib.MlpDesc(D, 256, A, _lib.RLKS_PRECISION_SF16)
+    stride = _lib.lib().rlks_minibatch_stride(C.byref(desc))
+    co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.0)
+    g = torch.Generator(device=d).manual_seed(A)
+    p_ref = PolicyParams(D, 256, A, device=d, seed=3)
+    p_fus = PolicyParams(D, 256, A, device=d, seed=3)
+    p_ref.desc.precision = p_fus.desc.precision = _lib.RLKS_PRECISION_SF16
+    P = p_ref.padded
+    dyn = torch.tensor([0.1, 1.3, 0.2, 1.0 / M, 0, 0, 0, 0], dtype=torch.float32, device=d)
+    wsb = C.c_int64()
+    _lib.call("rlks_ppo_workspace_bytes", C.byref(desc), M, C.byref(wsb))
+    ws_ref = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
+    ws_fus = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
+    st = {k: torch.zeros(P, device=d) for k in ("m_ref", "v_ref", "g_ref", "m_fus", "v_fus", "g_fus")}
+    stats_ref = torch.zeros(8, dtype=torch.float64, device=d)
+    stats_fus = torch.zeros(8, dtype=torch.float64, device=d)
+    for step in range(1, 6):
+        mb = torch.zeros(M, stride, device=d)
+        mb[:, :D] = torch.rand(M, D, generator=g, device=d)
+        mb[:, D:D + A] = torch.randn(M, A, generator=g, device=d)
+        mb[:, D + A] = torch.randn(M, generator=g, device=d)
+        mb[:, D + A + 1] = torch.randn(M, generator=g, device=d) * 30
+        mb[:, D + A + 2] = -torch.rand(M, generator=g, device=d) * 2
+        mb[:, D + A + 3] = torch.randint(0, A, (M,), generator=g, device=d).float()
+        _lib.call("rlks_ppo_grad", C.byref(desc), C.byref(co), p_ref.flat.data_ptr(), dyn.data_ptr(), mb.data_ptr(), M,
+                  st["g_ref"].data_ptr(), stats_ref.data_ptr(), ws_ref.data_ptr(), ws_ref.numel(), None)
+        _lib.call("rlks_adam_step", p_ref.flat.data_ptr(), st["g_ref"].data_ptr(), st["m_ref"].data_ptr(),
+                  st["v_ref"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, None)
+        _lib.call("rlks_ppo_sgd_step", C.byref(desc), C.byref(co), p_fus.flat.data_ptr(), dyn.data_ptr(),
+                  mb.data_ptr(), M, st["g_fus"].data_ptr(), stats_fus.data_ptr(), st["m_fus"].data_ptr(),
+                  st["v_fus"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, 1, ws_fus.data_ptr(), ws_fus.numel(),
+                  None)
+        for a, b in (("g_ref", "g_fus"), ("m_ref", "m_fus"), ("v_ref", "v_fus")):
+            assert torch.equal(st[a].view(torch.int32), st[b].view(torch.int32)), (step, a)
+        assert torch.equal(p_ref.flat.view(torch.int32), p_fus.flat.view(torch.int32)), step
+        assert torch.equal(stats_ref, stats_fus)
+
+
 # ----------------------------------------------------------------------------- end to end
 def test_ppo_iteration_parity_and_surface(tmp_path):
     """one iteration at the c2 size (4,096 lanes x 128 steps): the fused rollout's env transitions
