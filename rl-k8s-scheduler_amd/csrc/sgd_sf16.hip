@@ -39,6 +39,9 @@ using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
 using v4u = __attribute__((ext_vector_type(4))) unsigned;  // 16-byte staging register (a vector, not HIP's uint4 struct, so it stays in VGPRs)
 
+#ifndef RLKS_F1B_ONEPASS
+#define RLKS_F1B_ONEPASS 1
+#endif
 #ifndef RLKS_F2_PHASES
 #define RLKS_F2_PHASES 1
 #endif
@@ -1032,7 +1035,9 @@ __device__ __forceinline__ void sf_bwd_body(const SfArgs& g) {
   const int D = g.D, stride = g.x_stride;
   const int tile = blockIdx.x * W + w, row0 = tile * 32, blk = blockIdx.x;
 
+#if !RLKS_F1B_ONEPASS
   half_dma<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
+#endif
   float xv[KS * 8];
   const float* xr = g.x + (size_t)(row0 + r) * stride;
 #pragma unroll
@@ -1092,6 +1097,108 @@ __device__ __forceinline__ void sf_bwd_body(const SfArgs& g) {
   vm_drain();
   __syncthreads();
 
+#if RLKS_F1B_ONEPASS
+  // ---- one pass: the eight dH1 k-tile accumulators (AGPRs) over the 8 n-tiles; chunk nt = W2's
+  // w2t columns [32 nt, +32) of all 256 rows k ([256][32] hi / lo image), single-buffered through
+  // registers: a step computes from LDS while the next chunk and dZ2^T n-tile load into registers,
+  // then barrier / store / barrier.  Each dZ2^T element is read and split once.
+  {
+    f32x16 dh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dh[j][q] = 0.f;
+    v4u stg[32 / W];
+    float dzc[16], dzn[16];
+    chunk_load<W>(N, 8, w, l, stg);
+    dz_load(0, dzc);
+    vm_drain();
+    chunk_store<W>(sCh, w, l, stg);
+    __syncthreads();
+    for (int nt = 0; nt < 8; ++nt) {
+      if (nt < 7) {
+        chunk_load<W>(N, 9 + nt, w, l, stg);
+        dz_load(nt + 1, dzn);
+      }
+      h8 ah[2], al[2];
+      split8(dzc, 0, sdz, ah[0], al[0]);
+      split8(dzc, 8, sdz, ah[1], al[1]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        h8 fc[2][2];
+        sf_frag(sCh, 32 * j + r, h, fc);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          dh[j] = mma(al[s], fc[s][0], dh[j]);
+          dh[j] = mma(ah[s], fc[s][1], dh[j]);
+          dh[j] = mma(ah[s], fc[s][0], dh[j]);
+        }
+      }
+      __syncthreads();
+      if (nt < 7) {
+        vm_drain();
+        chunk_store<W>(sCh, w, l, stg);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dzc[q] = dzn[q];
+      }
+      __syncthreads();
+    }
+    // ---- dZ1 = dH1 (1 - H1^2) -> dW1a^T of the 8 k-tiles; sums over the W waves in the chunk
+    // buffer (free now), KPR k-tiles per round
+    constexpr int KT0 = 0, NKT = 8;
+#pragma unroll
+    for (int j = 0; j < NKT; ++j) {
+      const int kt = KT0 + j;
+      w1_frag(kt);
+      f32x16 z;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) z = mma3(xh[ks], xl[ks], wh[ks], wl[ks], z);
+      f32x16 dz;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float h1 = tanh_abs(z[q] * inv_z1);
+        dz[q] = dh[j][q] * (1.f - h1 * h1);
+      }
+      h8 zh[2], zl[2];
+      split16(dz, 0, sz1, zh[0], zl[0]);
+      split16(dz, 8, sz1, zh[1], zl[1]);
+      f32x16 wacc, wacc2;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) { wacc[q] = 0.f; wacc2[q] = 0.f; }
+      const h8 x0h = sXT[(w * 4 + 0) * 64 + l], x0l = sXT[(w * 4 + 1) * 64 + l];
+      const h8 x1h = sXT[(w * 4 + 2) * 64 + l], x1l = sXT[(w * 4 + 3) * 64 + l];
+      wacc = mma(x0l, zh[0], wacc);
+      wacc2 = mma(x1l, zh[1], wacc2);
+      wacc = mma(x0h, zl[0], wacc);
+      wacc2 = mma(x1h, zl[1], wacc2);
+      wacc = mma(x0h, zh[0], wacc);
+      wacc2 = mma(x1h, zh[1], wacc2);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) wacc[q] += wacc2[q];
+#pragma unroll
+      for (int gq = 0; gq < NG; ++gq) {
+        float4 v = {wacc[4 * gq] * u1, wacc[4 * gq + 1] * u1, wacc[4 * gq + 2] * u1, wacc[4 * gq + 3] * u1};
+        *reinterpret_cast<float4*>(sEp + (j % KPR) * SLOT + (w * 32 + r) * DWR + 8 * gq + 4 * h) = v;
+      }
+      if (j % KPR == KPR - 1) {
+        __syncthreads();
+        const int nd = D + 1, kt0 = kt + 1 - KPR;
+        for (int e = tid; e < KPR * 32 * nd; e += NTHR) {
+          const int jj = e / (32 * nd), e2 = e - jj * 32 * nd, kk = e2 / nd, d = e2 - kk * nd;
+          const int k = 32 * (kt0 + jj) + kk;
+          float sum = 0.f;
+#pragma unroll
+          for (int ww = 0; ww < W; ++ww) sum += sEp[jj * SLOT + (ww * 32 + kk) * DWR + d];
+          if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = sum;
+          else N.part_b1[(size_t)blk * HID + k] = sum;
+        }
+        __syncthreads();
+      }
+    }
+  }
+#else
   // ---- two passes over the k-halves p: dH1 k-tiles 4p .. 4p+3 accumulate over the 8 n-tiles
   // (24 MFMAs per n-tile step; half-chunks double-buffered), then their dZ1 and dW1a^T
 #pragma unroll 1
@@ -1188,6 +1295,8 @@ __device__ __forceinline__ void sf_bwd_body(const SfArgs& g) {
       __syncthreads();
     }
   }
+
+#endif
 }
 
 template <int KD, int NG, int W>
