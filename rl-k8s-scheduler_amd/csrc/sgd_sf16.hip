@@ -121,6 +121,22 @@ __device__ __forceinline__ float xa_elem(const float* __restrict__ xr, int d, in
   return fmaf(v, d < D ? 1.f : 0.f, d == D ? 1.f : 0.f);
 }
 
+// elements [base, base + 8) of Xa = [X | 1 | 0] for a record row xr of S floats (S a multiple of 4,
+// S >= D + 4, 16-byte aligned rows): two 16-byte loads and arithmetic selects.  A block that starts
+// past S - 8 lies entirely beyond the obs (base >= D + 1 for the record shapes used) and loads
+// the row's last 8 floats in its place so that no load leaves the row.
+__device__ __forceinline__ void xa_row8(const float* __restrict__ xr, int base, int D, int S, float (&o)[8]) {
+  using v4f = __attribute__((ext_vector_type(4))) float;
+  const int pb = base < S - 8 ? base : S - 8;
+  const v4f a = *reinterpret_cast<const v4f*>(xr + pb), b = *reinterpret_cast<const v4f*>(xr + pb + 4);
+  const float t[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int d = base + j;
+    o[j] = fmaf(t[j], (d < D && pb == base) ? 1.f : 0.f, d == D ? 1.f : 0.f);
+  }
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -1380,24 +1396,37 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
     for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
 
   // X rows of the next tile are loaded one step ahead (their latency hides behind the MFMAs)
-  float xnext[KS * 8];
+  float xnext[KD == 16 ? KS * 8 : 1];
   auto load_x = [&](int t) {
+    if constexpr (KD != 16) return;
     const float* xr = g.x + (size_t)(t * 32 + r) * stride;
+    // exec-masked loads of the obs columns (measured faster here than xa_row8's vector loads)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int d = 16 * ks + 8 * h + j;
-        xnext[ks * 8 + j] = d < D ? xr[d] : (d == D ? 1.f : 0.f);
-      }
+    for (int j = 0; j < 8; ++j) {
+      const int d = 8 * h + j;
+      xnext[j] = d < D ? xr[d] : (d == D ? 1.f : 0.f);
+    }
   };
-  // H1 tile (rows m in registers, columns k = 32w + r on lanes) of the X rows in xnext, as the B
-  // operand; then xnext <- the rows of tile tn
-  auto h1 = [&](int tn, h8 (&bh)[2], h8 (&bl)[2]) {
+  // H1 tile (rows m in registers, columns k = 32w + r on lanes) of tile tc's X rows, as the B
+  // operand.  Obs 6 / 12 (KD 16): the rows were loaded a step ahead into xnext, and tile tn's are
+  // loaded now; obs 24 (KD 32): loaded here (the prefetch registers would spill)
+  constexpr bool XPRE = KD == 16;
+  auto h1 = [&](int tc, int tn, h8 (&bh)[2], h8 (&bl)[2]) {
     float xv[KS * 8];
+    if constexpr (XPRE) {
 #pragma unroll
-    for (int i = 0; i < KS * 8; ++i) xv[i] = xnext[i];
-    load_x(tn);
+      for (int i = 0; i < KS * 8; ++i) xv[i] = xnext[i];
+      load_x(tn);
+    } else {
+      const float* xr = g.x + (size_t)(tc * 32 + r) * stride;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        float v[8];
+        xa_row8(xr, 16 * ks + 8 * h, D, stride, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[ks * 8 + j] = v[j];
+      }
+    }
     float xm = 0.f;
 #pragma unroll
     for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
@@ -1427,8 +1456,8 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   load(t0);
   store(0);
   if (t0 + 1 < t1) load(t0 + 1);
-  load_x(t0);
-  h1(t0 + 1 < t1 ? t0 + 1 : t0, bh, bl);
+  if constexpr (XPRE) load_x(t0);
+  h1(t0, t0 + 1 < t1 ? t0 + 1 : t0, bh, bl);
   __syncthreads();
   // Waves 4-7 share SIMDs with waves 0-3 (wave i runs on SIMD i mod 4) and run the same step
   // with the VALU blocks moved (H1 first, the tile split late): the two waves of a SIMD are then
@@ -1441,7 +1470,8 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
     const _Float16* b = sA + buf * 2 * SF_CH;
     h8 nbh[2], nbl[2];
     const int th = t + 2 < t1 ? t + 2 : t + 1 < t1 ? t + 1 : t;
-    if (NT_H1 < 0) h1(th, nbh, nbl);  // tile t + 1's H1
+    const int tc = t + 1 < t1 ? t + 1 : t;
+    if (NT_H1 < 0) h1(tc, th, nbh, nbl);  // tile t + 1's H1
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
       const int n = 32 * nt + r;
@@ -1454,14 +1484,14 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
       }
       if (nt == NT_STORE && more) store(buf ^ 1);              // tile t + 1 -> other buffer
       if (nt == NT_LOAD && t + 2 < t1) load(t + 2);            // tile t + 2 -> registers
-      if (nt == NT_H1) h1(th, nbh, nbl);                       // tile t + 1's H1
+      if (nt == NT_H1) h1(tc, th, nbh, nbl);                   // tile t + 1's H1
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) { bh[s] = nbh[s]; bl[s] = nbl[s]; }
     __syncthreads();
   };
 #if RLKS_F2_PHASES
-  if (w & 4)
+  if (KD == 16 && (w & 4))
     for (int t = t0; t < t1; ++t) step(std::integral_constant<int, 1>{}, t);
   else
 #endif
