@@ -263,8 +263,9 @@ def kernel_timing(algo, torch, config="c2", reps=20):
 
 def node_env_timing(algo, torch, timed, n=65536, C=8, nodes=256, depart_prob="stationary"):
     """BASELINE configs[2]: the node-level step kernel k_node_step (65,536 envs x 8 clusters x 256
-    nodes, Poisson(1) arrivals, first-fit, per-pod departures: "stationary" = arrivals balance
-    departures at the initial occupancy U(0, 50%); a float = that per-pod probability).
+    nodes, Poisson(1) arrivals, first-fit, per-pod departures realised as geometric skips:
+    "stationary" = arrivals balance departures at the initial occupancy U(0, 50%); a float = that
+    per-pod probability).
 
     Timed as a production driver runs it: ABI steps on preallocated buffers captured once into a
     HIP graph and replayed.  `ms` = the kernel alone (trusted actions: status = NULL);
@@ -309,32 +310,30 @@ def node_env_timing(algo, torch, timed, n=65536, C=8, nodes=256, depart_prob="st
     ms = timed(g_kernel.replay, n=5) / reps
     ms_checked = timed(g_checked.replay, n=5) / reps
     venv.check_status()
-    checks, placed, rejected, departed, written = cnt
-    # algorithmic bytes per env-step: every node read once (8 B), written nodes 8 B, obs 12C,
-    # used aggregates 4C, action 4, step r/w 8, episode 4, ep_ret r/w 16, reward 8, done 1, trunc 1, step_out 4
-    read_nodes = 8.0 * C * nodes
-    algo_bytes = read_nodes + 8 * written + 12 * C + 4 * C + 4 + 8 + 4 + 16 + 8 + 1 + 1 + 4
+    checks, placed, rejected, departed, written, chunks = cnt
+    # algorithmic bytes per env-step: the 8-node chunks the step reads (64 B each: those holding
+    # departing pods, the first-fit chunks) and the nodes it writes back (8 B); the chunk pod totals
+    # (2 B per chunk: at most a cluster's worth per departure and for the arrivals, and one write per
+    # chunk read); used millicores of every cluster 4C (departure draws and obs); obs 12C; action 4,
+    # step r/w 8, episode 4, ep_ret r/w 16, reward 8, done 1, trunc 1, step_out 4
+    algo_bytes = (64 * chunks + 8 * written + 2 * (nodes // 8) * (departed + 1) + 2 * chunks + 4 * C + 12 * C
+                  + 4 + 8 + 4 + 16 + 8 + 1 + 1 + 4)
     gbs = algo_bytes * n / (ms * 1e-3) / 1e9
-    # SURVEY.md §8(d)'s per-env-step figure counts the chosen cluster's first-fit scan only
-    # (256 x 8 B + 8 B + 72 B obs + the 41 B of the table env = 2,169 B at C = 8, N = 256); this
-    # kernel also realises every other cluster's per-pod departures each step, so
-    # both rates are reported
+    # SURVEY.md §8(d)'s per-env-step figure: the chosen cluster's nodes, 256 x 8 B + 8 B + 72 B obs +
+    # the 41 B of the table env = 2,169 B at C = 8, N = 256
     survey_bytes = nodes * 8 + 8 + (12 * C - 24) + ENV_BYTES_PER_STEP
     res = {"kernel": "k_node_step", "depart_prob": spec.depart_prob, "ms": ms, "ms_validated": ms_checked, "envs": n, "clusters": C,
            "nodes": nodes, "env_steps_per_s": n / (ms * 1e-3), "env_steps_per_s_validated": n / (ms_checked * 1e-3),
            "node_checks_per_step": checks, "placed_per_step": placed, "rejected_per_step": rejected,
-           "departed_per_step": departed, "nodes_written_per_step": written,
+           "departed_per_step": departed, "nodes_written_per_step": written, "chunks_read_per_step": chunks,
            "bytes_per_step": algo_bytes, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
            "survey_bytes_per_step": survey_bytes,
            "frac_hbm_survey_bytes": survey_bytes * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
-    # HBM bytes per launch from the committed PMC passes (tools/pmc_node_traffic.py), for the cache
-    # policy this churn selects (csrc/env.hip: streaming when depart_prob x max pods < 0.02)
     pmc = pmc_traffic()
-    key = "k_node_step_streaming" if spec.depart_prob * int(np.max(spec.max_pods())) < 0.02 else "k_node_step_default"
-    if pmc and key in pmc and (n, C, nodes) == (65536, 8, 256):
-        res["traffic"] = pmc[key]["hbm_bytes_per_launch"]
-        res["traffic_over_algorithmic"] = pmc[key]["hbm_bytes_per_launch"] / (algo_bytes * n)
-        res["traffic_source"] = pmc[key]["source"]
+    if pmc and "k_node_step" in pmc and (n, C, nodes) == (65536, 8, 256) and depart_prob == "stationary":
+        res["traffic"] = pmc["k_node_step"]["hbm_bytes_per_launch"]
+        res["traffic_over_algorithmic"] = pmc["k_node_step"]["hbm_bytes_per_launch"] / (algo_bytes * n)
+        res["traffic_source"] = pmc["k_node_step"]["source"]
     venv.close()
     return res
 

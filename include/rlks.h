@@ -115,8 +115,8 @@ int rlks_env_load_state(rlks_env* env, const void* src_dev, void* stream);
  * per-cluster used millicores [n_envs][n_clouds] (any pointer may be NULL) */
 int rlks_env_node_state(rlks_env* env, int32_t* free_cpu_dev, int32_t* free_mem_dev, int32_t* used_cpu_dev,
                         void* stream);
-/* node counters {node checks by first fit, pods placed, pods rejected, pods departed, nodes written}
- * (u64[5]) copied to out_dev when non-NULL; enable = 1 / 0 turns counting on (zeroed) / off, -1
+/* node counters {node checks by first fit, pods placed, pods rejected, pods departed, node
+ * write-backs, node reads} (u64[6]) copied to out_dev when non-NULL; enable = 1 / 0 turns counting on (zeroed) / off, -1
  * leaves it unchanged.  The flag is read when a step is launched (a captured graph keeps it). */
 int rlks_env_counters(rlks_env* env, int enable, unsigned long long* out_dev, void* stream);
 

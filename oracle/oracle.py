@@ -64,7 +64,8 @@ def lib():
         h.ro_env_enable_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         h.ro_env_node_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         h.ro_env_counters.argtypes = [C.c_void_p, C.c_void_p]
-        h.ro_binom_cdf32.argtypes = [C.c_int, C.c_double, C.c_void_p]
+        h.ro_skip32.argtypes = [C.c_int, C.c_double, C.c_void_p]
+        h.ro_skip32.restype = C.c_int
         h.ro_env_lane_step.argtypes = [C.c_void_p, C.c_int]
         h.ro_env_lane_episode.argtypes = [C.c_void_p, C.c_int]
         h.ro_env_lane_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
@@ -196,8 +197,8 @@ class OracleEnv:
         return fc, fm, used
 
     def counters(self):
-        """[node checks, pods placed, pods rejected, pods departed, nodes written]"""
-        c = np.zeros(5, np.int64)
+        """[node checks, pods placed, pods rejected, pods departed, node write-backs, node reads]"""
+        c = np.zeros(6, np.int64)
         lib().ro_env_counters(self.h, c.ctypes.data)
         return c
 
@@ -469,8 +470,10 @@ def ppo_iteration(flat, off, D, H, A, buf, *, perm_seed, epochs, mb, lr, gamma=0
     return p, m, v, kl_coeff, stats
 
 
-def binom_cdf32(maxp, p):
-    """[maxp+1][maxp+1] Binomial(n, p) CDF table in units of 2^-32 (departure draws)"""
-    out = np.zeros((maxp + 1, maxp + 1), np.uint32)
-    lib().ro_binom_cdf32(int(maxp), float(p), out.ctypes.data)
-    return out
+def skip32(pmax, p):
+    """departure-skip survival table round((1 - p)^j 2^32), j < min(pmax, last nonzero) + 1
+    """
+    n = lib().ro_skip32(int(pmax), float(p), None)
+    out = np.zeros(max(n, 1), np.uint32)
+    lib().ro_skip32(int(pmax), float(p), out.ctypes.data)
+    return out[:n]

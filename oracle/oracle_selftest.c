@@ -27,7 +27,7 @@ int ro_env_reset(ro_env* e, const uint8_t* mask, float* obs);
 int ro_env_step(ro_env* e, const int32_t* actions, float* obs, double* reward, uint8_t* term, int32_t* step_out,
                 float* final_obs, int32_t* status);
 void ro_env_node_state(const ro_env* e, int32_t* free_cpu, int32_t* free_mem, int32_t* used_cpu);
-void ro_env_counters(const ro_env* e, int64_t* out5);
+void ro_env_counters(const ro_env* e, int64_t* out6);
 void ro_env_lane_counters(const ro_env* e, int32_t* step, int32_t* episode);
 
 static rlks_env_cfg cfg_of(int n, int C, int noise, uint64_t seed, int autoreset) {
@@ -130,7 +130,7 @@ int main(int argc, char** argv) {
         }
         if (u != used[i * 8 + k]) { fprintf(stderr, "used aggregate mismatch\n"); return 1; }
       }
-    int64_t cnt[5];
+    int64_t cnt[6];
     ro_env_counters(e, cnt);
     cnt_total += cnt[1] + cnt[3];
     ro_env_destroy(e);

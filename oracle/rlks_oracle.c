@@ -132,8 +132,10 @@ typedef struct ro_env {
   double* enl;        /* exp(-lam), computed once on the host */
   int n_trace;
   int maxp;           /* most pods a node can hold */
-  uint32_t* cdf;      /* [maxp+1][maxp+1] Binomial(n, depart_prob) CDF in units of 2^-32 */
-  int64_t counters[5]; /* node checks, pods placed, pods rejected, pods departed, nodes written */
+  uint32_t* skip;     /* [n_skip] geometric survival (1 - depart_prob)^j in units of 2^-32 */
+  int n_skip;
+  int64_t counters[6]; /* node checks, pods placed, pods rejected, pods departed, node write-backs,
+                          node reads */
 } ro_env;
 
 ro_env* ro_env_create(const rlks_env_cfg* cfg, const double* cost, const double* lat) {
@@ -160,7 +162,7 @@ void ro_env_destroy(ro_env* e) {
   if (!e) return;
   free(e->cost); free(e->lat); free(e->step); free(e->episode); free(e->mt);
   free(e->cap_cpu); free(e->cap_mem); free(e->init_max); free(e->free_cpu); free(e->free_mem);
-  free(e->used_cpu); free(e->lam); free(e->enl); free(e->cdf);
+  free(e->used_cpu); free(e->lam); free(e->enl); free(e->skip);
   free(e);
 }
 
@@ -170,46 +172,46 @@ void ro_env_destroy(ro_env* e) {
  *  reset: node g = c*N + n gets pods0 = (x * (init_max[c] + 1)) >> 32 with x = word (g & 3) of
  *         Philox(ctr = {gid, episode, g >> 2, OCCUPANCY << 16}).
  *  step(a) at row t:
- *   1. departures (geometric per pod-slot): for every node g = c*N + n holding
- *      pods = (cap_cpu[c] - free_cpu[g]) / req_cpu pods, u = word (g & 3) of
- *      Philox({gid, episode, t, DEPART << 16 | g >> 2}); d = 0; while (d < pods && u >=
- *      cdf[pods][d]) d++; d pods leave.  cdf = ro_binom_cdf32(maxp, depart_prob) is the
- *      Binomial(pods, p) CDF in units of 2^-32.  (Nodes are processed in blocks of 4 that share
- *      one Philox call; a block whose 4 nodes are all empty draws nothing.)
+ *   1. departures (every running pod leaves independently with probability p =
+ *      depart_prob), realised per cluster as geometric skips over the cluster's P pods (numbered in
+ *      node order at the start of the step), so that a step reads only clusters where a pod leaves:
+ *      for c = 0..C-1 with P = used_cpu[c] / req_cpu > 0 (and p > 0): pos = 0, k = 0; while pos < P:
+ *      u = word (k & 3) of Philox({gid, episode, t | (k >> 2) << 16, DEPART << 16 | c}), k++;
+ *      R = P - pos; if u < S(R) stop (none of the remaining R pods leaves); else s = #{j in [1,
+ *      min(R, L)) : S(j) > u} pods survive and pod pos + s leaves; pos += s + 1.  S = ro_skip32(p)
+ *      (length L; S(j) = 0 for j >= L) is the survival table round((1 - p)^j 2^32), capped at
+ *      2^32 - 1, so P(s >= j) = (1 - p)^j: the departing set has the per-pod Bernoulli(p) law.
+ *      The pod's node is found by scanning the cluster's nodes in order (pods per node as at the
+ *      start of the step); its free cpu / mem grow by one request;
  *   2. arrivals: k ~ Poisson(lam) by inverse transform on u53 of Philox({gid, episode, t,
  *      ARRIVAL << 16}) words (0, 1): p = exp(-lam); F = p; while (u > F && k < 64)
  *      { k++; p = p * lam / k; F += p; }  (f64, no FMA; lam = rate, or trace[t mod n_trace]);
  *   3. first-fit: each pod goes to the lowest-index node of cluster a with free cpu >= req_cpu
  *      and free mem >= req_mem (the scan resumes where the previous pod landed); none -> rejected;
  *   4. reward = scale * (w_cost * cost[t][a] + w_lat * lat[t][a]) - penalty * rejected;
- *   5. t += 1; obs = [cost[t][.], lat[t][.], (float)used_cpu[c] / (float)(N * cap_cpu[c])]. */
+ *   5. t += 1; obs = [cost[t][.], lat[t][.], (float)used_cpu[c] / (float)(N * cap_cpu[c])].
+ *  counters: [0] first-fit node checks, [1] placed, [2] rejected, [3] departed, [4] node write-backs
+ *  (one per node that lost pods, one per node that received pods), [5] 8-node chunks read (those
+ *  holding departing pods; first fit: the chunks up to the last one tried, except chunks whose 8
+ *  nodes are all full, which the device skips by its per-chunk pod totals). */
 
-/* Binomial(n, p) CDF rows n = 0..maxp: P(X <= j) * 2^32 rounded half-up, capped at 2^32 - 1
- * (columns j >= n hold 2^32 - 1; the walk above stops at d = pods).  Plain f64 multiply / divide /
- * add, in this order. */
-void ro_binom_cdf32(int maxp, double p, uint32_t* cdf) {
-  const int M1 = maxp + 1;
-  for (int i = 0; i < M1 * M1; ++i) cdf[i] = 0xffffffffu;
-  for (int n = 0; n <= maxp; ++n) {
-    uint32_t* row = cdf + (size_t)n * M1;
-    if (p >= 1.0) {
-      for (int j = 0; j < n; ++j) row[j] = 0;
-      continue;
-    }
-    if (p <= 0.0) continue;
-    const double q = 1.0 - p, r = p / q;
-    double pmf = 1.0, acc = 0.0;
-    for (int i = 0; i < n; ++i) pmf = pmf * q;
-    for (int j = 0; j < n; ++j) {
-      acc = acc + pmf;
-      double x = acc * 4294967296.0;
-      x = x + 0.5;
-      row[j] = x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
-      pmf = pmf * (double)(n - j);
-      pmf = pmf / (double)(j + 1);
-      pmf = pmf * r;
-    }
+/* Survival table of the departure skips: S[j] = round((1 - p)^j * 2^32) capped at 2^32 - 1, for
+ * j = 0 .. n - 1 where n = min(pmax, first j with S[j] == 0) + 1 (entries past the table are 0).
+ * Plain f64 multiplies in this order.  Returns n (out may be NULL to size the table). */
+int ro_skip32(int pmax, double p, uint32_t* out) {
+  const double q = 1.0 - p;
+  double acc = 1.0;
+  int n = 0;
+  for (int j = 0; j <= pmax; ++j) {
+    double x = acc * 4294967296.0;
+    x = x + 0.5;
+    const uint32_t v = x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
+    if (v == 0u) break;
+    if (out) out[j] = v;
+    n = j + 1;
+    acc = acc * q;
   }
+  return n;
 }
 
 static void nodes_reset_lane(ro_env* e, int lane) {
@@ -242,29 +244,46 @@ static int nodes_step_lane(ro_env* e, int lane, int a, int t) {
   int32_t* used = e->used_cpu + (size_t)lane * C;
   uint32_t key[2] = {(uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32)};
   const uint32_t gid = (uint32_t)(cfg->env_offset + lane), ep = (uint32_t)e->episode[lane];
-  const int M1 = e->maxp + 1;
-  uint8_t* dirty = (uint8_t*)calloc((size_t)C * N, 1); /* nodes the step writes back */
-  for (int g0 = 0; g0 < C * N; g0 += 4) {
-    const int c = g0 / N;
-    int pods[4], any = 0;
-    for (int q = 0; q < 4; ++q) {
-      pods[q] = (e->cap_cpu[c] - fc[g0 + q]) / cfg->pod_cpu_m;
-      any |= pods[q] > 0;
+  const double pdep = cfg->depart_prob;
+  for (int c = 0; c < C && pdep > 0.0; ++c) {
+    const int P = used[c] / cfg->pod_cpu_m;
+    int32_t* cfc = fc + (size_t)c * N;
+    int32_t* cfm = fm + (size_t)c * N;
+    int pos = 0, k = 0, n = 0, cum = 0, dn = 0;  /* node scan: n, pods before it, departures from it */
+    int seen = -1;                                /* last 8-node chunk holding a departing pod */
+    uint32_t x[4] = {0, 0, 0, 0};
+    while (pos < P) {
+      if ((k & 3) == 0) {
+        uint32_t ctr[4] = {gid, ep, (uint32_t)t | ((uint32_t)(k >> 2) << 16),
+                           ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)c};
+        ro_philox4x32_10(ctr, key, x);
+      }
+      const uint32_t u = x[k & 3];
+      ++k;
+      const int R = P - pos;
+      const uint32_t sR = R < e->n_skip ? e->skip[R] : 0u;
+      if (u < sR) break;
+      int s = 0;
+      const int lim = R < e->n_skip ? R : e->n_skip;
+      while (s + 1 < lim && e->skip[s + 1] > u) ++s;
+      const int idx = pos + s;
+      pos = idx + 1;
+      /* node of pod idx: advance the scan, writing back the node left behind */
+      for (;;) {
+        const int pn = (e->cap_cpu[c] - cfc[n]) / cfg->pod_cpu_m + dn; /* pods at the start of the step */
+        if (idx < cum + pn) break;
+        if (dn) { e->counters[4] += 1; dn = 0; }
+        cum += pn;
+        ++n;
+      }
+      if ((n >> 3) != seen) { e->counters[5] += 1; seen = n >> 3; }
+      cfc[n] += cfg->pod_cpu_m;
+      cfm[n] += cfg->pod_mem_mi;
+      used[c] -= cfg->pod_cpu_m;
+      ++dn;
+      e->counters[3] += 1;
     }
-    if (!any) continue;
-    uint32_t x[4];
-    uint32_t ctr[4] = {gid, ep, (uint32_t)t, ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)(g0 >> 2)};
-    ro_philox4x32_10(ctr, key, x);
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t* row = e->cdf + (size_t)pods[q] * M1;
-      int d = 0;
-      while (d < pods[q] && x[q] >= row[d]) ++d;
-      fc[g0 + q] += d * cfg->pod_cpu_m;
-      fm[g0 + q] += d * cfg->pod_mem_mi;
-      used[c] -= d * cfg->pod_cpu_m;
-      e->counters[3] += d;
-      if (d) dirty[g0 + q] = 1;
-    }
+    if (dn) e->counters[4] += 1;
   }
   uint32_t x[4];
   uint32_t ctr[4] = {gid, ep, (uint32_t)t, (uint32_t)RLKS_PURPOSE_ARRIVAL << 16};
@@ -279,23 +298,40 @@ static int nodes_step_lane(ro_env* e, int lane, int a, int t) {
     p = p * lam / (double)k;
     F = F + p;
   }
-  int n = 0, rejected = 0;
+  int n = 0, rejected = 0, last = -1;
   int32_t* ac = fc + (size_t)a * N;
   int32_t* am = fm + (size_t)a * N;
+  int32_t* ac_start = (int32_t*)malloc((size_t)N * sizeof(int32_t)); /* free cpu before the arrivals */
+  memcpy(ac_start, ac, (size_t)N * sizeof(int32_t));
   for (int i = 0; i < k; ++i) {
     while (n < N && !(ac[n] >= cfg->pod_cpu_m && am[n] >= cfg->pod_mem_mi)) ++n;
     e->counters[0] += (n < N) ? 1 : 0;
     if (n == N) { rejected = k - i; break; }
+    if (n != last) { e->counters[4] += 1; last = n; }
     ac[n] -= cfg->pod_cpu_m;
     am[n] -= cfg->pod_mem_mi;
-    dirty[(size_t)a * N + n] = 1;
     used[a] += cfg->pod_cpu_m;
     e->counters[1] += 1;
   }
   e->counters[0] += n;
   e->counters[2] += rejected;
-  for (int g = 0; g < C * N; ++g) e->counters[4] += dirty[g];
-  free(dirty);
+  { /* first-fit chunk reads: the 8-node chunks the scan reaches with pods left to place, except
+       those whose nodes are all full (skipped by their pod totals) */
+    int mp = e->cap_cpu[a] / cfg->pod_cpu_m;
+    if (e->cap_mem[a] / cfg->pod_mem_mi < mp) mp = e->cap_mem[a] / cfg->pod_mem_mi;
+    const int last_ch = k == 0 ? -1 : (rejected ? N / 8 - 1 : n >> 3);
+    for (int ch = 0; ch <= last_ch; ++ch) {
+      int full = 1;
+      for (int q = 0; q < 8; ++q) {
+        const int node = 8 * ch + q;
+        /* fullness when the scan reached the chunk: before it (ch < n >> 3 and not rejected) the
+           chunk is full now iff it was then (first fit placed nothing there) */
+        if ((e->cap_cpu[a] - ac_start[node]) / cfg->pod_cpu_m < mp) full = 0;
+      }
+      if (!full) e->counters[5] += 1;
+    }
+  }
+  free(ac_start);
   return rejected;
 }
 
@@ -317,9 +353,10 @@ int ro_env_enable_nodes(ro_env* e, const int32_t* cap_cpu, const int32_t* cap_me
     if (e->init_max[c] > mp) e->init_max[c] = mp;
     if (mp > e->maxp) e->maxp = mp;
   }
-  if (e->maxp > 64 || N % 8 != 0 || (long)C * N > 262144) return -1;
-  e->cdf = (uint32_t*)malloc((size_t)(e->maxp + 1) * (e->maxp + 1) * sizeof(uint32_t));
-  ro_binom_cdf32(e->maxp, cfg->depart_prob, e->cdf);
+  if (e->maxp > 64 || N % 8 != 0 || (long)C * N > 262144 || cfg->n_rows > 65535 || C > 1024) return -1;
+  e->n_skip = ro_skip32(N * e->maxp, cfg->depart_prob, NULL);
+  e->skip = (uint32_t*)malloc((size_t)(e->n_skip > 0 ? e->n_skip : 1) * sizeof(uint32_t));
+  ro_skip32(N * e->maxp, cfg->depart_prob, e->skip);
   e->n_trace = cfg->arrival_mode ? n_trace : 1;
   e->lam = (double*)malloc(e->n_trace * sizeof(double));
   e->enl = (double*)malloc(e->n_trace * sizeof(double));
@@ -341,7 +378,7 @@ void ro_env_node_state(const ro_env* e, int32_t* free_cpu, int32_t* free_mem, in
   if (used_cpu) memcpy(used_cpu, e->used_cpu, n * e->cfg.n_clouds * sizeof(int32_t));
 }
 
-void ro_env_counters(const ro_env* e, int64_t* out5) { memcpy(out5, e->counters, sizeof(e->counters)); }
+void ro_env_counters(const ro_env* e, int64_t* out6) { memcpy(out6, e->counters, sizeof(e->counters)); }
 
 int ro_env_seed_lane(ro_env* e, int lane, const uint32_t* key, int keylen) {
   if (!e || lane < 0 || lane >= e->cfg.n_envs || keylen <= 0) return -1;

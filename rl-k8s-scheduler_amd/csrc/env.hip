@@ -218,168 +218,250 @@ __global__ __launch_bounds__(256) void k_env_step2(EnvView v, const double* __re
 }
 
 // ---------------------------------------------------------------- node-level step (c3 / c5)
-// One workgroup = 64 envs (one per lane) x W waves; wave w sweeps clusters w, w+W, ... of its 64
-// envs.  Per node: one 16-bit Philox draw -> departures ~ Binomial(pods, depart_prob) by the
-// LDS-resident inverse-CDF table; then, in the chosen cluster, first-fit placement of the
-// arriving pods; only changed nodes are written back.  The per-cluster used millicores meet in
-// LDS, wave 0 does the reward / step / episode bookkeeping, the auto-reset lanes re-draw their
-// occupancy, and the whole workgroup writes the 64 contiguous obs rows.  Same order and counters
-// as oracle/rlks_oracle.c:nodes_step_lane.
-constexpr int NODE_CHUNK = 16;
-// Cache policy of the node sweep.  NT (streaming) loads and stores suit a sweep that rewrites few
-// nodes: at c3's stationary churn (~1e-3 writes per node-step) they raise the sweep from 57% to
-// 61% of HBM peak.  With heavy churn the partial-line write-backs of non-resident lines cost more
-// than NT saves (depart_prob 0.02: 0.36 -> 0.44 ms), so launch_node_step picks the policy from the
-// expected writes per node.
-typedef int i32x2 __attribute__((ext_vector_type(2)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-template <bool NT>
-__device__ __forceinline__ void node_store(int2* p, int2 v) {
-  if constexpr (NT) __builtin_nontemporal_store(i32x2{v.x, v.y}, reinterpret_cast<i32x2*>(p));
-  else *p = v;
-}
-template <bool NT>
-__device__ __forceinline__ i32x4 node_load2(const int4* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(p));
-  else return *reinterpret_cast<const i32x4*>(p);
-}
+// One lane per env; the same algorithm, Philox counters and counters as
+// oracle/rlks_oracle.c:nodes_step_lane.  Departures: per cluster with pods, geometric skips over its
+// pods (one 32-bit draw per departure plus one to stop; the survival table is in LDS when it fits),
+// each departing pod located by a forward scan of the cluster's nodes, a node written back once
+// when the scan leaves it; arrivals: first fit from node 0 of the chosen cluster.  A lane reads
+// only the clusters where a pod leaves and the first-fit prefix: per env-step about one cluster of
+// nodes at c3's stationary churn instead of all C x N.
+constexpr int SKIP_LDS_MAX = 4096;  // survival-table entries staged in LDS (16 KB)
 
-__device__ __forceinline__ float node_obs(const EnvView& v, const double* __restrict__ cost,
-                                          const double* __restrict__ lat, const int32_t* s_used, int row,
-                                          int e, int j) {
-  const int C = v.C;
-  if (j < C) return (float)cost[row * C + j];
-  if (j < 2 * C) return (float)lat[row * C + j - C];
-  const int c = j - 2 * C;
-  return __fdiv_rn((float)s_used[c * 64 + e], (float)(v.nodes * v.cap[c]));
+__device__ __forceinline__ int node_pods(const EnvView& v, int32_t cc, int32_t free_cpu) {
+  return (int)(__umul24((uint32_t)(cc - free_cpu), v.pod_mag) >> v.pod_shift);
 }
-
-template <bool NT>
-__global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __restrict__ cost,
-                                                    const double* __restrict__ lat,
-                                                    const int32_t* __restrict__ actions, float* __restrict__ obs,
-                                                    double* __restrict__ rew64, float* __restrict__ rew32,
-                                                    uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                    int32_t* __restrict__ step_out, float* __restrict__ final_obs,
-                                                    int32_t* __restrict__ status) {
-  if (status && status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const int C = v.C, N = v.nodes, D = 3 * C, M1 = v.maxp + 1;
-  const int W = blockDim.x >> 6, l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint4* s_pre = (uint4*)smem;                             // [M1] first 4 CDF columns of each row
-  uint32_t* s_cdf = (uint32_t*)(s_pre + M1);               // [M1][M1]
-  int32_t* s_used = (int32_t*)(s_cdf + M1 * M1);           // [C][64]
-  int32_t* s_rej = s_used + C * 64;                        // [64]
-  int32_t* s_row = s_rej + 64;                             // [64] obs row, -1 = none
-  int32_t* s_frow = s_row + 64;                            // [64] final-obs row of auto-reset lanes, -1 = none
-  for (int i = threadIdx.x; i < M1 * M1; i += blockDim.x) s_cdf[i] = v.cdf[i];
-  for (int i = threadIdx.x; i < M1; i += blockDim.x) {
-    const uint32_t* r = v.cdf + (size_t)i * M1;
-    s_pre[i] = make_uint4(r[0], 1 < M1 ? r[1] : 0xffffffffu, 2 < M1 ? r[2] : 0xffffffffu,
-                          3 < M1 ? r[3] : 0xffffffffu);  // columns >= i hold 2^32-1; d is clamped to pods
+// the 8 nodes of a chunk: one 64-byte line, four 16-byte loads
+__device__ __forceinline__ void load_chunk(const int2* p, int2 (&f)[8]) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4* q = reinterpret_cast<const i32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const i32x4 x = q[i];
+    f[2 * i] = make_int2(x[0], x[1]);
+    f[2 * i + 1] = make_int2(x[2], x[3]);
   }
-  const int env0 = blockIdx.x * 64, env = env0 + l;
-  const bool live = env < v.N;
-  int t = 0, ep = 0, a = -1;
-  if (live) { t = v.step[env]; ep = v.episode[env]; a = actions[env]; }
-  const bool act = live && t < v.T;  // iloc[t] in bounds: this lane steps
-  if (w == 0) s_rej[l] = 0;
-  __syncthreads();
-  const uint32_t gid = (uint32_t)(v.env_offset + env);
-  const int32_t pc = v.pod_cpu, pm = v.pod_mem;
-  int2* base = v.free + (size_t)blockIdx.x * (size_t)C * N * 64 + 2 * l;
-  unsigned long long n_checks = 0, n_placed = 0, n_rej = 0, n_dep = 0, n_wr = 0;
-  for (int c = w; c < C; c += W) {
-    int32_t used = 0;
-    if (act) {
-      const int32_t cc = v.cap[c];
-      int rem = (a == c) ? arrivals(v, gid, ep, t) : 0;
-      int passed = 0, placed = 0, departed = 0, written = 0;
-      int2* col = base + (size_t)c * N * 64;
-      int32_t sum_free = 0;
-      const int4* p = reinterpret_cast<const int4*>(col);
-      for (int n0 = 0; n0 < N; n0 += NODE_CHUNK, p += NODE_CHUNK / 2 * 64) {
-        int2 f[NODE_CHUNK];
-        int pods[NODE_CHUNK];
+}
+// 8 chunk totals (16 bytes); returns their sum
+__device__ __forceinline__ int load_tot8(const uint16_t* p, int (&t)[8]) {
+  const uint4 x = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  int s = 0;
 #pragma unroll
-        for (int q = 0; q < NODE_CHUNK / 2; ++q) {  // 16 B per lane: a node pair, one pointer
-          const i32x4 x = node_load2<NT>(p + q * 64);
-          f[2 * q] = make_int2(x[0], x[1]);
-          f[2 * q + 1] = make_int2(x[2], x[3]);
-        }
-        int any = 0;
+  for (int i = 0; i < 4; ++i) {
+    t[2 * i] = (int)(w[i] & 0xffffu);
+    t[2 * i + 1] = (int)(w[i] >> 16);
+    s += t[2 * i] + t[2 * i + 1];
+  }
+  return s;
+}
+// write back the chunk's nodes that lost pods and its new total
+__device__ __forceinline__ void flush_chunk(int2* col, uint16_t* tot, int ch, int ctot, const int2 (&f)[8],
+                                            const int (&dep)[8], unsigned long long& n_wr) {
+  int d = 0;
 #pragma unroll
-        for (int q = 0; q < NODE_CHUNK; ++q) {
-          pods[q] = (int)(__umul24((uint32_t)(cc - f[q].x), v.pod_mag) >> v.pod_shift);
-          any |= pods[q];
-        }
-        int2* pw = col + (size_t)n0 * 64;  // node n0 + q at pw[node_off(q)] (n0 even)
-        unsigned dep_mask = 0;  // nodes already written by a departure this chunk
-        if (any) {  // departures: every pod-slot leaves with depart_prob (4 nodes per Philox draw)
-#pragma unroll
-          for (int h = 0; h < NODE_CHUNK; h += 4) {
-            if (!(pods[h] | pods[h + 1] | pods[h + 2] | pods[h + 3])) continue;  // empty block draws nothing
-            const u32x4 x = philox4x32_10_mad(u32x4{gid, (uint32_t)ep, (uint32_t)t,
-                                                    ((uint32_t)RLKS_PURPOSE_DEPART << 16) |
-                                                        (uint32_t)((c * N + n0 + h) >> 2)},
-                                              v.k0, v.k1);
-            const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int q = h + j;
-              const uint32_t u = wd[j];
-              const uint4 pre = s_pre[pods[q]];
-              int d = (int)(u >= pre.x) + (int)(u >= pre.y) + (int)(u >= pre.z) + (int)(u >= pre.w);
-              d = min(d, pods[q]);
-              if (d == 4 && pods[q] > 4) {  // 4 or more pods left this node: continue the inverse-CDF walk
-                const uint32_t* row = s_cdf + pods[q] * M1;
-                while (d < pods[q] && u >= row[d]) ++d;
-              }
-              if (d) {
-                f[q].x += __umul24(d, pc);
-                f[q].y += __umul24(d, pm);
-                departed += d;
-                ++written;
-                dep_mask |= 1u << q;
-                node_store<NT>(pw + node_off(q), f[q]);
-              }
-            }
-          }
-        }
-        if (rem > 0) {  // first fit: lowest node with room; a node passed over stays passed
-#pragma unroll
-          for (int q = 0; q < NODE_CHUNK; ++q) {
-            if (rem > 0) {
-              bool put = false;
-              while (rem > 0 && f[q].x >= pc && f[q].y >= pm) {
-                f[q].x -= pc;
-                f[q].y -= pm;
-                --rem;
-                ++placed;
-                put = true;
-              }
-              if (put) {
-                node_store<NT>(pw + node_off(q), f[q]);
-                written += !((dep_mask >> q) & 1u);  // one write-back per node, as the oracle counts
-              }
-              if (rem > 0) ++passed;
-            }
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < NODE_CHUNK; ++q) sum_free += f[q].x;
-      }
-      used = N * cc - sum_free;
-      if (a == c) {
-        s_rej[l] = rem;
-        n_checks += passed + placed;
-        n_placed += placed;
-        n_rej += rem;
-      }
-      n_dep += departed;
-      n_wr += written;
+  for (int q = 0; q < 8; ++q)
+    if (dep[q]) {
+      col[8 * ch + q] = f[q];
+      ++n_wr;
+      d += dep[q];
     }
-    s_used[c * 64 + l] = used;
+  tot[ch] = (uint16_t)(ctot - d);
+}
+
+// obs row `row` from the lane's used millicores (exact ints, IEEE f32 divide)
+__device__ __forceinline__ void node_obs_row(const EnvView& v, const double* __restrict__ cost,
+                                             const double* __restrict__ lat, int lane, int row,
+                                             float* __restrict__ o) {
+  const int C = v.C;
+  for (int c = 0; c < C; ++c) o[c] = (float)cost[row * C + c];
+  for (int c = 0; c < C; ++c) o[C + c] = (float)lat[row * C + c];
+  for (int c = 0; c < C; ++c)
+    o[2 * C + c] = __fdiv_rn((float)v.used_cpu[(size_t)c * v.N + lane], (float)(v.nodes * v.cap[c]));
+}
+
+template <bool LDS_SKIP>
+__global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __restrict__ cost,
+                                                   const double* __restrict__ lat,
+                                                   const int32_t* __restrict__ actions, float* __restrict__ obs,
+                                                   double* __restrict__ rew64, float* __restrict__ rew32,
+                                                   uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                   int32_t* __restrict__ step_out, float* __restrict__ final_obs,
+                                                   int32_t* __restrict__ status) {
+  if (status && status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
+  __shared__ uint32_t s_skip[LDS_SKIP ? SKIP_LDS_MAX : 1];
+  if (LDS_SKIP) {
+    for (int i = threadIdx.x; i < v.n_skip; i += blockDim.x) s_skip[i] = v.skip[i];
+    __syncthreads();
+  }
+  const uint32_t* S = LDS_SKIP ? s_skip : v.skip;
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  const int C = v.C, N = v.nodes, D = 3 * C;
+  const int32_t pc = v.pod_cpu, pm = v.pod_mem;
+  bool over = false;
+  unsigned long long n_checks = 0, n_placed = 0, n_rej = 0, n_dep = 0, n_wr = 0, n_rd = 0;
+  if (lane < v.N) {
+    const int t = v.step[lane], ep = v.episode[lane], a = actions[lane];
+    if (t >= v.T) {  // iloc[t] out of bounds before any change
+      over = true;
+      if (rew64) rew64[lane] = 0.0;
+      if (rew32) rew32[lane] = 0.f;
+      term[lane] = 0;
+      if (step_out) step_out[lane] = t;
+    } else {
+      const uint32_t gid = (uint32_t)(v.env_offset + lane);
+      int2* nodes = node_col(v, lane);
+      // 1. departures
+      for (int c = 0; c < C && v.depart_prob > 0.0; ++c) {
+        int32_t used = v.used_cpu[(size_t)c * v.N + lane];
+        const int P = used / pc;
+        if (P == 0) continue;
+        const int32_t cc = v.cap[c];
+        int2* col = nodes + (size_t)c * N;
+        uint16_t* tot = chunk_tot(v, lane, c);
+        int pos = 0, k = 0;
+        int grp = 0, gcum = 0, gsum = -1;  // group of 8 chunk totals holding the next pod
+        int gt[8];
+        int ch = -1, ccum = 0, ctot = 0;    // loaded chunk, pods before it, its pods at the start
+        int2 f[8];
+        int dep[8];
+        u32x4 x{0u, 0u, 0u, 0u};
+        while (pos < P) {
+          if ((k & 3) == 0)
+            x = philox4x32_10_mad(u32x4{gid, (uint32_t)ep, (uint32_t)t | ((uint32_t)(k >> 2) << 16),
+                                        ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)c},
+                                  v.k0, v.k1);
+          const uint32_t u = (k & 3) == 0 ? x.x : (k & 3) == 1 ? x.y : (k & 3) == 2 ? x.z : x.w;
+          ++k;
+          const int R = P - pos;
+          if (u < (R < v.n_skip ? S[R] : 0u)) break;  // none of the remaining R pods leaves
+          // surviving pods before the departure: the largest s in [0, min(R, L)) with S[s] > u
+          int lo = 0, hi = min(R, v.n_skip) - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (S[mid] > u) lo = mid;
+            else hi = mid - 1;
+          }
+          const int idx = pos + lo;
+          pos = idx + 1;
+          // pod idx (numbered in node order at the start of the step): its group, chunk, node
+          for (;;) {
+            if (gsum < 0) gsum = load_tot8(tot + 8 * grp, gt);
+            if (idx < gcum + gsum) break;
+            gcum += gsum;
+            ++grp;
+            gsum = -1;
+          }
+          int j = 0, cj = gcum, tj = gt[0];
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (j == q && idx >= cj + gt[q]) { cj += gt[q]; j = q + 1; }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) tj = (q == j) ? gt[q] : tj;
+          if (8 * grp + j != ch) {
+            if (ch >= 0) flush_chunk(col, tot, ch, ctot, f, dep, n_wr);
+            ch = 8 * grp + j;
+            ccum = cj;
+            ctot = tj;
+            load_chunk(col + 8 * ch, f);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dep[q] = 0;
+            ++n_rd;
+          }
+          int qn = 0, cq = ccum;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int pq = node_pods(v, cc, f[q].x) + dep[q];
+            if (qn == q && idx >= cq + pq) { cq += pq; qn = q + 1; }
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q == qn) {
+              ++dep[q];
+              f[q].x += pc;
+              f[q].y += pm;
+            }
+          used -= pc;
+          ++n_dep;
+        }
+        if (ch >= 0) {  // some pod left this cluster
+          flush_chunk(col, tot, ch, ctot, f, dep, n_wr);
+          v.used_cpu[(size_t)c * v.N + lane] = used;
+        }
+      }
+      // 2. arrivals at the chosen cluster, first fit: chunks whose 8 nodes are all full are skipped
+      // by their totals, the others are loaded and filled node by node in order
+      int rem = arrivals(v, gid, ep, t);
+      {
+        const int32_t cc = v.cap[a], cm = v.cap[C + a];
+        const int full = 8 * min(cc / pc, cm / pm);
+        int2* col = nodes + (size_t)a * N;
+        uint16_t* tot = chunk_tot(v, lane, a);
+        const int NC = N >> 3;
+        int placed = 0, last = -1;
+        for (int g = 0; 8 * g < NC && rem > 0; ++g) {
+          int gt[8];
+          (void)load_tot8(tot + 8 * g, gt);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int chn = 8 * g + j;
+            if (rem > 0 && chn < NC && gt[j] < full) {
+              int2 f[8];
+              load_chunk(col + 8 * chn, f);
+              ++n_rd;
+              int here = 0;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                int put = 0;
+                while (rem > 0 && f[q].x >= pc && f[q].y >= pm) {
+                  f[q].x -= pc;
+                  f[q].y -= pm;
+                  --rem;
+                  ++put;
+                }
+                if (put) {
+                  col[8 * chn + q] = f[q];
+                  ++n_wr;
+                  here += put;
+                  last = 8 * chn + q;
+                }
+              }
+              if (here) tot[chn] = (uint16_t)(gt[j] + here);
+              placed += here;
+            }
+          }
+        }
+        if (placed) v.used_cpu[(size_t)a * v.N + lane] += placed * pc;
+        const int nfin = rem > 0 ? N : (placed ? last : 0);
+        n_checks = (unsigned long long)(placed + nfin);
+        n_placed = (unsigned long long)placed;
+        n_rej = (unsigned long long)rem;
+      }
+      // 3. step (:115-144): reward on row t, t += 1, done, episode bookkeeping, obs
+      double r = __dmul_rn(v.scale, __dadd_rn(__dmul_rn(v.w_cost, cost[t * C + a]), __dmul_rn(v.w_lat, lat[t * C + a])));
+      if (v.penalty != 0.0) r = __dsub_rn(r, __dmul_rn(v.penalty, (double)rem));
+      const int t1 = t + 1;
+      v.step[lane] = t1;
+      const bool done = t1 >= v.max_steps;
+      if (t1 >= v.T) {
+        over = true;
+      } else {
+        if (v.track_returns) track_return(v, lane, ep, r, done);
+        if (done && v.autoreset) {
+          if (final_obs) node_obs_row(v, cost, lat, lane, t1, final_obs + (size_t)lane * D);
+          v.step[lane] = 0;
+          v.episode[lane] = ep + 1;
+          nodes_reset_lane(v, lane, ep + 1);
+          node_obs_row(v, cost, lat, lane, 0, obs + (size_t)lane * D);
+        } else {
+          node_obs_row(v, cost, lat, lane, t1, obs + (size_t)lane * D);
+        }
+      }
+      if (rew64) rew64[lane] = r;
+      if (rew32) rew32[lane] = (float)r;
+      term[lane] = (uint8_t)done;
+      if (step_out) step_out[lane] = t1;
+    }
+    if (trunc) trunc[lane] = 0;
   }
   if (v.counters) {
     n_checks = wave_sum_u64(n_checks);
@@ -387,77 +469,18 @@ __global__ void __launch_bounds__(1024) k_node_step(EnvView v, const double* __r
     n_rej = wave_sum_u64(n_rej);
     n_dep = wave_sum_u64(n_dep);
     n_wr = wave_sum_u64(n_wr);
-    if (l == 0) {
+    n_rd = wave_sum_u64(n_rd);
+    if ((threadIdx.x & 63) == 0) {
       if (n_checks) atomicAdd(&v.counters[0], n_checks);
       if (n_placed) atomicAdd(&v.counters[1], n_placed);
       if (n_rej) atomicAdd(&v.counters[2], n_rej);
       if (n_dep) atomicAdd(&v.counters[3], n_dep);
       if (n_wr) atomicAdd(&v.counters[4], n_wr);
+      if (n_rd) atomicAdd(&v.counters[5], n_rd);
     }
   }
-  __syncthreads();
-  bool over = false, reset = false;
-  if (w == 0) {  // step (:115-144): reward on row t, t += 1, done, episode bookkeeping
-    int row = -1, frow = -1;
-    if (live) {
-      if (!act) {  // iloc[t] out of bounds before any change
-        over = true;
-        if (rew64) rew64[env] = 0.0;
-        if (rew32) rew32[env] = 0.f;
-        term[env] = 0;
-        if (step_out) step_out[env] = t;
-      } else {
-        double r = __dmul_rn(v.scale, __dadd_rn(__dmul_rn(v.w_cost, cost[t * C + a]),
-                                                __dmul_rn(v.w_lat, lat[t * C + a])));
-        if (v.penalty != 0.0) r = __dsub_rn(r, __dmul_rn(v.penalty, (double)s_rej[l]));
-        const int t1 = t + 1;
-        v.step[env] = t1;
-        const bool done = t1 >= v.max_steps;
-        if (t1 >= v.T) {
-          over = true;
-        } else {
-          if (v.track_returns) track_return(v, env, ep, r, done);
-          row = t1;
-          if (done && v.autoreset) {
-            frow = t1;
-            row = 0;
-            reset = true;
-            v.step[env] = 0;
-            v.episode[env] = ep + 1;
-          }
-        }
-        if (rew64) rew64[env] = r;
-        if (rew32) rew32[env] = (float)r;
-        term[env] = (uint8_t)done;
-        if (step_out) step_out[env] = t1;
-      }
-      if (trunc) trunc[env] = 0;
-    }
-    s_row[l] = row;
-    s_frow[l] = frow;
-    const unsigned long long m = __ballot(over);
-    if (status && l == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
-  }
-  if (__syncthreads_or(reset)) {  // auto-reset lanes: final obs, then the next episode's occupancy
-    const int nrow = min(64, v.N - env0);
-    if (final_obs)
-      for (int i = threadIdx.x; i < nrow * D; i += blockDim.x) {
-        const int e = i / D, j = i - e * D;
-        if (s_frow[e] >= 0) final_obs[(size_t)env0 * D + i] = node_obs(v, cost, lat, s_used, s_frow[e], e, j);
-      }
-    __syncthreads();
-    if (live && s_frow[l] >= 0)
-      for (int c = w; c < C; c += W)
-        s_used[c * 64 + l] = nodes_reset_cluster(v, base + (size_t)c * N * 64, c, gid, ep + 1);
-    __syncthreads();
-  }
-  if (act)
-    for (int c = w; c < C; c += W) v.used_cpu[(size_t)c * v.N + env] = s_used[c * 64 + l];
-  const int nrow = min(64, v.N - env0);
-  for (int i = threadIdx.x; i < nrow * D; i += blockDim.x) {
-    const int e = i / D, j = i - e * D;
-    if (s_row[e] >= 0) obs[(size_t)env0 * D + i] = node_obs(v, cost, lat, s_used, s_row[e], e, j);
-  }
+  const unsigned long long m = __ballot(over);
+  if (status && (threadIdx.x & 63) == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
 }
 
 // TorchCategorical sample / argmax over A logits, then step
@@ -567,35 +590,21 @@ __global__ void k_mt_draws(uint32_t* __restrict__ mt, double* __restrict__ out, 
 using namespace rlks;
 
 namespace {
-// Binomial(n, p) CDF for n = 0..maxp in units of 2^-32 (row n, column j = P(X <= j)), capped at
-// 2^32 - 1 and computed in f64 exactly as oracle/rlks_oracle.c:ro_binom_cdf32 does; columns j >= n
-// hold 2^32 - 1 (the departure walk stops at d = pods).
-std::vector<uint32_t> binom_cdf32(int maxp, double p) {
-  const int M1 = maxp + 1;
-  std::vector<uint32_t> cdf((size_t)M1 * M1, 0xffffffffu);
-  for (int n = 0; n <= maxp; ++n) {
-    uint32_t* row = cdf.data() + (size_t)n * M1;
-    if (p >= 1.0) {
-      for (int j = 0; j < n; ++j) row[j] = 0;
-      continue;
-    }
-    if (p <= 0.0) continue;
-    const double q = 1.0 - p;
-    const double r = p / q;
-    double pmf = 1.0;
-    for (int i = 0; i < n; ++i) pmf = pmf * q;
-    double acc = 0.0;
-    for (int j = 0; j < n; ++j) {
-      acc = acc + pmf;
-      double x = acc * 4294967296.0;
-      x = x + 0.5;
-      row[j] = x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
-      pmf = pmf * (double)(n - j);
-      pmf = pmf / (double)(j + 1);
-      pmf = pmf * r;
-    }
+// Departure-skip survival table S[j] = round((1 - p)^j 2^32) capped at 2^32 - 1, j <
+// min(pmax, first j with S[j] == 0) + 1: computed in f64 exactly as oracle/rlks_oracle.c:ro_skip32.
+std::vector<uint32_t> skip32(int pmax, double p) {
+  std::vector<uint32_t> out;
+  const double q = 1.0 - p;
+  double acc = 1.0;
+  for (int j = 0; j <= pmax; ++j) {
+    double x = acc * 4294967296.0;
+    x = x + 0.5;
+    const uint32_t v = x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
+    if (v == 0u) break;
+    out.push_back(v);
+    acc = acc * q;
   }
-  return cdf;
+  return out;
 }
 }  // namespace
 
@@ -625,6 +634,8 @@ int rlks_env_create_ext(const rlks_env_cfg* cfg, const double* cost, const doubl
     RLKS_REQUIRE((long)C * NN <= 262144, RLKS_ERR_UNSUPPORTED,
                  "rlks_env_create_ext: at most 262,144 nodes per env (16-bit Philox block index)");
     RLKS_REQUIRE(C <= 1024, RLKS_ERR_UNSUPPORTED, "rlks_env_create_ext: at most 1,024 clusters");
+    RLKS_REQUIRE(cfg->n_rows <= 65535, RLKS_ERR_UNSUPPORTED,
+                 "rlks_env_create_ext: at most 65,535 table rows (16-bit step field of the departure counter)");
     RLKS_REQUIRE(cfg->depart_prob <= 1.0, RLKS_ERR_ARG, "rlks_env_create_ext: depart_prob must be <= 1");
     RLKS_REQUIRE(cfg->pod_cpu_m > 0 && cfg->pod_mem_mi > 0, RLKS_ERR_ARG, "rlks_env_create_ext: bad pod request");
     RLKS_REQUIRE(cfg->arrival_mode == 0 || (arrival_trace && n_trace > 0), RLKS_ERR_ARG,
@@ -675,22 +686,25 @@ int rlks_env_create_ext(const rlks_env_cfg* cfg, const double* cost, const doubl
       cap[2 * C + c] = std::min(mp, (int32_t)std::floor(cfg->init_occupancy * (double)mp));
       e->maxp = std::max(e->maxp, mp);
     }
-    const std::vector<uint32_t> cdf = binom_cdf32(e->maxp, cfg->depart_prob);
+    std::vector<uint32_t> skip = skip32(NN * e->maxp, cfg->depart_prob);
+    e->n_skip = (int)skip.size();
+    if (skip.empty()) skip.push_back(0u);
     e->n_trace = cfg->arrival_mode ? n_trace : 1;
     std::vector<double> lam(2 * e->n_trace);
     for (int i = 0; i < e->n_trace; ++i) {
       lam[i] = cfg->arrival_mode ? arrival_trace[i] : cfg->arrival_rate;
       lam[e->n_trace + i] = std::exp(-lam[i]);
     }
-    const size_t cells = (size_t)C * NN * cdiv((long)N, 64) * 64;  // wavefront-tiled, padded to 64 lanes
+    const size_t cells = (size_t)C * NN * N;  // [env][C][N]
     alloc((void**)&e->d_cap, cap.size() * sizeof(int32_t));
     alloc((void**)&e->d_lam, lam.size() * sizeof(double));
-    alloc((void**)&e->d_cdf, cdf.size() * sizeof(uint32_t));
+    alloc((void**)&e->d_skip, skip.size() * sizeof(uint32_t));
     alloc((void**)&e->d_free, cells * sizeof(int2));
+    alloc((void**)&e->d_chunk, (size_t)C * (((NN >> 3) + 7) & ~7) * N * sizeof(uint16_t));
     alloc((void**)&e->d_used_cpu, (size_t)C * N * sizeof(int32_t));
     if (err == hipSuccess) err = hipMemcpy(e->d_cap, cap.data(), cap.size() * sizeof(int32_t), hipMemcpyHostToDevice);
     if (err == hipSuccess) err = hipMemcpy(e->d_lam, lam.data(), lam.size() * sizeof(double), hipMemcpyHostToDevice);
-    if (err == hipSuccess) err = hipMemcpy(e->d_cdf, cdf.data(), cdf.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(e->d_skip, skip.data(), skip.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (err == hipSuccess) {
       hipLaunchKernelGGL(k_nodes_init, dim3(cdiv(N, ENV_BLOCK)), dim3(ENV_BLOCK), 0, 0, view(e));
       err = hipGetLastError();
@@ -720,8 +734,9 @@ int rlks_env_destroy(rlks_env* e) {
   if (e->d_mt) hipFree(e->d_mt);
   if (e->d_cap) hipFree(e->d_cap);
   if (e->d_lam) hipFree(e->d_lam);
-  if (e->d_cdf) hipFree(e->d_cdf);
+  if (e->d_skip) hipFree(e->d_skip);
   if (e->d_free) hipFree(e->d_free);
+  if (e->d_chunk) hipFree(e->d_chunk);
   if (e->d_used_cpu) hipFree(e->d_used_cpu);
   delete e;
   return RLKS_OK;
@@ -776,16 +791,13 @@ int rlks_env_step(rlks_env* e, const int32_t* actions, float* obs, double* rew64
     RLKS_LAUNCHED();
   }
   if (e->cfg.nodes_per_cluster > 0) {
-    const int C = e->cfg.n_clouds, W = std::min(C, 16), M1 = e->maxp + 1;
-    const size_t lds = (size_t)M1 * 16 + (size_t)M1 * M1 * sizeof(uint32_t) + ((size_t)C * 64 + 3 * 64) * sizeof(int32_t);
-    // expected node writes per node-step ~ depart_prob x mean pods (+ arrivals, < 1 per env-step)
-    const bool nt = e->cfg.depart_prob * e->maxp < 0.02;
-    if (nt)
-      hipLaunchKernelGGL(k_node_step<true>, dim3(cdiv(e->cfg.n_envs, 64)), dim3(64 * W), lds, s, view(e), e->d_cost,
-                         e->d_lat, actions, obs, rew64, rew32, term, trunc, step_out, final_obs, status);
+    const dim3 grid(cdiv(e->cfg.n_envs, 256)), blk(256);
+    if (e->n_skip <= SKIP_LDS_MAX)
+      hipLaunchKernelGGL(k_node_step<true>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64, rew32,
+                         term, trunc, step_out, final_obs, status);
     else
-      hipLaunchKernelGGL(k_node_step<false>, dim3(cdiv(e->cfg.n_envs, 64)), dim3(64 * W), lds, s, view(e), e->d_cost,
-                         e->d_lat, actions, obs, rew64, rew32, term, trunc, step_out, final_obs, status);
+      hipLaunchKernelGGL(k_node_step<false>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64,
+                         rew32, term, trunc, step_out, final_obs, status);
     RLKS_LAUNCHED();
     return RLKS_OK;
   }
@@ -855,7 +867,8 @@ int env_segments(const rlks_env* e, Seg* out) {
   out[n++] = {e->d_ep_cnt, N * sizeof(int32_t)};
   if (e->d_mt) out[n++] = {e->d_mt, (size_t)(MT_N + 1) * N * sizeof(uint32_t)};
   if (e->cfg.nodes_per_cluster > 0) {
-    out[n++] = {e->d_free, (size_t)e->cfg.n_clouds * e->cfg.nodes_per_cluster * cdiv((long)N, 64) * 64 * sizeof(int2)};
+    out[n++] = {e->d_free, (size_t)e->cfg.n_clouds * e->cfg.nodes_per_cluster * (size_t)N * sizeof(int2)};
+    out[n++] = {e->d_chunk, (size_t)e->cfg.n_clouds * (((e->cfg.nodes_per_cluster >> 3) + 7) & ~7) * N * sizeof(uint16_t)};
     out[n++] = {e->d_used_cpu, (size_t)e->cfg.n_clouds * N * sizeof(int32_t)};
   }
   return n;
@@ -865,7 +878,7 @@ size_t aligned(size_t b) { return (b + 255) / 256 * 256; }
 
 int rlks_env_state_bytes(const rlks_env* e, int64_t* bytes) {
   RLKS_REQUIRE(e && bytes, RLKS_ERR_ARG, "rlks_env_state_bytes: null argument");
-  Seg seg[8];
+  Seg seg[12];
   const int n = env_segments(e, seg);
   size_t b = 0;
   for (int i = 0; i < n; ++i) b += aligned(seg[i].bytes);
@@ -875,7 +888,7 @@ int rlks_env_state_bytes(const rlks_env* e, int64_t* bytes) {
 
 int rlks_env_save_state(const rlks_env* e, void* dst, void* stream) {
   RLKS_REQUIRE(e && dst, RLKS_ERR_ARG, "rlks_env_save_state: null argument");
-  Seg seg[8];
+  Seg seg[12];
   const int n = env_segments(e, seg);
   char* o = (char*)dst;
   for (int i = 0; i < n; ++i) {
@@ -887,7 +900,7 @@ int rlks_env_save_state(const rlks_env* e, void* dst, void* stream) {
 
 int rlks_env_load_state(rlks_env* e, const void* src, void* stream) {
   RLKS_REQUIRE(e && src, RLKS_ERR_ARG, "rlks_env_load_state: null argument");
-  Seg seg[8];
+  Seg seg[12];
   const int n = env_segments(e, seg);
   const char* o = (const char*)src;
   for (int i = 0; i < n; ++i) {
@@ -917,10 +930,10 @@ int rlks_env_node_state(rlks_env* e, int32_t* free_cpu, int32_t* free_mem, int32
 int rlks_env_counters(rlks_env* e, int enable, unsigned long long* out_dev, void* stream) {
   RLKS_REQUIRE(e, RLKS_ERR_ARG, "rlks_env_counters: null env");
   hipStream_t s = (hipStream_t)stream;
-  if (out_dev) RLKS_HIP(hipMemcpyAsync(out_dev, e->d_counters, 5 * sizeof(unsigned long long),
+  if (out_dev) RLKS_HIP(hipMemcpyAsync(out_dev, e->d_counters, 6 * sizeof(unsigned long long),
                                        hipMemcpyDeviceToDevice, s));
   if (enable >= 0) {
-    if (enable && !e->counters_on) RLKS_HIP(hipMemsetAsync(e->d_counters, 0, 5 * sizeof(unsigned long long), s));
+    if (enable && !e->counters_on) RLKS_HIP(hipMemsetAsync(e->d_counters, 0, 6 * sizeof(unsigned long long), s));
     e->counters_on = enable;
   }
   return RLKS_OK;

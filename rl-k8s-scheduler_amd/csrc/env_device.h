@@ -31,8 +31,10 @@ struct rlks_env {
   double* d_lam;        // [2][n_trace]: arrival rate, exp(-rate)
   int n_trace;
   int maxp;             // most pods a node can hold (over all clusters)
-  uint32_t* d_cdf;      // [maxp+1][maxp+1] Binomial(n, depart_prob) CDF in 1/65536 units
-  int2* d_free;         // [ceil(n_envs/64)][C*N/2][64][2] {free millicores, free MiB}
+  uint32_t* d_skip;     // [n_skip] departure-skip survival table round((1 - depart_prob)^j 2^32)
+  int n_skip;
+  int2* d_free;         // [n_envs][C][N] {free millicores, free MiB}
+  uint16_t* d_chunk;    // [n_envs][C][N/8] pods per 8-node chunk (the step's index into d_free)
   int32_t* d_used_cpu;  // [C][n_envs]
   unsigned long long* d_counters;  // [5] node checks, pods placed, pods rejected, pods departed,
                                    // nodes written (opt-in)
@@ -60,14 +62,16 @@ struct EnvView {
   int32_t* ep_cnt;
   uint32_t* mt;
   // node-level extension; nodes == 0 is the reference env
-  int nodes, pod_cpu, pod_mem, arrival_mode, n_trace, maxp;
+  int nodes, pod_cpu, pod_mem, arrival_mode, n_trace, n_skip;
   uint32_t pod_mag;     // pods on a node = mul_u24(cap - free, pod_mag) >> pod_shift (exact: see view())
   int pod_shift;
   double penalty;
   const int32_t* cap;   // [3][C]
   const double* lam;    // [2][n_trace]
-  const uint32_t* cdf;  // [maxp+1][maxp+1]
-  int2* free;           // [ceil(n_envs/64)][C*N][64] {free millicores, free MiB}: one 8-byte load per node
+  const uint32_t* skip; // [n_skip] departure-skip survival table
+  double depart_prob;
+  int2* free;           // [n_envs][C][N] {free millicores, free MiB}: a lane's nodes are contiguous
+  uint16_t* chunk;      // [n_envs][C][N/8] pods held by each 8-node chunk (64-byte line of free)
   int32_t* used_cpu;    // [C][n_envs]
   unsigned long long* counters;  // null unless enabled
   double* eplog;        // [RLKS_EPLOG_CAP] completed-episode returns (see rlks_env)
@@ -86,14 +90,15 @@ inline EnvView view(const rlks_env* e) {
   v.step = e->d_step; v.episode = e->d_episode; v.ep_ret = e->d_ep_ret; v.ret_sum = e->d_ret_sum;
   v.ep_cnt = e->d_ep_cnt; v.mt = e->d_mt;
   v.nodes = e->cfg.nodes_per_cluster; v.pod_cpu = e->cfg.pod_cpu_m; v.pod_mem = e->cfg.pod_mem_mi;
-  v.arrival_mode = e->cfg.arrival_mode; v.n_trace = e->n_trace; v.maxp = e->maxp;
+  v.arrival_mode = e->cfg.arrival_mode; v.n_trace = e->n_trace; v.n_skip = e->n_skip;
+  v.depart_prob = e->cfg.depart_prob;
   // (cap - free) = pods * pod_cpu with pods <= 64 and cap < 2^22: with m = ceil(2^24 / pod_cpu),
   // pods * pod_cpu * m / 2^24 = pods + pods * pod_cpu * delta / 2^24, delta < 1, and the error term
   // stays below 1 for pod_cpu < 2^18; the 24-bit product stays below 2^32.  pod_cpu = 1: identity.
   v.pod_shift = v.pod_cpu > 1 ? 24 : 0;
   v.pod_mag = v.pod_cpu > 1 ? (uint32_t)((16777216u + (uint32_t)v.pod_cpu - 1u) / (uint32_t)v.pod_cpu) : 1u;
   v.penalty = e->cfg.reject_penalty;
-  v.cap = e->d_cap; v.lam = e->d_lam; v.cdf = e->d_cdf; v.free = e->d_free;
+  v.cap = e->d_cap; v.lam = e->d_lam; v.skip = e->d_skip; v.free = e->d_free; v.chunk = e->d_chunk;
   v.used_cpu = e->d_used_cpu; v.counters = e->counters_on ? e->d_counters : nullptr;
   v.eplog = e->d_eplog; v.eplog_key = e->d_eplog_key; v.eplog_n = e->d_eplog_n;
   return v;
@@ -142,33 +147,43 @@ __device__ __forceinline__ double noise(const EnvView& v, int lane, int t, int c
 
 // ---------------------------------------------------------------- node-level extension
 // DESIGN.md §4 (builder-defined; same algorithm and the same Philox counters as
-// oracle/rlks_oracle.c).  Node state is int2 {free cpu, free mem}, tiled by wavefront in node
-// pairs: [ceil(n_envs/64)][C*N/2][64 lanes][2 nodes], so a wave's read of nodes (2p, 2p+1) is one
-// coalesced 1-KB access of 16 B per lane and a workgroup's 64 envs occupy one contiguous
-// C*N*512-byte region that the step kernel streams.  Node g of a lane sits at col[node_off(g)].
+// oracle/rlks_oracle.c).  Node state is int2 {free cpu, free mem}, [env][C][N]: each lane walks
+// its own contiguous nodes (a step touches only the clusters where a pod leaves and the chosen
+// cluster's first-fit prefix, different clusters in different lanes).
 __device__ __forceinline__ int2* node_col(const EnvView& v, int lane) {  // node 0 of `lane`
-  return v.free + (size_t)(lane >> 6) * (size_t)v.C * v.nodes * 64 + 2 * (lane & 63);
+  return v.free + (size_t)lane * v.C * v.nodes;
 }
-__device__ __forceinline__ size_t node_off(size_t g) { return (g >> 1) * 128 + (g & 1); }
+__device__ __forceinline__ size_t node_off(size_t g) { return g; }
+// chunk totals of cluster c of `lane`: N/8 entries padded to a multiple of 8 (16-byte groups)
+__device__ __forceinline__ int chunk_stride(int nodes) { return ((nodes >> 3) + 7) & ~7; }
+__device__ __forceinline__ uint16_t* chunk_tot(const EnvView& v, int lane, int c) {
+  return v.chunk + ((size_t)lane * v.C + c) * chunk_stride(v.nodes);
+}
 
-// initial occupancy of cluster c for one lane (episode `episode`); col = node_col(lane) + c*N*64
-// (N even: cluster c starts on a pair boundary).
-// Returns the cluster's used millicores.
-__device__ __forceinline__ int32_t nodes_reset_cluster(const EnvView& v, int2* col, int c, uint32_t gid,
-                                                       int episode) {
+// initial occupancy of cluster c for one lane (episode `episode`); col = node_col(lane) + c*N,
+// tot = the cluster's chunk totals.  Returns the cluster's used millicores.
+__device__ __forceinline__ int32_t nodes_reset_cluster(const EnvView& v, int2* col, uint16_t* tot, int c,
+                                                       uint32_t gid, int episode) {
   const int C = v.C, N = v.nodes;
   const int32_t cc = v.cap[c], cm = v.cap[C + c], m1 = v.cap[2 * C + c] + 1;
   int32_t used = 0;
-  for (int n4 = 0; n4 < N; n4 += 4) {
-    const u32x4 x = philox4x32_10(u32x4{gid, (uint32_t)episode, (uint32_t)((c * N + n4) >> 2),
-                                        (uint32_t)RLKS_PURPOSE_OCCUPANCY << 16}, v.k0, v.k1);
-    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  for (int n8 = 0; n8 < N; n8 += 8) {
+    int32_t ct = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int32_t pods = (int32_t)(((uint64_t)w[j] * (uint64_t)m1) >> 32);
-      col[node_off(n4 + j)] = make_int2(cc - pods * v.pod_cpu, cm - pods * v.pod_mem);
-      used += pods * v.pod_cpu;
+    for (int h = 0; h < 8; h += 4) {
+      const int n4 = n8 + h;
+      const u32x4 x = philox4x32_10(u32x4{gid, (uint32_t)episode, (uint32_t)((c * N + n4) >> 2),
+                                          (uint32_t)RLKS_PURPOSE_OCCUPANCY << 16}, v.k0, v.k1);
+      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int32_t pods = (int32_t)(((uint64_t)w[j] * (uint64_t)m1) >> 32);
+        col[node_off(n4 + j)] = make_int2(cc - pods * v.pod_cpu, cm - pods * v.pod_mem);
+        ct += pods;
+      }
     }
+    tot[n8 >> 3] = (uint16_t)ct;
+    used += ct * v.pod_cpu;
   }
   return used;
 }
@@ -177,7 +192,8 @@ __device__ __forceinline__ void nodes_reset_lane(const EnvView& v, int lane, int
   const uint32_t gid = (uint32_t)(v.env_offset + lane);
   int2* col = node_col(v, lane);
   for (int c = 0; c < v.C; ++c)
-    v.used_cpu[(size_t)c * v.N + lane] = nodes_reset_cluster(v, col + (size_t)c * v.nodes * 64, c, gid, episode);
+    v.used_cpu[(size_t)c * v.N + lane] =
+        nodes_reset_cluster(v, col + (size_t)c * v.nodes, chunk_tot(v, lane, c), c, gid, episode);
 }
 
 // pods arriving at row t: Poisson(lam) by inverse transform (f64, no contraction)

@@ -441,10 +441,10 @@ class VecK8sMultiCloudEnv:
         return fc, fm, used
 
     def counters(self, enable=-1):
-        """[node checks, pods placed, pods rejected, pods departed, nodes written] since counting was
-        enabled (enable=1 resets)"""
+        """[node checks, pods placed, pods rejected, pods departed, node write-backs, node reads] since
+        counting was enabled (enable=1 resets)"""
         torch = _torch()
-        out = torch.zeros(5, dtype=torch.int64, device=self.device)
+        out = torch.zeros(6, dtype=torch.int64, device=self.device)
         _lib.call("rlks_env_counters", self.handle, int(enable), _lib.ptr(out), self.dev.stream)
         return out
 

@@ -50,8 +50,8 @@ def test_node_state_invariants_and_obs(mode):
         np.testing.assert_array_equal(obs[:, 2 * C:], util)
         row = np.where(term.astype(bool), 0, step)  # auto-reset lanes show their new episode's row 0
         np.testing.assert_array_equal(obs[:, :C], cost[row].astype(np.float32))
-    scanned, placed, rejected, departed, written = env.counters()
-    assert placed > 0 and scanned >= placed and departed > 0 and written > 0
+    scanned, placed, rejected, departed, written, reads = env.counters()
+    assert placed > 0 and scanned >= placed and departed > 0 and written > 0 and reads > 0
 
 
 def test_first_fit_places_on_lowest_fitting_node():
@@ -73,7 +73,7 @@ def test_first_fit_places_on_lowest_fitting_node():
         if changed.size:
             assert (prev[: changed.min()] < 100).all()  # every lower node was already full
         prev = fc.copy()
-    _, placed, rejected, _, _ = env.counters()
+    _, placed, rejected, _, _, _ = env.counters()
     assert placed == min(placed + rejected, 3 * N) and rejected >= 0
 
 
@@ -113,17 +113,17 @@ def test_reject_penalty_applies():
     assert tot == 0.5 * pen.counters()[2]
 
 
-def test_binomial_departure_table():
-    """the departure table is the Binomial(n, p) CDF to 2^-32 (scipy), monotone, capped at 2^32-1"""
-    from scipy.stats import binom
-
-    for p in (0.0, 1.1e-4, 0.02, 0.3, 0.5, 1.0):
-        cdf = oracle.binom_cdf32(20, p).astype(np.int64)
-        for n in range(21):
-            row = cdf[n, : n + 1]
-            assert row[-1] == 2**32 - 1 and (np.diff(row) >= 0).all()
-            ref = np.minimum(np.round(binom.cdf(np.arange(n), n, p) * 2.0**32), 2**32 - 1)
-            assert n == 0 or np.abs(row[:n] - ref).max() <= 2, (p, n)
+def test_departure_skip_table():
+    """the departure-skip table is the geometric survival (1 - p)^j to 2^-32, non-increasing, capped
+    at 2^32 - 1, and ends at pmax or where it reaches 0"""
+    for p, pmax in ((0.0, 50), (1.1e-4, 10240), (0.02, 65536), (0.3, 500), (0.5, 100), (1.0, 10)):
+        s = oracle.skip32(pmax, p).astype(np.int64)
+        j = np.arange(len(s))
+        ref = np.minimum(np.round((1.0 - p) ** j * 2.0**32), 2**32 - 1)
+        assert s[0] == 2**32 - 1 and (np.diff(s) <= 0).all() and (s > 0).all()
+        assert np.abs(s - ref).max() <= 2, p
+        if len(s) < pmax + 1:
+            assert np.round((1.0 - p) ** len(s) * 2.0**32) == 0, p
 
 
 @pytest.mark.parametrize("p", [0.0, 1e-3, 0.05, 1.0])

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Add k_node_step's per-launch HBM traffic (separate --pmc FETCH_SIZE / WRITE_SIZE passes over
-tools/node_step_time.py, gfx950 correction FETCH x 2) to profiles/pmc_traffic.json, keyed by the
-cache-policy variant (<true> = streaming, the c3 stationary case; <false> = default, heavy churn).
+tools/node_step_time.py, gfx950 correction FETCH x 2) to profiles/pmc_traffic.json (key k_node_step:
+the c3 stationary-churn case bench.py reports traffic for).
 
 usage: pmc_node_traffic.py <fetch counter csv> <write counter csv> <source> [pmc_traffic.json]"""
 import collections
@@ -23,7 +23,7 @@ def main():
     dst = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
     out = json.load(open(dst))
     for k, f in fetch.items():
-        key = "k_node_step_streaming" if "<true>" in k else "k_node_step_default"
+        key = "k_node_step"
         rd, wr = f * 1024 * 2, write.get(k, 0.0) * 1024
         out[key] = {"kernel": k, "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
                     "source": sys.argv[3]}
