@@ -943,19 +943,22 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
       const int n0 = 32 * nt + 8 * gq + 4 * h;
       const float4 bb = *reinterpret_cast<const float4*>(sB2 + n0);
       const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
-      float wv[A_][4];
-#pragma unroll
-      for (int a = 0; a < A_; ++a) {
-        const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
-        wv[a][0] = t.x; wv[a][1] = t.y; wv[a][2] = t.z; wv[a][3] = t.w;
-      }
+      float h2v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int q = 4 * gq + i;
-        const float h2 = tanh_abs(fmaf(acc[nt][q], inv_z2, bv[i]));
-        acc[nt][q] = h2;
+        h2v[i] = tanh_abs(fmaf(acc[nt][q], inv_z2, bv[i]));
+        acc[nt][q] = h2v[i];
+      }
+      // one action's W3 quad at a time (4 registers live instead of 4 A): the same fma order per
+      // out[a] as element-major
 #pragma unroll
-        for (int a = 0; a < A_; ++a) out[a] = fmaf(h2, wv[a][i], out[a]);
+      for (int a = 0; a < A_; ++a) {
+        const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
+        out[a] = fmaf(h2v[0], t.x, out[a]);
+        out[a] = fmaf(h2v[1], t.y, out[a]);
+        out[a] = fmaf(h2v[2], t.z, out[a]);
+        out[a] = fmaf(h2v[3], t.w, out[a]);
       }
     }
 #pragma unroll
@@ -1000,18 +1003,19 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
       for (int gq = 0; gq < 4; ++gq) {
         float* dst = dst0 + (size_t)nt * 32 * 32 + (size_t)8 * gq * 32;
         const int n0 = 32 * nt + 8 * gq + 4 * h;
-        float wv[A_][4];
+        float gs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int a = 0; a < A_; ++a) {
           const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
-          wv[a][0] = t.x; wv[a][1] = t.y; wv[a][2] = t.z; wv[a][3] = t.w;
+          gs[0] = fmaf(dl[a], t.x, gs[0]);
+          gs[1] = fmaf(dl[a], t.y, gs[1]);
+          gs[2] = fmaf(dl[a], t.z, gs[2]);
+          gs[3] = fmaf(dl[a], t.w, gs[3]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int q = 4 * gq + i;
-          float gsum = 0.f;
-#pragma unroll
-          for (int a = 0; a < A_; ++a) gsum = fmaf(dl[a], wv[a][i], gsum);
+          const float gsum = gs[i];
           const float h2 = acc[nt][q];
           const float dz = gsum * (1.f - h2 * h2);
           dmx = fmaxf(dmx, fabsf(dz));
