@@ -377,9 +377,19 @@ __device__ unsigned long long g_sf_stamps[2][4096][8];
 __device__ unsigned long long g_sf_stamps2[2][4096][8];
 #define SF_STAMP2(i) \
   if (l == 0 && tile < 4096) g_sf_stamps2[NET][tile][i] = __builtin_amdgcn_s_memtime()
+// F1a (k_sf_fwd) phase clocks [net][tile][phase]; slot 7 = HW_ID | XCC_ID << 32
+__device__ unsigned long long g_fa_stamps[2][4096][8];
+#define FA_STAMP(i) \
+  if (l == 0 && tile < 4096) g_fa_stamps[NET][tile][i] = __builtin_amdgcn_s_memtime()
+#define FA_HWID()                                                                                   \
+  if (l == 0 && tile < 4096)                                                                        \
+  g_fa_stamps[NET][tile][7] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |       \
+                              ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32)
 #else
 #define SF_STAMP(i)
 #define SF_STAMP2(i)
+#define FA_STAMP(i)
+#define FA_HWID()
 #endif
 
 // W waves per workgroup, one 32-row tile each; one wave per SIMD (waves_per_eu 1) so that every
@@ -853,6 +863,8 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int D = g.D, stride = g.x_stride;
   const int tile = blockIdx.x * W + w, row0 = tile * 32;
+  FA_STAMP(0);
+  FA_HWID();
 
   half_dma<W>(N.w2ph, N.w2pl, 0, 0, sCh, w, l);
   for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i];
@@ -900,6 +912,7 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
   };
   vm_drain();
   __syncthreads();
+  FA_STAMP(1);
 
   // ---- Z2^T = W2 H1^T: 16 steps (k-tile c, n-half p) of 24 MFMAs over double-buffered
   // half-chunks; H1^T of k-tile c is computed at the start of its first step
@@ -929,7 +942,9 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
       vm_drain();
       __syncthreads();
     }
+    if (c == 0) FA_STAMP(2);
   }
+  FA_STAMP(3);
 
   // ---- H2^T = tanh(Z2^T + b2), head out[a] = b3 + sum_n W3[a][n] H2[n]
   const float inv_z2 = N.sc[3] / SF_H1_SCALE;
@@ -963,6 +978,7 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
     }
 #pragma unroll
   for (int a = 0; a < A_; ++a) out[a] += __shfl_xor(out[a], 32, 64) + N.b3[a];
+  FA_STAMP(4);
   float dl[A_];
   float st[4];
   sf_loss<A_, NET>(g, out, row0 + r, dl, st);
@@ -992,6 +1008,7 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
       }
     }
   }
+  FA_STAMP(5);
   // ---- dZ2^T = (dl W3) (1 - H2^2) -> HBM; the tile's split exponent for F1b, max for F2
   float dmx = 0.f;
   {
@@ -1028,6 +1045,7 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
     atomicMax(N.dzmax, __float_as_uint(dmx));
     N.tile_edz[tile] = sf_exp(dmx);
   }
+  FA_STAMP(6);
 }
 
 template <int A_, int KD, int W>
@@ -1526,6 +1544,9 @@ extern "C" int rlks_dbg_sf_stamps(unsigned long long* host) {
 }
 extern "C" int rlks_dbg_sf_stamps2(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sf_stamps2), sizeof(g_sf_stamps2)) == hipSuccess ? 0 : 1;
+}
+extern "C" int rlks_dbg_fa_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fa_stamps), sizeof(g_fa_stamps)) == hipSuccess ? 0 : 1;
 }
 #endif
 

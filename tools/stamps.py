@@ -42,9 +42,50 @@ def roll():
             print(f"  {n:26s} median {np.median(dt[:, i]):7.0f} cyc")
 
 
+def fwd_report(lib, tiles):
+    """F1a (k_sf_fwd) phases per wave, and how the waves that share a SIMD overlap in time"""
+    st = np.zeros((2, 4096, 8), np.uint64)
+    assert lib.rlks_dbg_fa_stamps(st.ctypes.data_as(C.c_void_p)) == 0
+    names = ["prologue", "Z2 k-tile 0", "Z2 k-tiles 1-7", "H2 + head", "loss + dW3 + stats", "dZ2 store"]
+    t = st[:, :tiles, :7].astype(np.int64)
+    hw = st[:, :tiles, 7]
+    t0 = t[..., 0].min()
+    for net in range(2):
+        s = t[net]
+        dt = np.diff(s, axis=1)
+        tot = s[:, 6] - s[:, 0]
+        print(f"F1a net {net}: wave lifetime median {np.median(tot):.0f} cyc (p10 {np.percentile(tot, 10):.0f}, "
+              f"p90 {np.percentile(tot, 90):.0f})")
+        for i, n in enumerate(names):
+            print(f"  {n:20s} median {np.median(dt[:, i]):8.0f}  p90 {np.percentile(dt[:, i], 90):8.0f}")
+    # SIMD identity: XCC, SE, SH, CU, SIMD fields of HW_ID (gfx9 layout)
+    hwid = (hw & 0xFFFFFFFF).astype(np.int64)
+    xcc = (hw >> 32).astype(np.int64) & 0xF
+    simd = (hwid >> 4) & 3
+    cu = (hwid >> 8) & 0xF
+    sh = (hwid >> 12) & 1
+    se = (hwid >> 13) & 7
+    key = (((xcc * 8 + se) * 2 + sh) * 16 + cu) * 4 + simd
+    start = t[..., 0].ravel() - t0
+    end = t[..., 6].ravel() - t0
+    k = key.ravel()
+    print(f"distinct SIMDs {len(np.unique(k))}, kernel span {end.max():.0f} cyc")
+    # per SIMD: busy span vs sum of wave lifetimes -> average waves resident
+    spans, conc = [], []
+    for q in np.unique(k)[:4096]:
+        m = k == q
+        spans.append(end[m].max() - start[m].min())
+        conc.append((end[m] - start[m]).sum() / max(1, spans[-1]))
+    print(f"per-SIMD span median {np.median(spans):.0f}, waves per SIMD {np.bincount(np.unique(k, return_counts=True)[1]).nonzero()[0]}, "
+          f"mean resident waves {np.mean(conc):.2f}")
+    order = np.argsort(start)
+    print("first 12 waves (start, end, simd key):", [(int(start[i]), int(end[i]), int(k[i])) for i in order[:12]])
+
+
 def main():
     if "--roll" in sys.argv:
         return roll()
+
     import torch
     from rlks import _lib
     from rlks.policy import PolicyParams
@@ -73,6 +114,10 @@ def main():
         _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
                   rows, grad.data_ptr(), None, ws.data_ptr(), ws.numel(), None)
     torch.cuda.synchronize()
+    tiles = rows // 32
+    if getattr(_lib.lib(), "rlks_dbg_fa_stamps", None) is not None and os.environ.get("RLKS_F1_SPLIT", "1") != "0":
+        fwd_report(_lib.lib(), tiles)  # split F1 (the default): F1a phases
+        return
     st = np.zeros((2, 4096, 8), np.uint64)
     assert _lib.lib().rlks_dbg_sf_stamps(st.ctypes.data_as(C.c_void_p)) == 0
     tiles = rows // 32
