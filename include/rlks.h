@@ -263,6 +263,20 @@ int rlks_ppo_sgd_step(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, 
                       float* adam_m_dev, float* adam_v_dev, int64_t n_params, float lr, float beta1, float beta2,
                       float eps, int step, int prev_fused, void* workspace, int64_t ws_bytes, void* stream);
 
+/* The same SGD step across ranks (reference: RLlib's multi-GPU learner, one gradient all-reduce per
+ * minibatch): rlks_ppo_grad_step writes the rank's gradient (as rlks_ppo_grad; its operand split
+ * reads the maxima the previous rlks_ppo_adam_apply left when prev_fused = 1); the caller all-reduces
+ * grad_dev; rlks_ppo_adam_apply then applies Adam step `step` in place (as rlks_adam_step,
+ * bit-identical) and leaves the new weights' maxima for the next step.  `rows` / the workspace are
+ * those of the gradient call; n_params = the padded layout size.  Other precisions run
+ * rlks_ppo_grad / rlks_adam_step. */
+int rlks_ppo_grad_step(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
+                       const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
+                       int step, int prev_fused, void* workspace, int64_t ws_bytes, void* stream);
+int rlks_ppo_adam_apply(const rlks_mlp_desc* desc, float* params_dev, const float* grad_dev, float* adam_m_dev,
+                        float* adam_v_dev, int64_t n_params, float lr, float beta1, float beta2, float eps, int step,
+                        void* workspace, int64_t ws_bytes, int rows, void* stream);
+
 /* RLlib update_kl: kl = stats_sum[0] / stats_sum[1]; x1.5 if kl > 2*target, x0.5 if < target/2 */
 int rlks_kl_update(float* dyn_dev, const double* kl_sum_count_dev, float kl_target, void* stream);
 

@@ -718,6 +718,8 @@ struct FusedAdam {
   float *p, *m, *v;
   AdamCo co;
   int step, prev_fused;
+  bool apply = true;  // false: the prep uses the previous step's maxima, the reduce only sums (an
+                      // all-reduce follows; rlks_ppo_adam_apply then applies Adam)
 };
 
 static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
@@ -773,7 +775,7 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     R.a.stats = stats;
     R.a.rows = (double)M;
   }
-  if (fa) {  // Adam on every parameter as its gradient is summed; W2 / W1a maxima -> the next prep
+  if (fa && fa->apply) {  // Adam on every parameter as its gradient is summed; W2 / W1a maxima -> the next prep
     for (int k = 0; k < 4; ++k)
       RLKS_REQUIRE(R.mnext[k] <= SF_PMAX, RLKS_ERR_UNSUPPORTED, "rlks_ppo_sgd_step: too many reduce blocks per weight");
     R.a.p = fa->p; R.a.m = fa->m; R.a.v = fa->v; R.a.grad = grad; R.a.co = fa->co;
@@ -909,6 +911,65 @@ int rlks_ppo_sgd_step(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, float* 
   FusedAdam fa{params, adam_m, adam_v, adam_co(lr, beta1, beta2, eps, step), step, prev_fused ? 1 : 0};
   return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
                  &fa);
+}
+
+// The multi-rank form of rlks_ppo_sgd_step: the gradient (its prep reading the previous step's
+// maxima when prev_fused), then, after the caller's all-reduce, Adam as a reduce over one partial
+// (the summed gradient) that also leaves the new maxima and the step tag, so no SGD step needs the
+// separate weight-max pass.  Same arithmetic as k_adam / the fused reduce: bit-identical parameters.
+int rlks_ppo_grad_step(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
+                       const float* mb, int M, float* grad, double* stats, int step, int prev_fused, void* workspace,
+                       int64_t ws_bytes, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(co && params && dyn && mb && grad && workspace && step >= 1, RLKS_ERR_ARG,
+               "rlks_ppo_grad_step: bad argument");
+  if (d->precision != RLKS_PRECISION_SF16 || is_wide(d))
+    return rlks_ppo_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, stream);
+  FusedAdam fa{nullptr, nullptr, nullptr, AdamCo{}, step, prev_fused ? 1 : 0, false};
+  return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
+                 &fa);
+}
+
+int rlks_ppo_adam_apply(const rlks_mlp_desc* d, float* params, const float* grad, float* adam_m, float* adam_v,
+                        int64_t n_params, float lr, float beta1, float beta2, float eps, int step, void* workspace,
+                        int64_t ws_bytes, int rows, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(params && grad && adam_m && adam_v && workspace && step >= 1, RLKS_ERR_ARG,
+               "rlks_ppo_adam_apply: bad argument");
+  if (d->precision != RLKS_PRECISION_SF16 || is_wide(d))
+    return rlks_adam_step(params, grad, adam_m, adam_v, n_params, lr, beta1, beta2, eps, step, stream);
+  RLKS_REQUIRE(rows > 0 && rows % 256 == 0, RLKS_ERR_ARG, "rlks_ppo_adam_apply: rows as in rlks_ppo_grad_step");
+  const int D = d->obs_dim, A = d->n_actions, H = HID;
+  const SfWs w = sf_ws_layout(D, A, rows, (char*)workspace);
+  RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_ppo_adam_apply: workspace too small");
+  const Layout L = make_layout(D, H, A);
+  RLKS_REQUIRE(n_params == L.padded, RLKS_ERR_ARG, "rlks_ppo_adam_apply: n_params must be the padded layout size");
+  float* g = const_cast<float*>(grad);  // one partial, summed in place (each element read and written by one thread)
+  Reducer R;
+  for (int net = 0; net < 2; ++net) {
+    const int An = net == 0 ? A : 1;
+    const int64_t* o = L.off + 6 * net;
+    R.add(g + o[0], g + o[0], nullptr, 0, 1, H * D, 2 * net + 1);
+    R.add(g + o[1], g + o[1], nullptr, 0, 1, H, 2 * net + 1);
+    R.add(g + o[2], g + o[2], nullptr, 0, 1, H * H, 2 * net);
+    R.add(g + o[3], g + o[3], nullptr, 0, 1, H);
+    R.add(g + o[4], g + o[4], nullptr, 0, 1, An * H);
+    R.add(g + o[5], g + o[5], nullptr, 0, 1, An);
+  }
+  for (int k = 0; k < 4; ++k)
+    RLKS_REQUIRE(R.mnext[k] <= SF_PMAX, RLKS_ERR_UNSUPPORTED, "rlks_ppo_adam_apply: too many blocks per weight");
+  R.a.p = params; R.a.m = adam_m; R.a.v = adam_v; R.a.grad = grad; R.a.co = adam_co(lr, beta1, beta2, eps, step);
+  const int par = step & 1;
+  for (int net = 0; net < 2; ++net) {
+    R.a.slot[2 * net] = w.w[net].pmax + (par * 2 + 0) * SF_PMAX;
+    R.a.slot[2 * net + 1] = w.w[net].pmax + (par * 2 + 1) * SF_PMAX;
+  }
+  R.a.tag[0] = w.w[0].tag + par;
+  R.a.tag[1] = w.w[1].tag + par;
+  R.a.tag_val = (unsigned)step + 1u;
+  hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, (hipStream_t)stream, R.a);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
 }
 
 int rlks_kl_update(float* dyn, const double* kc, float target, void* stream) {

@@ -371,13 +371,16 @@ class PPO:
                       self.ws.numel(), s)
             self._fused_prev = True
             return
-        _lib.call("rlks_ppo_grad", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat), _lib.ptr(self.dyn),
-                  _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row), _lib.ptr(self.ws),
-                  self.ws.numel(), s)
+        # ranks: gradient -> all-reduce -> Adam, the Adam pass also leaving the next split's weight
+        # maxima (rlks_ppo_grad_step / rlks_ppo_adam_apply: no weight-max pass per SGD step)
+        _lib.call("rlks_ppo_grad_step", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat), _lib.ptr(self.dyn),
+                  _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row), self.adam_step,
+                  int(self._fused_prev), _lib.ptr(self.ws), self.ws.numel(), s)
         self._allreduce(self.grad)
-        _lib.call("rlks_adam_step", _lib.ptr(self.params.flat), _lib.ptr(self.grad), _lib.ptr(self.adam_m),
+        _lib.call("rlks_ppo_adam_apply", desc, _lib.ptr(self.params.flat), _lib.ptr(self.grad), _lib.ptr(self.adam_m),
                   _lib.ptr(self.adam_v), self.params.padded, float(self.config.lr), float(beta1), float(beta2),
-                  float(self.config.adam_eps), self.adam_step, s)
+                  float(self.config.adam_eps), self.adam_step, _lib.ptr(self.ws), self.ws.numel(), self.mb, s)
+        self._fused_prev = True
 
     def update(self):
         cfg = self.config

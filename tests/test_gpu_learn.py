@@ -332,7 +332,8 @@ def test_packed_gather_equals_direct_gather(D, A, T, N, groups):
 @pytest.mark.parametrize("A", [2, 8])
 def test_fused_sgd_step_equals_grad_then_adam(A):
     """rlks_ppo_sgd_step (Adam inside the gradient reduction, the next step's weight maxima from
-    its slots) gives the parameters, Adam moments and gradients of rlks_ppo_grad + rlks_adam_step,
+    its slots) and the multi-rank pair rlks_ppo_grad_step + rlks_ppo_adam_apply (an all-reduce goes
+    between them) give the parameters, Adam moments and gradients of rlks_ppo_grad + rlks_adam_step,
     bit for bit, over consecutive steps -- including a first step that claims prev_fused with no
     fused predecessor (the device-side tag check falls back to scanning the weights)"""
     from rlks import _lib
@@ -346,16 +347,20 @@ def test_fused_sgd_step_equals_grad_then_adam(A):
     g = torch.Generator(device=d).manual_seed(A)
     p_ref = PolicyParams(D, 256, A, device=d, seed=3)
     p_fus = PolicyParams(D, 256, A, device=d, seed=3)
-    p_ref.desc.precision = p_fus.desc.precision = _lib.RLKS_PRECISION_SF16
+    p_spl = PolicyParams(D, 256, A, device=d, seed=3)
+    p_ref.desc.precision = p_fus.desc.precision = p_spl.desc.precision = _lib.RLKS_PRECISION_SF16
     P = p_ref.padded
     dyn = torch.tensor([0.1, 1.3, 0.2, 1.0 / M, 0, 0, 0, 0], dtype=torch.float32, device=d)
     wsb = C.c_int64()
     _lib.call("rlks_ppo_workspace_bytes", C.byref(desc), M, C.byref(wsb))
     ws_ref = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
     ws_fus = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
-    st = {k: torch.zeros(P, device=d) for k in ("m_ref", "v_ref", "g_ref", "m_fus", "v_fus", "g_fus")}
+    ws_spl = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
+    st = {k: torch.zeros(P, device=d) for k in ("m_ref", "v_ref", "g_ref", "m_fus", "v_fus", "g_fus", "m_spl", "v_spl",
+                                                 "g_spl")}
     stats_ref = torch.zeros(8, dtype=torch.float64, device=d)
     stats_fus = torch.zeros(8, dtype=torch.float64, device=d)
+    stats_spl = torch.zeros(8, dtype=torch.float64, device=d)
     for step in range(1, 6):
         mb = torch.zeros(M, stride, device=d)
         mb[:, :D] = torch.rand(M, D, generator=g, device=d)
@@ -372,10 +377,21 @@ def test_fused_sgd_step_equals_grad_then_adam(A):
                   mb.data_ptr(), M, st["g_fus"].data_ptr(), stats_fus.data_ptr(), st["m_fus"].data_ptr(),
                   st["v_fus"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, 1, ws_fus.data_ptr(), ws_fus.numel(),
                   None)
-        for a, b in (("g_ref", "g_fus"), ("m_ref", "m_fus"), ("v_ref", "v_fus")):
-            assert torch.equal(st[a].view(torch.int32), st[b].view(torch.int32)), (step, a)
+        _lib.call("rlks_ppo_grad_step", C.byref(desc), C.byref(co), p_spl.flat.data_ptr(), dyn.data_ptr(),
+                  mb.data_ptr(), M, st["g_spl"].data_ptr(), stats_spl.data_ptr(), step, 1, ws_spl.data_ptr(),
+                  ws_spl.numel(), None)
+        g_summed = st["g_spl"].clone()  # what a one-rank all-reduce leaves
+        _lib.call("rlks_ppo_adam_apply", C.byref(desc), p_spl.flat.data_ptr(), st["g_spl"].data_ptr(),
+                  st["m_spl"].data_ptr(), st["v_spl"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, ws_spl.data_ptr(),
+                  ws_spl.numel(), M, None)
+        assert torch.equal(st["g_spl"].view(torch.int32), g_summed.view(torch.int32)), step
+        for sfx in ("fus", "spl"):
+            for k in ("g", "m", "v"):
+                assert torch.equal(st[k + "_ref"].view(torch.int32), st[k + "_" + sfx].view(torch.int32)), (step, k, sfx)
         assert torch.equal(p_ref.flat.view(torch.int32), p_fus.flat.view(torch.int32)), step
+        assert torch.equal(p_ref.flat.view(torch.int32), p_spl.flat.view(torch.int32)), step
         assert torch.equal(stats_ref, stats_fus)
+        assert torch.equal(stats_ref, stats_spl)
 
 
 # ----------------------------------------------------------------------------- end to end
