@@ -137,10 +137,27 @@ __device__ __forceinline__ void xa_row8(const float* __restrict__ xr, int base, 
   }
 }
 
+// wave-wide reductions as a butterfly over lane bits 0..5 in VALU cross-lane ops (DPP quad_perm,
+// row_half_mirror, row_ror:8, v_permlane16/32_swap) instead of __shfl_xor's ds_bpermute round trips
+// through the LDS pipe (each a dependent lgkmcnt wait: ~40 of them per F1a epilogue).  Every step
+// adds a lane's value to its partner's (a + b on one lane, b + a on the other), so all lanes end
+// with the same bits.
+template <typename Op>
+__device__ __forceinline__ float wave_reduce(float v, Op op) {
+  v = op(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]: lane ^ 1
+  v = op(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]: lane ^ 2
+  v = op(v, dpp<0x141>(v));  // row_half_mirror: the other quad of the 8
+  v = op(v, dpp<0x128>(v));  // row_ror:8: lane ^ 8
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = op(__uint_as_float(p[0]), __uint_as_float(p[1]));  // rows 0 + 1, 2 + 3
+  p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return op(__uint_as_float(p[0]), __uint_as_float(p[1]));  // rows 0-1 + rows 2-3
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float a, float b) { return fmaxf(a, b); });
+}
+__device__ __forceinline__ float wave_sum_f(float v) {
+  return wave_reduce(v, [](float a, float b) { return a + b; });
 }
 
 // ----------------------------------------------------------------------------- weight prep
@@ -612,7 +629,7 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
     sv[A_] = h ? 0.f : st_pl; sv[A_ + 1] = h ? 0.f : st_vf; sv[A_ + 2] = h ? 0.f : st_kl; sv[A_ + 3] = h ? 0.f : st_ent;
 #pragma unroll
     for (int i = 0; i < A_ + 4; ++i) {
-      const float t = wave_sum(sv[i]);
+      const float t = wave_sum_f(sv[i]);
       if (l == 0) {
         if (i < A_) N.part_b3[(size_t)tile * A_ + i] = t;
         else N.part_stat[(size_t)tile * 4 + i - A_] = t;
@@ -999,12 +1016,14 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
     for (int a = 0; a < A_; ++a) sv[a] = h ? 0.f : dl[a];
 #pragma unroll
     for (int i = 0; i < 4; ++i) sv[A_ + i] = h ? 0.f : st[i];
+    float tv[A_ + 4];
 #pragma unroll
-    for (int i = 0; i < A_ + 4; ++i) {
-      const float t = wave_sum(sv[i]);
-      if (l == 0) {
-        if (i < A_) N.part_b3[(size_t)tile * A_ + i] = t;
-        else N.part_stat[(size_t)tile * 4 + i - A_] = t;
+    for (int i = 0; i < A_ + 4; ++i) tv[i] = wave_sum_f(sv[i]);  // independent chains, interleaved
+    if (l == 0) {
+#pragma unroll
+      for (int i = 0; i < A_ + 4; ++i) {
+        if (i < A_) N.part_b3[(size_t)tile * A_ + i] = tv[i];
+        else N.part_stat[(size_t)tile * 4 + i - A_] = tv[i];
       }
     }
   }
