@@ -21,7 +21,7 @@ struct SfNetW {
   float* pmax;        // [2 parity][2 kind: W2, W1a][SF_PMAX] per-block max |w| (k_sf_wmax: entries
                       // 0..15 of each kind; the fused reduce: one entry per reduce block)
   unsigned* tag;      // [2 parity]: the Adam step whose fused reduce filled pmax[parity] (0: none)
-  unsigned* dzmax;    // zeroed here (F1 atomicMax)
+  unsigned* dzmax;    // zeroed here: SF_DZ_SLOTS partial maxima (F1 atomicMax)
 };
 // parity: which half of pmax holds this prep's maxima; the split zeroes the other half, which the
 // fused reduce + Adam of the coming SGD step fills (one entry per reduce block, no atomics) for the

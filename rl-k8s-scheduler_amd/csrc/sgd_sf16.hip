@@ -48,6 +48,13 @@ using v4u = __attribute__((ext_vector_type(4))) unsigned;  // 16-byte staging re
 constexpr int SF_ROWS = 256;        // minibatch rows must be a multiple of this
 constexpr int SF_CH = 8192;         // halves per staged chunk (per hi / lo array)
 constexpr float SF_H1_SCALE = 16384.f;  // tanh outputs (|h| < 1) scaled by 2^14
+// max |dZ2| of an SGD step as SF_DZ_SLOTS partial maxima, one 64-byte line apart: F1a waves update
+// the slot of (tile mod SF_DZ_SLOTS), F2 takes the max over them.  One address for all 4,096 tile
+// atomics serialised at its L2 channel and cost F1a ~12 us of 93 (profiles/r02d/f1a_atomic_xp).
+constexpr int SF_DZ_SLOTS = 64, SF_DZ_STRIDE = 16;
+__device__ __forceinline__ unsigned* dz_slot(unsigned* base, int tile) {
+  return base + (tile & (SF_DZ_SLOTS - 1)) * SF_DZ_STRIDE;
+}
 
 __device__ __forceinline__ int sf_perm(int s, int h, int j) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
 
@@ -272,7 +279,7 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
   if (blockIdx.y == 0 && tid == 0) {
     N.sc[0] = s1; N.sc[1] = 1.f / s1; N.sc[4] = (float)e1;
     N.sc[2] = s2; N.sc[3] = 1.f / s2; N.sc[5] = (float)e2;
-    *N.dzmax = 0u;
+    for (int i = 0; i < SF_DZ_SLOTS; ++i) N.dzmax[i * SF_DZ_STRIDE] = 0u;
   }
   if (blockIdx.y == 0) {  // the other parity's entries: the coming fused reduce writes some of them
     float4* z = reinterpret_cast<float4*>(N.pmax + (g.parity ^ 1) * 2 * SF_PMAX);
@@ -670,7 +677,7 @@ __device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
       }
   }
   dmx = wave_max(dmx);
-  if (l == 0) atomicMax(N.dzmax, __float_as_uint(dmx));
+  if (l == 0) atomicMax(dz_slot(N.dzmax, tile), __float_as_uint(dmx));
   const int edz = sf_exp(dmx);
   const float sdz = pow2(edz);
   {
@@ -1061,7 +1068,7 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
   }
   dmx = wave_max(dmx);
   if (l == 0) {
-    atomicMax(N.dzmax, __float_as_uint(dmx));
+    atomicMax(dz_slot(N.dzmax, tile), __float_as_uint(dmx));
     N.tile_edz[tile] = sf_exp(dmx);
   }
   FA_STAMP(6);
@@ -1383,7 +1390,9 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   const int D = g.D, stride = g.x_stride;
   const int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
 
-  const float mxg = __uint_as_float(*N.dzmax);
+  // the step's max |dZ2|: lane i of every wave loads F1a's slot i, one wave-wide max
+  static_assert(SF_DZ_SLOTS == 64, "one slot per lane");
+  const float mxg = wave_max(__uint_as_float(N.dzmax[(threadIdx.x & 63) * SF_DZ_STRIDE]));
   const int eg = sf_exp(mxg);
   const float sg = pow2(eg);
   const float unscale = 1.f / (sg * SF_H1_SCALE);
