@@ -1390,12 +1390,9 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   const int D = g.D, stride = g.x_stride;
   const int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
 
-  // the step's max |dZ2|: lane i of every wave loads F1a's slot i, one wave-wide max
-  static_assert(SF_DZ_SLOTS == 64, "one slot per lane");
-  const float mxg = wave_max(__uint_as_float(N.dzmax[(threadIdx.x & 63) * SF_DZ_STRIDE]));
-  const int eg = sf_exp(mxg);
-  const float sg = pow2(eg);
-  const float unscale = 1.f / (sg * SF_H1_SCALE);
+  static_assert(SF_DZ_SLOTS == 64, "one max slot per lane");
+  // sg / unscale: from the step's max |dZ2|, read after the first tile's loads are in flight
+  float sg = 0.f, unscale = 0.f;
   const float inv_w1 = N.sc[1];
 
   h8 wh[KS], wl[KS];
@@ -1504,6 +1501,11 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   // other's VALU phases.
   h8 bh[2], bl[2];
   load(t0);
+  {  // lane i of every wave loads F1a's max slot i; one wave-wide max
+    const float mxg = wave_max(__uint_as_float(N.dzmax[(threadIdx.x & 63) * SF_DZ_STRIDE]));
+    sg = pow2(sf_exp(mxg));
+    unscale = 1.f / (sg * SF_H1_SCALE);
+  }
   store(0);
   if (t0 + 1 < t1) load(t0 + 1);
   if constexpr (XPRE) load_x(t0);
