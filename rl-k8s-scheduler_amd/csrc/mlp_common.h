@@ -71,6 +71,29 @@ __device__ __forceinline__ float half_wave_reduce16(const float (&v)[16], int l)
   return y + dpp<0xB1>(y);                                                                         // quad [1,0,3,2]
 }
 
+// wave-wide reductions as a butterfly over lane bits 0..5 in VALU cross-lane ops (DPP quad_perm,
+// row_half_mirror, row_ror:8, v_permlane16/32_swap) instead of __shfl_xor's ds_bpermute round trips
+// through the LDS pipe (each a dependent lgkmcnt wait: ~40 of them per F1a epilogue).  Every step
+// adds a lane's value to its partner's (a + b on one lane, b + a on the other), so all lanes end
+// with the same bits.
+template <typename Op>
+__device__ __forceinline__ float wave_reduce(float v, Op op) {
+  v = op(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]: lane ^ 1
+  v = op(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]: lane ^ 2
+  v = op(v, dpp<0x141>(v));  // row_half_mirror: the other quad of the 8
+  v = op(v, dpp<0x128>(v));  // row_ror:8: lane ^ 8
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = op(__uint_as_float(p[0]), __uint_as_float(p[1]));  // rows 0 + 1, 2 + 3
+  p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return op(__uint_as_float(p[0]), __uint_as_float(p[1]));  // rows 0-1 + rows 2-3
+}
+__device__ __forceinline__ float wave_max(float v) {
+  return wave_reduce(v, [](float a, float b) { return fmaxf(a, b); });
+}
+__device__ __forceinline__ float wave_sum_f(float v) {
+  return wave_reduce(v, [](float a, float b) { return a + b; });
+}
+
 // ----------------------------------------------------------------------------- layout
 struct Layout {
   int64_t off[RLKS_N_TENSORS];

@@ -43,11 +43,6 @@ __device__ __forceinline__ float tanh_abs(float x) {
   const float e = __builtin_amdgcn_exp2f(x * 2.885390081777927f);
   return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
 
 }  // namespace
 
