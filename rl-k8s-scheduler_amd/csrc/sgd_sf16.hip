@@ -854,7 +854,6 @@ template <int A_, int NET, int KD, int W>
 __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
   constexpr int NTHR = 64 * W;
   constexpr int KS = KD / 16;
-  constexpr int HALF = SF_CH / 2;
   const SfNet& N = g.n[NET];
   extern __shared__ __attribute__((aligned(16))) float lds[];
   _Float16* sCh = reinterpret_cast<_Float16*>(lds);             // [2 buf][2 hi/lo][128][32] (32 KB)
