@@ -400,7 +400,6 @@ static Ws ws_layout(int D, int A, int M, char* base) {
 }
 
 // split-fp16 path: pre-split weights, dZ2^T, per-F1-block and per-F2-split partials
-constexpr int SF_DZ_SLOTS_WS = 64 * 16;  // sgd_sf16.hip: SF_DZ_SLOTS partial maxima, SF_DZ_STRIDE apart
 struct SfWs {
   SfNetW w[2];
   SfNet n[2];
@@ -442,7 +441,7 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     W.pmax = (float*)take(4LL * 4 * SF_PMAX);
     W.tag = (unsigned*)take(4 * 2);
     w.pmax_roll[net] = (float*)take(4LL * 4 * SF_PMAX);
-    W.dzmax = (unsigned*)take(4 * SF_DZ_SLOTS_WS);
+    W.dzmax = (unsigned*)take(4 * SF_DZ_SLOTS * SF_DZ_STRIDE);
     n.w1h = W.w1h; n.w1l = W.w1l; n.w2ph = W.w2ph; n.w2pl = W.w2pl; n.w2th = W.w2th; n.w2tl = W.w2tl;
     n.sc = W.sc; n.dzmax = W.dzmax;
   }

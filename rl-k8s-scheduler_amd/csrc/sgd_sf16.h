@@ -9,6 +9,7 @@ namespace rlks {
 #endif
 constexpr int SF_F1_W = RLKS_F1_W;  // waves per F1 workgroup (one per SIMD); 32 rows each
 constexpr int SF_PMAX = 1024;       // weight-max entries per (parity, kind)
+constexpr int SF_DZ_SLOTS = 64, SF_DZ_STRIDE = 16;  // max |dZ2| partial maxima (sgd_sf16.hip dz_slot)
 }  // namespace rlks
 
 namespace rlks {

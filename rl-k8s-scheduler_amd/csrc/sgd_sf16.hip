@@ -51,7 +51,6 @@ constexpr float SF_H1_SCALE = 16384.f;  // tanh outputs (|h| < 1) scaled by 2^14
 // max |dZ2| of an SGD step as SF_DZ_SLOTS partial maxima, one 64-byte line apart: F1a waves update
 // the slot of (tile mod SF_DZ_SLOTS), F2 takes the max over them.  One address for all 4,096 tile
 // atomics serialised at its L2 channel and cost F1a ~12 us of 93 (profiles/r02d/f1a_atomic_xp).
-constexpr int SF_DZ_SLOTS = 64, SF_DZ_STRIDE = 16;
 __device__ __forceinline__ unsigned* dz_slot(unsigned* base, int tile) {
   return base + (tile & (SF_DZ_SLOTS - 1)) * SF_DZ_STRIDE;
 }
