@@ -726,18 +726,18 @@ int rlks_env_create_ext(const rlks_env_cfg* cfg, const double* cost, const doubl
 
 int rlks_env_destroy(rlks_env* e) {
   if (!e) return RLKS_OK;
-  hipDeviceSynchronize();
-  hipFree(e->d_cost); hipFree(e->d_lat); hipFree(e->d_step); hipFree(e->d_episode);
-  hipFree(e->d_ep_ret); hipFree(e->d_ret_sum); hipFree(e->d_ep_cnt); hipFree(e->d_status);
-  hipFree(e->d_counters);
-  hipFree(e->d_eplog); hipFree(e->d_eplog_key); hipFree(e->d_eplog_n);
-  if (e->d_mt) hipFree(e->d_mt);
-  if (e->d_cap) hipFree(e->d_cap);
-  if (e->d_lam) hipFree(e->d_lam);
-  if (e->d_skip) hipFree(e->d_skip);
-  if (e->d_free) hipFree(e->d_free);
-  if (e->d_chunk) hipFree(e->d_chunk);
-  if (e->d_used_cpu) hipFree(e->d_used_cpu);
+  (void)hipDeviceSynchronize();  // teardown: errors are not actionable here
+  (void)hipFree(e->d_cost); (void)hipFree(e->d_lat); (void)hipFree(e->d_step); (void)hipFree(e->d_episode);
+  (void)hipFree(e->d_ep_ret); (void)hipFree(e->d_ret_sum); (void)hipFree(e->d_ep_cnt); (void)hipFree(e->d_status);
+  (void)hipFree(e->d_counters);
+  (void)hipFree(e->d_eplog); (void)hipFree(e->d_eplog_key); (void)hipFree(e->d_eplog_n);
+  if (e->d_mt) (void)hipFree(e->d_mt);
+  if (e->d_cap) (void)hipFree(e->d_cap);
+  if (e->d_lam) (void)hipFree(e->d_lam);
+  if (e->d_skip) (void)hipFree(e->d_skip);
+  if (e->d_free) (void)hipFree(e->d_free);
+  if (e->d_chunk) (void)hipFree(e->d_chunk);
+  if (e->d_used_cpu) (void)hipFree(e->d_used_cpu);
   delete e;
   return RLKS_OK;
 }
@@ -964,8 +964,8 @@ int rlks_mt_random(const uint32_t* key, int keylen, double* out, int n, void* st
   if (n) hipLaunchKernelGGL(k_mt_draws, dim3(1), dim3(64), 0, s, mt, out, n);
   RLKS_LAUNCHED();
   RLKS_HIP(hipStreamSynchronize(s));
-  hipFree(mt);
-  hipFree(kl);
+  RLKS_HIP(hipFree(mt));
+  RLKS_HIP(hipFree(kl));
   return RLKS_OK;
 }
 
