@@ -61,14 +61,14 @@ struct RedArgs {
   unsigned tag_val;
 };
 
-__global__ __launch_bounds__(256) void k_reduce(RedArgs g) {
+__device__ __forceinline__ void reduce_block(const RedArgs& g, const int bx) {
   __shared__ double sh[4][256];
   int ti = 0;
-  while (ti + 1 < g.ntasks && (int)blockIdx.x >= g.t[ti + 1].blk0) ++ti;
+  while (ti + 1 < g.ntasks && bx >= g.t[ti + 1].blk0) ++ti;
   const RedTask T = g.t[ti];
   const int opb = 256 / T.G;
   const int o = threadIdx.x % opb, grp = threadIdx.x / opb;
-  const int iv = ((int)blockIdx.x - T.blk0) * opb + o;  // output vector
+  const int iv = (bx - T.blk0) * opb + o;  // output vector
   double s[4] = {0.0, 0.0, 0.0, 0.0};
   if (T.V == 4) {
     if (4 * iv < T.len)
@@ -121,17 +121,19 @@ __global__ __launch_bounds__(256) void k_reduce(RedArgs g) {
     if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = wmax;
     __syncthreads();
     if (threadIdx.x == 0)
-      g.slot[T.mslot][T.mbase + (int)blockIdx.x - T.blk0] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+      g.slot[T.mslot][T.mbase + bx - T.blk0] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
   }
-  if (g.stats && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (g.stats && bx == 0 && threadIdx.x == 0) {
     g.stats[RLKS_STAT_ROWS] = g.rows;
     g.stats[5] = g.stats[6] = g.stats[7] = 0.0;
   }
-  if (g.p && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (g.p && bx == 0 && threadIdx.x == 0) {
     *g.tag[0] = g.tag_val;
     *g.tag[1] = g.tag_val;
   }
 }
+
+__global__ __launch_bounds__(256) void k_reduce(RedArgs g) { reduce_block(g, (int)blockIdx.x); }
 
 struct Reducer {
   RedArgs a{};
@@ -231,19 +233,22 @@ struct GatherArgs {
 
 // source index t * N + n of minibatch row i: rows [k rows_g, (k+1) rows_g) come from lane group
 // k, whose permutation p -> (t = p / Ng, lane k Ng + p mod Ng)
-__device__ __forceinline__ int64_t gather_src(const GatherArgs& g, uint32_t i) {
-  const uint32_t k = i / (uint32_t)g.rows_g, ii = i - k * (uint32_t)g.rows_g;
-  const uint64_t p = perm_apply(g.perm[k], (uint64_t)(g.row0g + ii));
+__device__ __forceinline__ int64_t gather_src(const Perm* perm, int64_t row0g, int rows_g, int Ng, int N, uint32_t i) {
+  const uint32_t k = i / (uint32_t)rows_g, ii = i - k * (uint32_t)rows_g;
+  const uint64_t p = perm_apply(perm[k], (uint64_t)(row0g + ii));
   uint64_t t, nl;
   if (p >> 32) {
-    t = p / (uint64_t)g.Ng;
-    nl = p - t * (uint64_t)g.Ng;
+    t = p / (uint64_t)Ng;
+    nl = p - t * (uint64_t)Ng;
   } else {  // 32-bit division (every train batch below 2^32 rows per group)
-    const uint32_t t32 = (uint32_t)p / (uint32_t)g.Ng;
+    const uint32_t t32 = (uint32_t)p / (uint32_t)Ng;
     t = t32;
-    nl = (uint32_t)p - t32 * (uint32_t)g.Ng;
+    nl = (uint32_t)p - t32 * (uint32_t)Ng;
   }
-  return (int64_t)(t * (uint64_t)g.b.N + (uint64_t)k * g.Ng + nl);
+  return (int64_t)(t * (uint64_t)N + (uint64_t)k * Ng + nl);
+}
+__device__ __forceinline__ int64_t gather_src(const GatherArgs& g, uint32_t i) {
+  return gather_src(g.perm, g.row0g, g.rows_g, g.Ng, g.b.N, i);
 }
 
 // narrow records (stride 12 / 20 / 36: 2, 4 or 8 clouds): one thread per row computes the row's permuted source
@@ -325,14 +330,42 @@ __global__ __launch_bounds__(256) void k_pack(rlks_rollout_bufs b, int D, int A,
 // record's 16-byte piece q, so that every load instruction reads whole 64-byte lines (one line
 // per row for PS = 16) and the stores are contiguous
 template <int S, int PS>
-__global__ __launch_bounds__(256) void k_gather_packed(GatherArgs g) {
+__device__ __forceinline__ void gather_packed_elem(const Perm* perm, int64_t row0g, int rows_g, int Ng, int N, int rows,
+                                                   const float* packed, float* mb, uint32_t e) {
   constexpr int TPR = PS / 4;
-  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t i = e / TPR, q = e % TPR;
-  if (i >= (uint32_t)g.rows) return;
-  const int64_t tn = gather_src(g, i);
-  const float4 v = reinterpret_cast<const float4*>(g.packed + tn * PS)[q];
-  if (4 * q < (uint32_t)S) reinterpret_cast<float4*>(g.mb + (size_t)i * S)[q] = v;
+  if (i >= (uint32_t)rows) return;
+  const int64_t tn = gather_src(perm, row0g, rows_g, Ng, N, i);
+  const float4 v = reinterpret_cast<const float4*>(packed + tn * PS)[q];
+  if (4 * q < (uint32_t)S) reinterpret_cast<float4*>(mb + (size_t)i * S)[q] = v;
+}
+template <int S, int PS>
+__global__ __launch_bounds__(256) void k_gather_packed(GatherArgs g) {
+  gather_packed_elem<S, PS>(g.perm, g.row0g, g.rows_g, g.Ng, g.b.N, g.rows, g.packed, g.mb,
+                            blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// The next SGD step's packed gather, run by extra blocks of this step's reduce (single rank): the
+// reduce reads only gradient partials, and every kernel reading the minibatch buffer has finished
+// when it starts, so the gather may rewrite that buffer; one launch instead of two, and the gather's
+// latency-bound reads hide under the reduce's streaming.
+constexpr int NEXT_GROUPS = 8;
+struct NextGather {
+  Perm perm[NEXT_GROUPS];
+  int64_t row0g;
+  int rows, rows_g, Ng, N;
+  float* mb;
+  const float* packed;
+  int blk0;  // blocks [0, blk0) reduce, the rest gather
+};
+template <int S, int PS>
+__global__ __launch_bounds__(256) void k_reduce_gather(RedArgs g, NextGather n) {
+  if ((int)blockIdx.x < n.blk0) {
+    reduce_block(g, (int)blockIdx.x);
+    return;
+  }
+  gather_packed_elem<S, PS>(n.perm, n.row0g, n.rows_g, n.Ng, n.N, n.rows, n.packed, n.mb,
+                            ((uint32_t)blockIdx.x - (uint32_t)n.blk0) * 256u + threadIdx.x);
 }
 
 static Perm make_perm(uint64_t seed, int epoch, uint64_t S) {
@@ -724,7 +757,7 @@ struct FusedAdam {
 
 static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
                    const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes, int phases,
-                   hipStream_t s, const FusedAdam* fa = nullptr) {
+                   hipStream_t s, const FusedAdam* fa = nullptr, const NextGather* nx = nullptr) {
   RLKS_REQUIRE(M > 0 && M % 256 == 0, RLKS_ERR_ARG, "rlks_ppo_grad: split-fp16 rows must be a positive multiple of 256");
   const int D = d->obs_dim, A = d->n_actions, H = HID;
   const SfWs w = sf_ws_layout(D, A, M, (char*)workspace);
@@ -790,7 +823,17 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     R.a.tag[1] = w.w[1].tag + par;
     R.a.tag_val = (unsigned)fa->step + 1u;  // tag of step s = s + 1 (0: none), expected by step s + 1's prep
   }
-  hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
+  if (nx && nx->rows > 0) {  // + the next step's gather (blocks after the reduce's)
+    NextGather n = *nx;
+    n.blk0 = R.blocks;
+    const int ps = rlks_packed_stride(d), stride = mb_stride(D, A);
+    const dim3 grid(R.blocks + (int)cdiv((int64_t)n.rows * ps / 4, 256));
+    if (stride == 12) hipLaunchKernelGGL((k_reduce_gather<12, 16>), grid, dim3(256), 0, s, R.a, n);
+    else if (stride == 20) hipLaunchKernelGGL((k_reduce_gather<20, 32>), grid, dim3(256), 0, s, R.a, n);
+    else hipLaunchKernelGGL((k_reduce_gather<36, 48>), grid, dim3(256), 0, s, R.a, n);
+  } else {
+    hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
+  }
   RLKS_LAUNCHED();
   return RLKS_OK;
 }
@@ -911,6 +954,45 @@ int rlks_ppo_sgd_step(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, float* 
   FusedAdam fa{params, adam_m, adam_v, adam_co(lr, beta1, beta2, eps, step), step, prev_fused ? 1 : 0};
   return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
                  &fa);
+}
+
+int rlks_ppo_sgd_step_next(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, float* params, const float* dyn,
+                           const float* mb, int M, float* grad, double* stats, float* adam_m, float* adam_v,
+                           int64_t n_params, float lr, float beta1, float beta2, float eps, int step, int prev_fused,
+                           const rlks_gather_next* x, void* workspace, int64_t ws_bytes, void* stream) {
+  if (!x)
+    return rlks_ppo_sgd_step(d, co, params, dyn, mb, M, grad, stats, adam_m, adam_v, n_params, lr, beta1, beta2, eps,
+                             step, prev_fused, workspace, ws_bytes, stream);
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(x->packed_dev && x->mb_dev && x->rows >= 0 && x->T > 0 && x->N > 0, RLKS_ERR_ARG,
+               "rlks_ppo_sgd_step_next: bad gather argument");
+  RLKS_REQUIRE(rlks_packed_stride(d) > 0, RLKS_ERR_UNSUPPORTED,
+               "rlks_ppo_sgd_step_next: records of 2, 4 or 8 clouds only");
+  GatherArgs g;
+  if (int rc = gather_args(d, x->T, x->N, x->perm_seed, x->epoch, x->groups, x->group0, x->row0, x->rows, x->mb_dev, g))
+    return rc;
+  const bool fused = d->precision == RLKS_PRECISION_SF16 && !is_wide(d) && x->groups <= NEXT_GROUPS;
+  if (!fused) {  // the two calls
+    if (int rc = rlks_ppo_sgd_step(d, co, params, dyn, mb, M, grad, stats, adam_m, adam_v, n_params, lr, beta1, beta2,
+                                   eps, step, prev_fused, workspace, ws_bytes, stream))
+      return rc;
+    return rlks_ppo_gather_packed(d, x->packed_dev, x->T, x->N, x->perm_seed, x->epoch, x->groups, x->group0, x->row0,
+                                  x->rows, x->mb_dev, stream);
+  }
+  RLKS_REQUIRE(co && params && dyn && mb && grad && adam_m && adam_v && workspace && step >= 1, RLKS_ERR_ARG,
+               "rlks_ppo_sgd_step: bad argument");
+  NextGather n{};
+  for (int k = 0; k < x->groups; ++k) n.perm[k] = g.perm[k];
+  n.row0g = g.row0g;
+  n.rows = g.rows;
+  n.rows_g = g.rows_g;
+  n.Ng = g.Ng;
+  n.N = x->N;
+  n.mb = x->mb_dev;
+  n.packed = x->packed_dev;
+  FusedAdam fa{params, adam_m, adam_v, adam_co(lr, beta1, beta2, eps, step), step, prev_fused ? 1 : 0};
+  return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
+                 &fa, &n);
 }
 
 // The multi-rank form of rlks_ppo_sgd_step: the gradient (its prep reading the previous step's

@@ -67,6 +67,13 @@ class RolloutBufs(C.Structure):
                 ("vtarg", C.c_void_p), ("T", C.c_int32), ("N", C.c_int32)]
 
 
+class GatherNext(C.Structure):
+    """rlks_gather_next: the next SGD step's packed gather (rlks_ppo_sgd_step_next)"""
+    _fields_ = [("packed", C.c_void_p), ("mb", C.c_void_p), ("perm_seed", C.c_uint64), ("row0", C.c_int64),
+                ("T", C.c_int32), ("N", C.c_int32), ("epoch", C.c_int32), ("groups", C.c_int32),
+                ("group0", C.c_int32), ("rows", C.c_int32)]
+
+
 _P = C.c_void_p
 _I = C.c_int
 _I64 = C.c_int64
@@ -119,6 +126,8 @@ SIGNATURES = {
     "rlks_adam_step": [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _I, _P],
     "rlks_ppo_sgd_step": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _P, _I64, _F, _F, _F,
                           _F, _I, _I, _P, _I64, _P],
+    "rlks_ppo_sgd_step_next": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _P, _I64, _F,
+                               _F, _F, _F, _I, _I, C.POINTER(GatherNext), _P, _I64, _P],
     "rlks_ppo_grad_step": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _I, _I, _P, _I64, _P],
     "rlks_ppo_adam_apply": [C.POINTER(MlpDesc), _P, _P, _P, _P, _I64, _F, _F, _F, _F, _I, _P, _I64, _I, _P],
     "rlks_kl_update": [_P, _P, _F, _P],

@@ -394,6 +394,69 @@ def test_fused_sgd_step_equals_grad_then_adam(A):
         assert torch.equal(stats_ref, stats_spl)
 
 
+@pytest.mark.parametrize("A,groups", [(2, 1), (4, 2), (2, 16)])
+def test_sgd_step_next_equals_step_then_gather(A, groups):
+    """rlks_ppo_sgd_step_next (the next minibatch's packed gather run by extra blocks of the step's
+    reduce launch, rewriting the minibatch buffer the step just read) leaves the parameters, Adam
+    moments, stats and minibatch buffer of rlks_ppo_sgd_step + rlks_ppo_gather_packed, bit for bit,
+    over consecutive steps crossing an epoch; 16 lane groups exceed the fused form (two launches)"""
+    from rlks import _lib
+    from rlks.policy import PolicyParams
+
+    d = _dev()
+    D, T, N, M = 3 * A, 8, 2048, 2048
+    desc = _lib.MlpDesc(D, 256, A, _lib.RLKS_PRECISION_SF16)
+    L = _lib.lib()
+    stride, ps = L.rlks_minibatch_stride(C.byref(desc)), L.rlks_packed_stride(C.byref(desc))
+    co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.0)
+    g = torch.Generator(device=d).manual_seed(groups)
+    packed = torch.zeros(T * N, ps, device=d)
+    packed[:, :D] = torch.rand(T * N, D, generator=g, device=d)
+    packed[:, D:D + A] = torch.randn(T * N, A, generator=g, device=d)
+    packed[:, D + A] = torch.randn(T * N, generator=g, device=d)
+    packed[:, D + A + 1] = torch.randn(T * N, generator=g, device=d) * 30
+    packed[:, D + A + 2] = -torch.rand(T * N, generator=g, device=d) * 2
+    packed[:, D + A + 3] = torch.randint(0, A, (T * N,), generator=g, device=d).float()
+    dyn = torch.tensor([0.1, 1.3, 0.2, 1.0 / M, 0, 0, 0, 0], dtype=torch.float32, device=d)
+    wsb = C.c_int64()
+    _lib.call("rlks_ppo_workspace_bytes", C.byref(desc), M, C.byref(wsb))
+    run = {}
+    for k in ("ref", "nxt"):
+        p = PolicyParams(D, 256, A, device=d, seed=5)
+        p.desc.precision = _lib.RLKS_PRECISION_SF16
+        run[k] = dict(p=p, m=torch.zeros(p.padded, device=d), v=torch.zeros(p.padded, device=d),
+                      grad=torch.zeros(p.padded, device=d), ws=torch.zeros(wsb.value, dtype=torch.uint8, device=d),
+                      mb=torch.zeros(M, stride, device=d), stats=torch.zeros(6, 8, dtype=torch.float64, device=d))
+    seed = 0x1234ABCD
+    steps = [(e, b) for e in range(2) for b in range(3)]  # 3 minibatches of the 8 x 2048 batch, 2 epochs
+
+    def gather(r, e, b):
+        _lib.call("rlks_ppo_gather_packed", C.byref(desc), packed.data_ptr(), T, N, seed, e, groups, 0, b * M, M,
+                  r["mb"].data_ptr(), None)
+
+    def step_args(r, k):
+        return (C.byref(desc), C.byref(co), r["p"].flat.data_ptr(), dyn.data_ptr(), r["mb"].data_ptr(), M,
+                r["grad"].data_ptr(), r["stats"][k].data_ptr(), r["m"].data_ptr(), r["v"].data_ptr(), r["p"].padded,
+                3e-3, 0.9, 0.999, 1e-8, k + 1, int(k > 0))
+
+    ref, nxt = run["ref"], run["nxt"]
+    gather(ref, *steps[0])
+    gather(nxt, *steps[0])
+    for k in range(len(steps)):
+        _lib.call("rlks_ppo_sgd_step", *step_args(ref, k), ref["ws"].data_ptr(), ref["ws"].numel(), None)
+        x = None
+        if k + 1 < len(steps):
+            ne, nb = steps[k + 1]
+            gather(ref, ne, nb)
+            x = C.byref(_lib.GatherNext(packed.data_ptr(), nxt["mb"].data_ptr(), seed, nb * M, T, N, ne, groups, 0, M))
+        _lib.call("rlks_ppo_sgd_step_next", *step_args(nxt, k), x, nxt["ws"].data_ptr(), nxt["ws"].numel(), None)
+        assert torch.equal(ref["mb"].view(torch.int32), nxt["mb"].view(torch.int32)), k
+        assert torch.equal(ref["p"].flat.view(torch.int32), nxt["p"].flat.view(torch.int32)), k
+        for key in ("m", "v", "grad"):
+            assert torch.equal(ref[key].view(torch.int32), nxt[key].view(torch.int32)), (k, key)
+    assert torch.equal(ref["stats"], nxt["stats"])
+
+
 # ----------------------------------------------------------------------------- end to end
 def test_ppo_iteration_parity_and_surface(tmp_path):
     """one iteration at the c2 size (4,096 lanes x 128 steps): the fused rollout's env transitions
