@@ -81,12 +81,20 @@ __device__ __forceinline__ void reduce_block(const RedArgs& g, const int bx) {
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) sh[j][threadIdx.x] = s[j];
+  // groups summed pairwise in a fixed tree order: log2 G LDS steps (the G group values summed
+  // serially by each output's thread: 35 us instead of 19 us per c4 reduce, a few threads per
+  // block doing G dependent LDS reads each)
+  for (int h = T.G / 2; h >= 1; h /= 2) {
+    __syncthreads();
+    if (grp < h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sh[j][threadIdx.x] += sh[j][threadIdx.x + h * opb];
+  }
   __syncthreads();
   float wmax = 0.f;
   if (grp == 0) {
     double t[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int j = 0; j < T.V; ++j)
-      for (int q = 0; q < T.G; ++q) t[j] += sh[j][q * opb + o];
+    for (int j = 0; j < T.V; ++j) t[j] = sh[j][o];
     const int i0 = T.V * iv;
     if (T.out64) {
       for (int j = 0; j < T.V && i0 + j < T.len; ++j) T.out64[i0 + j] = t[j];
@@ -144,7 +152,10 @@ struct Reducer {
     t.mslot = mslot;
     t.mbase = 0;
     int G = 1;
-    while (G < 256 && G * 16 < P) G *= 2;
+#ifndef RLKS_RED_PPT
+#define RLKS_RED_PPT 32  // partials per thread (c4 reduce: 16 -> 19.0 us, 32 -> 19.0 us, 8 -> 23.9 us)
+#endif
+    while (G < 256 && G * RLKS_RED_PPT < P) G *= 2;
     const bool vec = len % 4 == 0 && pstride % 4 == 0 && ((uintptr_t)part & 15) == 0;
     t.part = part; t.out = out; t.out64 = out64; t.pstride = pstride; t.P = P; t.len = len; t.G = G;
     t.V = vec ? 4 : 1;
@@ -489,7 +500,7 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     n.part_w3 = (float*)take(4LL * tiles * An * HID);
     n.part_b3 = (float*)take(4LL * tiles * An);
     n.part_stat = (float*)take(4LL * tiles * 4);
-    n.part_w2 = (float*)take(4LL * w.splits * HID * HID);
+    n.part_w2 = (float*)take(4LL * w.splits * SF_W2_PSTRIDE);
     n.part_b2 = (float*)take(4LL * w.splits * HID);
   }
   w.stat64 = (double*)take(8 * 8);
@@ -794,7 +805,7 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     const SfNet& n = w.n[net];
     R.add(n.part_w1, grad + o[0], nullptr, (int64_t)H * D, w.blocks, H * D, 2 * net + 1);
     R.add(n.part_b1, grad + o[1], nullptr, H, w.blocks, H, 2 * net + 1);
-    R.add(n.part_w2, grad + o[2], nullptr, (int64_t)H * H, w.splits, H * H, 2 * net);
+    R.add(n.part_w2, grad + o[2], nullptr, SF_W2_PSTRIDE, w.splits, H * H, 2 * net);
     R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
     R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, M / 32, An * H);
     R.add(n.part_b3, grad + o[5], nullptr, An, M / 32, An);

@@ -1524,7 +1524,7 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   else
 #endif
     for (int t = t0; t < t1; ++t) step(std::integral_constant<int, 0>{}, t);
-  float* out = N.part_w2 + (size_t)blockIdx.x * HID * HID;
+  float* out = N.part_w2 + (size_t)blockIdx.x * SF_W2_PSTRIDE;
 #ifdef RLKS_F2_NOSTORE  // timing experiment only: the partials are not written
   if (acc[0][0] != 12345.f) return;
 #endif
