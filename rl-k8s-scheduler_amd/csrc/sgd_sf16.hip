@@ -177,6 +177,30 @@ __global__ __launch_bounds__(256) void k_sf_wmax(SfPrepArgs g) {
 __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
   const SfNetW& N = g.n[blockIdx.x];
   const int D = g.D, KD = g.KD, tid = threadIdx.x;
+  // the weights this thread splits, loaded before the scale is known: their latency overlaps the
+  // maxima's
+  const int base = blockIdx.y * 1024;
+  float vp[4], vt[4], vr[4], v1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = base + j * 256 + tid;
+    const int row = i >> 8, c = i & 255, blk = c >> 5, rem = c & 31;
+    const int src = 32 * blk + sf_perm(rem >> 4, (rem >> 3) & 1, rem & 7);
+    vp[j] = N.w2[row * HID + src];  // w2p[n = row][k perm]
+    vt[j] = N.w2[src * HID + row];  // w2t[k = row][n perm]
+    vr[j] = 0.f;
+    if (g.write_roll) {  // rollout copy: i = ((((q 8 + kt) 2 + s) 2 + ii) 64 + lane) 8 + jj -> w2p[n][32kt+16s+8h+jj]
+      const int jj = i & 7, lane = (i >> 3) & 63, ii = (i >> 9) & 1, ss = (i >> 10) & 1, kt = (i >> 11) & 7,
+                q = i >> 14;
+      const int n = 32 * (2 * q + ii) + (lane & 31);
+      vr[j] = N.w2[n * HID + 32 * kt + sf_perm(ss, lane >> 5, jj)];
+    }
+    v1[j] = 0.f;
+    if (i < HID * KD) {
+      const int k = i / KD, d = i - k * KD;
+      v1[j] = d < D ? N.w1[k * D + d] : (d == D ? N.b1[k] : 0.f);
+    }
+  }
   float m2 = 0.f, m1 = 0.f;
   if (g.skip_wmax && N.tag[g.parity] != g.expect_tag) {  // stale slots: this block scans the weights
     __shared__ float red[2][256];
@@ -204,51 +228,38 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
       m2 = fmaxf(m2, pm[i]);
       m1 = fmaxf(m1, pm[SF_PMAX + i]);
     }
-  } else {  // the fused reduce's per-block maxima (unused entries are zero)
-    __shared__ float red2[2][4];
+  } else {  // the fused reduce's per-block maxima (unused entries are zero): every wave reduces all
+            // of them itself (no barrier, so the weight loads above stay in flight)
     const float4* pm = reinterpret_cast<const float4*>(N.pmax + g.parity * 2 * SF_PMAX);
-    const float4 a = pm[tid], c = pm[SF_PMAX / 4 + tid];
-    m2 = fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w));
-    m1 = fmaxf(fmaxf(c.x, c.y), fmaxf(c.z, c.w));
+    const int l = tid & 63;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
-      m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
+    for (int q = 0; q < SF_PMAX / 256; ++q) {
+      const float4 a = pm[q * 64 + l], c = pm[SF_PMAX / 4 + q * 64 + l];
+      m2 = fmaxf(m2, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
+      m1 = fmaxf(m1, fmaxf(fmaxf(c.x, c.y), fmaxf(c.z, c.w)));
     }
-    if ((tid & 63) == 0) { red2[0][tid >> 6] = m2; red2[1][tid >> 6] = m1; }
-    __syncthreads();
-    m2 = fmaxf(fmaxf(red2[0][0], red2[0][1]), fmaxf(red2[0][2], red2[0][3]));
-    m1 = fmaxf(fmaxf(red2[1][0], red2[1][1]), fmaxf(red2[1][2], red2[1][3]));
+    m2 = wave_max(m2);
+    m1 = wave_max(m1);
   }
   const int e1 = sf_exp(m1), e2 = sf_exp(m2);
   const float s1 = pow2(e1), s2 = pow2(e2);
-  const int base = blockIdx.y * 1024;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int i = base + j * 256 + tid;
-    const int row = i >> 8, c = i & 255, blk = c >> 5, rem = c & 31;
-    const int src = 32 * blk + sf_perm(rem >> 4, (rem >> 3) & 1, rem & 7);
     _Float16 a, b;
-    split1(N.w2[row * HID + src] * s2, a, b);  // w2p[n = row][k perm]
+    split1(vp[j] * s2, a, b);
     N.w2ph[i] = a;
     N.w2pl[i] = b;
-    split1(N.w2[src * HID + row] * s2, a, b);  // w2t[k = row][n perm]
+    split1(vt[j] * s2, a, b);
     N.w2th[i] = a;
     N.w2tl[i] = b;
-    if (g.write_roll) {  // rollout copy: i = ((((q 8 + kt) 2 + s) 2 + ii) 64 + lane) 8 + j -> w2p[n][32kt+16s+8h+j]
-      const int j = i & 7, lane = (i >> 3) & 63, ii = (i >> 9) & 1, ss = (i >> 10) & 1, kt = (i >> 11) & 7,
-                q = i >> 14;
-      const int n = 32 * (2 * q + ii) + (lane & 31), kk = 32 * kt + 16 * ss + 8 * (lane >> 5) + j;
-      const int src2 = 32 * kt + sf_perm(ss, lane >> 5, j);
-      (void)kk;
-      split1(N.w2[n * HID + src2] * s2, a, b);
+    if (g.write_roll) {
+      split1(vr[j] * s2, a, b);
       N.w2rh[i] = a;
       N.w2rl[i] = b;
     }
     if (i < HID * KD) {
-      const int k = i / KD, d = i - k * KD;
-      const float v = d < D ? N.w1[k * D + d] : (d == D ? N.b1[k] : 0.f);
-      split1(v * s1, a, b);
+      split1(v1[j] * s1, a, b);
       N.w1h[i] = a;
       N.w1l[i] = b;
     }

@@ -11,7 +11,7 @@ import json, sys
 try:
     j = json.loads(open(sys.argv[1]).read().strip().split("\n")[-1])
     k = j["kernels"]
-    print(sys.argv[1], f"{j['value']/1e6:.2f}M", {n: round(k[n]["ms"] * 1000, 1) for n in ("k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce", "sgd_grad_total") if n in k})
+    print(sys.argv[1], f"{j['value']/1e6:.2f}M", {n: round(k[n]["ms"] * 1000, 1) for n in ("k_sf_prep", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce", "sgd_grad_total") if n in k})
 except Exception as e:
     print(sys.argv[1], "failed", open(sys.argv[1]).read()[-300:])
 PY
