@@ -326,8 +326,8 @@ def ppo_loss_grad(flat, off, D, H, A, mb, *, clip_param=0.3, vf_clip_param=10.0,
     vf = torch.clamp((value - vt) ** 2, 0, vf_clip_param)
     total = (-surr + vf_loss_coeff * vf - entropy_coeff * ent).sum() / count + kl_coeff * kl.sum() / count
     total.backward()
-    stats = {"policy_loss": float((-surr).sum()), "vf_loss": float(vf.sum()), "kl": float(kl.sum()),
-             "entropy": float(ent.sum()), "rows": rows}
+    stats = {"policy_loss": float((-surr).sum().detach()), "vf_loss": float(vf.sum().detach()),
+             "kl": float(kl.sum().detach()), "entropy": float(ent.sum().detach()), "rows": rows}
     return f.grad.numpy(), stats
 
 
