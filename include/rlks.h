@@ -266,7 +266,7 @@ int rlks_ppo_sgd_step(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, 
 /* rlks_ppo_sgd_step followed by the next step's rlks_ppo_gather_packed (the arguments below) into
  * next->mb_dev, which may be this step's own mb_dev: the gather runs inside the step's last launch
  * (its gradient reduction), after every read of the minibatch.  Same rows and bytes as the two
- * calls; next == NULL is rlks_ppo_sgd_step.  Single rank.  (Reference: RLlib's minibatch loop,
+ * calls; next == NULL is rlks_ppo_sgd_step.  (Reference: RLlib's minibatch loop,
  * sgd_minibatch_size at rl_scheduler/agent/train_ppo.py:16, draws minibatch k+1 after SGD step k.) */
 typedef struct rlks_gather_next {
   const float* packed_dev; /* rlks_ppo_pack records [T N] */
@@ -291,6 +291,12 @@ int rlks_ppo_sgd_step_next(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coe
 int rlks_ppo_grad_step(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
                        const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
                        int step, int prev_fused, void* workspace, int64_t ws_bytes, void* stream);
+/* rlks_ppo_grad_step + the next step's gather, as rlks_ppo_sgd_step_next (the gather blocks ride
+ * in the gradient-reduce launch, before the caller's all-reduce). */
+int rlks_ppo_grad_step_next(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
+                            const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
+                            int step, int prev_fused, const rlks_gather_next* next, void* workspace,
+                            int64_t ws_bytes, void* stream);
 int rlks_ppo_adam_apply(const rlks_mlp_desc* desc, float* params_dev, const float* grad_dev, float* adam_m_dev,
                         float* adam_v_dev, int64_t n_params, float lr, float beta1, float beta2, float eps, int step,
                         void* workspace, int64_t ws_bytes, int rows, void* stream);

@@ -967,6 +967,33 @@ int rlks_ppo_sgd_step(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, float* 
                  &fa);
 }
 
+// the next step's gather as extra reduce blocks (fused = true), or false: the caller gathers with
+// rlks_ppo_gather_packed after the step (wide / fp32 paths, more than NEXT_GROUPS lane groups)
+static int next_gather(const rlks_mlp_desc* d, const rlks_gather_next* x, NextGather& n, bool& fused) {
+  RLKS_REQUIRE(x->packed_dev && x->mb_dev && x->rows >= 0 && x->T > 0 && x->N > 0, RLKS_ERR_ARG,
+               "rlks_ppo_*_next: bad gather argument");
+  RLKS_REQUIRE(rlks_packed_stride(d) > 0, RLKS_ERR_UNSUPPORTED, "rlks_ppo_*_next: records of 2, 4 or 8 clouds only");
+  GatherArgs g;
+  if (int rc = gather_args(d, x->T, x->N, x->perm_seed, x->epoch, x->groups, x->group0, x->row0, x->rows, x->mb_dev, g))
+    return rc;
+  fused = d->precision == RLKS_PRECISION_SF16 && !is_wide(d) && x->groups <= NEXT_GROUPS;
+  n = NextGather{};
+  for (int k = 0; k < x->groups && k < NEXT_GROUPS; ++k) n.perm[k] = g.perm[k];
+  n.row0g = g.row0g;
+  n.rows = g.rows;
+  n.rows_g = g.rows_g;
+  n.Ng = g.Ng;
+  n.N = x->N;
+  n.mb = x->mb_dev;
+  n.packed = x->packed_dev;
+  return RLKS_OK;
+}
+
+static int gather_after(const rlks_mlp_desc* d, const rlks_gather_next* x, void* stream) {
+  return rlks_ppo_gather_packed(d, x->packed_dev, x->T, x->N, x->perm_seed, x->epoch, x->groups, x->group0, x->row0,
+                                x->rows, x->mb_dev, stream);
+}
+
 int rlks_ppo_sgd_step_next(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, float* params, const float* dyn,
                            const float* mb, int M, float* grad, double* stats, float* adam_m, float* adam_v,
                            int64_t n_params, float lr, float beta1, float beta2, float eps, int step, int prev_fused,
@@ -975,32 +1002,17 @@ int rlks_ppo_sgd_step_next(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, fl
     return rlks_ppo_sgd_step(d, co, params, dyn, mb, M, grad, stats, adam_m, adam_v, n_params, lr, beta1, beta2, eps,
                              step, prev_fused, workspace, ws_bytes, stream);
   if (int rc = check_desc(d)) return rc;
-  RLKS_REQUIRE(x->packed_dev && x->mb_dev && x->rows >= 0 && x->T > 0 && x->N > 0, RLKS_ERR_ARG,
-               "rlks_ppo_sgd_step_next: bad gather argument");
-  RLKS_REQUIRE(rlks_packed_stride(d) > 0, RLKS_ERR_UNSUPPORTED,
-               "rlks_ppo_sgd_step_next: records of 2, 4 or 8 clouds only");
-  GatherArgs g;
-  if (int rc = gather_args(d, x->T, x->N, x->perm_seed, x->epoch, x->groups, x->group0, x->row0, x->rows, x->mb_dev, g))
-    return rc;
-  const bool fused = d->precision == RLKS_PRECISION_SF16 && !is_wide(d) && x->groups <= NEXT_GROUPS;
+  NextGather n;
+  bool fused;
+  if (int rc = next_gather(d, x, n, fused)) return rc;
   if (!fused) {  // the two calls
     if (int rc = rlks_ppo_sgd_step(d, co, params, dyn, mb, M, grad, stats, adam_m, adam_v, n_params, lr, beta1, beta2,
                                    eps, step, prev_fused, workspace, ws_bytes, stream))
       return rc;
-    return rlks_ppo_gather_packed(d, x->packed_dev, x->T, x->N, x->perm_seed, x->epoch, x->groups, x->group0, x->row0,
-                                  x->rows, x->mb_dev, stream);
+    return gather_after(d, x, stream);
   }
   RLKS_REQUIRE(co && params && dyn && mb && grad && adam_m && adam_v && workspace && step >= 1, RLKS_ERR_ARG,
                "rlks_ppo_sgd_step: bad argument");
-  NextGather n{};
-  for (int k = 0; k < x->groups; ++k) n.perm[k] = g.perm[k];
-  n.row0g = g.row0g;
-  n.rows = g.rows;
-  n.rows_g = g.rows_g;
-  n.Ng = g.Ng;
-  n.N = x->N;
-  n.mb = x->mb_dev;
-  n.packed = x->packed_dev;
   FusedAdam fa{params, adam_m, adam_v, adam_co(lr, beta1, beta2, eps, step), step, prev_fused ? 1 : 0};
   return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
                  &fa, &n);
@@ -1021,6 +1033,28 @@ int rlks_ppo_grad_step(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const 
   FusedAdam fa{nullptr, nullptr, nullptr, AdamCo{}, step, prev_fused ? 1 : 0, false};
   return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
                  &fa);
+}
+
+int rlks_ppo_grad_step_next(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
+                            const float* mb, int M, float* grad, double* stats, int step, int prev_fused,
+                            const rlks_gather_next* x, void* workspace, int64_t ws_bytes, void* stream) {
+  if (!x)
+    return rlks_ppo_grad_step(d, co, params, dyn, mb, M, grad, stats, step, prev_fused, workspace, ws_bytes, stream);
+  if (int rc = check_desc(d)) return rc;
+  NextGather n;
+  bool fused;
+  if (int rc = next_gather(d, x, n, fused)) return rc;
+  if (!fused) {
+    if (int rc = rlks_ppo_grad_step(d, co, params, dyn, mb, M, grad, stats, step, prev_fused, workspace, ws_bytes,
+                                    stream))
+      return rc;
+    return gather_after(d, x, stream);
+  }
+  RLKS_REQUIRE(co && params && dyn && mb && grad && workspace && step >= 1, RLKS_ERR_ARG,
+               "rlks_ppo_grad_step: bad argument");
+  FusedAdam fa{nullptr, nullptr, nullptr, AdamCo{}, step, prev_fused ? 1 : 0, false};
+  return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
+                 &fa, &n);
 }
 
 int rlks_ppo_adam_apply(const rlks_mlp_desc* d, float* params, const float* grad, float* adam_m, float* adam_v,

@@ -18,7 +18,8 @@ One PPO iteration on one GPU (all launches on torch's current stream, no host sy
   update    num_sgd_iter x minibatches x (rlks_ppo_gather -> rlks_ppo_grad -> [all-reduce] ->
             rlks_adam_step); then rlks_kl_update from the mean KL over all SGD steps.  Single rank:
             rlks_ppo_sgd_step_next per minibatch (gradient + Adam, and the next minibatch's gather
-            inside the same reduce launch)
+            inside the same reduce launch); ranks: rlks_ppo_grad_step_next -> all-reduce ->
+            rlks_ppo_adam_apply
 Multi-GPU (torch.distributed, backend "nccl" = RCCL): each rank owns a contiguous block of lanes
 (env_offset = rank * lanes), the flat gradient and the few scalar sums are all-reduced.
 """
@@ -357,7 +358,7 @@ class PPO:
     def sgd_step(self, epoch, b, stat_row, gathered=False, next_mb=None):
         """one SGD step on minibatch b of epoch `epoch`.  gathered: the previous step's launch already
         gathered it (rlks_ppo_sgd_step_next); next_mb = (epoch, b) of the following step: gather it
-        inside this step's last launch (single rank, packed records)"""
+        inside this step's gradient-reduce launch (packed records)"""
         s = self.stream
         desc = C.byref(self.params.desc)
         beta1, beta2 = self.config.adam_betas
@@ -368,12 +369,12 @@ class PPO:
             _lib.call("rlks_ppo_gather_grouped", desc, C.byref(self.bufs), self.perm_seed(), epoch, self.groups,
                       self.group0, b * self.mb, self.mb, _lib.ptr(self.dyn), _lib.ptr(self.mbuf), s)
         self.adam_step += 1
+        nxt = None
+        if next_mb is not None:
+            ne, nb = next_mb
+            nxt = C.byref(_lib.GatherNext(_lib.ptr(self.packed), _lib.ptr(self.mbuf), self.perm_seed(), nb * self.mb,
+                                          self.T, self.N, ne, self.groups, self.group0, self.mb))
         if self.world == 1:  # no all-reduce between gradient and Adam: one fused launch sequence
-            nxt = None
-            if next_mb is not None:
-                ne, nb = next_mb
-                nxt = C.byref(_lib.GatherNext(_lib.ptr(self.packed), _lib.ptr(self.mbuf), self.perm_seed(),
-                                              nb * self.mb, self.T, self.N, ne, self.groups, self.group0, self.mb))
             _lib.call("rlks_ppo_sgd_step_next", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat),
                       _lib.ptr(self.dyn), _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row),
                       _lib.ptr(self.adam_m), _lib.ptr(self.adam_v), self.params.padded, float(self.config.lr),
@@ -383,9 +384,9 @@ class PPO:
             return
         # ranks: gradient -> all-reduce -> Adam, the Adam pass also leaving the next split's weight
         # maxima (rlks_ppo_grad_step / rlks_ppo_adam_apply: no weight-max pass per SGD step)
-        _lib.call("rlks_ppo_grad_step", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat), _lib.ptr(self.dyn),
-                  _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row), self.adam_step,
-                  int(self._fused_prev), _lib.ptr(self.ws), self.ws.numel(), s)
+        _lib.call("rlks_ppo_grad_step_next", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat),
+                  _lib.ptr(self.dyn), _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row),
+                  self.adam_step, int(self._fused_prev), nxt, _lib.ptr(self.ws), self.ws.numel(), s)
         self._allreduce(self.grad)
         _lib.call("rlks_ppo_adam_apply", desc, _lib.ptr(self.params.flat), _lib.ptr(self.grad), _lib.ptr(self.adam_m),
                   _lib.ptr(self.adam_v), self.params.padded, float(self.config.lr), float(beta1), float(beta2),
@@ -395,8 +396,8 @@ class PPO:
     def update(self):
         cfg = self.config
         steps = [(epoch, b) for epoch in range(cfg.num_sgd_iter) for b in range(self.n_mb)]
-        # single rank with packed records: each step's reduce launch also gathers the next minibatch
-        chain = self.world == 1 and self.packed is not None
+        # packed records: each step's gradient-reduce launch also gathers the next minibatch
+        chain = self.packed is not None
         for k, (epoch, b) in enumerate(steps):
             nxt = steps[k + 1] if chain and k + 1 < len(steps) else None
             self.sgd_step(epoch, b, self.stats[k], gathered=chain and k > 0, next_mb=nxt)

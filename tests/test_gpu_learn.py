@@ -399,7 +399,8 @@ def test_sgd_step_next_equals_step_then_gather(A, groups):
     """rlks_ppo_sgd_step_next (the next minibatch's packed gather run by extra blocks of the step's
     reduce launch, rewriting the minibatch buffer the step just read) leaves the parameters, Adam
     moments, stats and minibatch buffer of rlks_ppo_sgd_step + rlks_ppo_gather_packed, bit for bit,
-    over consecutive steps crossing an epoch; 16 lane groups exceed the fused form (two launches)"""
+    over consecutive steps crossing an epoch, and so does the multi-rank form rlks_ppo_grad_step_next
+    + rlks_ppo_adam_apply; 16 lane groups exceed the fused form (two launches)"""
     from rlks import _lib
     from rlks.policy import PolicyParams
 
@@ -421,7 +422,7 @@ def test_sgd_step_next_equals_step_then_gather(A, groups):
     wsb = C.c_int64()
     _lib.call("rlks_ppo_workspace_bytes", C.byref(desc), M, C.byref(wsb))
     run = {}
-    for k in ("ref", "nxt"):
+    for k in ("ref", "nxt", "rk"):
         p = PolicyParams(D, 256, A, device=d, seed=5)
         p.desc.precision = _lib.RLKS_PRECISION_SF16
         run[k] = dict(p=p, m=torch.zeros(p.padded, device=d), v=torch.zeros(p.padded, device=d),
@@ -439,22 +440,32 @@ def test_sgd_step_next_equals_step_then_gather(A, groups):
                 r["grad"].data_ptr(), r["stats"][k].data_ptr(), r["m"].data_ptr(), r["v"].data_ptr(), r["p"].padded,
                 3e-3, 0.9, 0.999, 1e-8, k + 1, int(k > 0))
 
-    ref, nxt = run["ref"], run["nxt"]
-    gather(ref, *steps[0])
-    gather(nxt, *steps[0])
+    ref, nxt, rk = run["ref"], run["nxt"], run["rk"]
+    for r in (ref, nxt, rk):
+        gather(r, *steps[0])
     for k in range(len(steps)):
         _lib.call("rlks_ppo_sgd_step", *step_args(ref, k), ref["ws"].data_ptr(), ref["ws"].numel(), None)
-        x = None
+        x = xr = None
         if k + 1 < len(steps):
             ne, nb = steps[k + 1]
             gather(ref, ne, nb)
             x = C.byref(_lib.GatherNext(packed.data_ptr(), nxt["mb"].data_ptr(), seed, nb * M, T, N, ne, groups, 0, M))
+            xr = C.byref(_lib.GatherNext(packed.data_ptr(), rk["mb"].data_ptr(), seed, nb * M, T, N, ne, groups, 0, M))
         _lib.call("rlks_ppo_sgd_step_next", *step_args(nxt, k), x, nxt["ws"].data_ptr(), nxt["ws"].numel(), None)
-        assert torch.equal(ref["mb"].view(torch.int32), nxt["mb"].view(torch.int32)), k
-        assert torch.equal(ref["p"].flat.view(torch.int32), nxt["p"].flat.view(torch.int32)), k
-        for key in ("m", "v", "grad"):
-            assert torch.equal(ref[key].view(torch.int32), nxt[key].view(torch.int32)), (k, key)
+        # the multi-rank form (one rank: the all-reduce is the identity)
+        a = step_args(rk, k)
+        _lib.call("rlks_ppo_grad_step_next", *a[:8], k + 1, int(k > 0), xr, rk["ws"].data_ptr(), rk["ws"].numel(),
+                  None)
+        _lib.call("rlks_ppo_adam_apply", C.byref(desc), rk["p"].flat.data_ptr(), rk["grad"].data_ptr(),
+                  rk["m"].data_ptr(), rk["v"].data_ptr(), rk["p"].padded, 3e-3, 0.9, 0.999, 1e-8, k + 1,
+                  rk["ws"].data_ptr(), rk["ws"].numel(), M, None)
+        for r in (nxt, rk):
+            assert torch.equal(ref["mb"].view(torch.int32), r["mb"].view(torch.int32)), k
+            assert torch.equal(ref["p"].flat.view(torch.int32), r["p"].flat.view(torch.int32)), k
+            for key in ("m", "v", "grad"):
+                assert torch.equal(ref[key].view(torch.int32), r[key].view(torch.int32)), (k, key)
     assert torch.equal(ref["stats"], nxt["stats"])
+    assert torch.equal(ref["stats"], rk["stats"])
 
 
 # ----------------------------------------------------------------------------- end to end
