@@ -10,10 +10,7 @@ namespace rlks {
 constexpr int SF_F1_W = RLKS_F1_W;  // waves per F1 workgroup (one per SIMD); 32 rows each
 constexpr int SF_PMAX = 1024;       // weight-max entries per (parity, kind)
 constexpr int SF_DZ_SLOTS = 64, SF_DZ_STRIDE = 16;
-#ifndef RLKS_W2_PAD
-#define RLKS_W2_PAD 0
-#endif
-constexpr int SF_W2_PSTRIDE = 256 * 256 + RLKS_W2_PAD;  // floats between F2's dW2 partials  // max |dZ2| partial maxima (sgd_sf16.hip dz_slot)
+constexpr int SF_W2_PSTRIDE = 256 * 256;  // floats between F2's dW2 partials (padding them apart: no gain)  // max |dZ2| partial maxima (sgd_sf16.hip dz_slot)
 }  // namespace rlks
 
 namespace rlks {
