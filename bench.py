@@ -157,11 +157,9 @@ def kernel_timing(algo, torch, config="c2", reps=20):
         peak, peak_name = SF16_PEAK_TFLOPS, "frac_sf16_mfma"
     elif algo.precision == "sf16":
         phase(_lib.RLKS_PHASE_ALL)()  # weight splits + dZ2 in place for the per-phase timings
-        if _lib.lib().rlks_sf_f1_split():  # F1 as k_sf_fwd + k_sf_bwd: each timed alone, and the pair
-            f1 = (("k_sf_fwd", _lib.RLKS_PHASE_F1A), ("k_sf_bwd", _lib.RLKS_PHASE_F1B),
-                  ("f1_total", _lib.RLKS_PHASE_FWD_PI | _lib.RLKS_PHASE_FWD_VF))
-        else:
-            f1 = (("k_sf_fwdbwd", _lib.RLKS_PHASE_FWD_PI | _lib.RLKS_PHASE_FWD_VF),)
+        # F1 = k_sf_fwd (F1a) + k_sf_bwd (F1b): each timed alone, and the pair
+        f1 = (("k_sf_fwd", _lib.RLKS_PHASE_F1A), ("k_sf_bwd", _lib.RLKS_PHASE_F1B),
+              ("f1_total", _lib.RLKS_PHASE_FWD_PI | _lib.RLKS_PHASE_FWD_VF))
         phases = (("k_sf_prep", _lib.RLKS_PHASE_PREP), *f1,
                   ("k_sf_dw2", _lib.RLKS_PHASE_DW2), ("k_reduce", _lib.RLKS_PHASE_REDUCE))
         peak, peak_name = SF16_PEAK_TFLOPS, "frac_sf16_mfma"
@@ -420,6 +418,8 @@ def main():
     value = steps_total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
+    # multi-rank: one more (untimed) iteration with events around every gradient all-reduce
+    allreduce = algo.profile_allreduce() if world > 1 else None
     kernels = None if args.no_kernel_timing else kernel_timing(algo, torch, args.config)
     # sanity: the policy is learning something finite
     st = algo.stats.cpu().numpy()
@@ -466,7 +466,7 @@ def main():
                        "envs_per_gpu": envs, "rollout_steps": args.rollout, "minibatch_per_gpu": algo.mb,
                        "epochs": args.epochs, "global_batch": algo.samples * world, "sgd_precision": algo.precision,
                        "parallelism": f"dp{world}"},
-            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "finite": finite,
+            "roofline": roofline, "cpu_baseline": cpu, "allreduce": allreduce, "kernels": kernels, "finite": finite,
         }
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -65,6 +65,12 @@ int rlks_env_seed(rlks_env* env, const uint8_t* mask_dev, const uint32_t* keys_d
  * MT19937 mode only).  Batched evaluation uses it to give lane e the stream position of episode e
  * of the reference's sequential loop (final_evaluation.py:42-49, one process-global generator). */
 int rlks_env_mt_discard(rlks_env* env, const uint8_t* mask_dev, const int64_t* n_draws_dev, void* stream);
+/* Lane's MT19937 state as CPython's random.getstate()[1] lays it out: 624 words then the position
+ * (0..624), copied to (to_env = 0) or from (to_env = 1) words_dev[625] (MT19937 mode only).  The
+ * drop-in env's "global" noise stream keeps the lane in step with the process-global `random`
+ * module this way: the reference draws its cpu noise from it (k8s_multi_cloud_env.py:87) and
+ * reseeds it in reset (:109-111). */
+int rlks_env_mt_words(rlks_env* env, int lane, uint32_t* words_dev, int to_env, void* stream);
 
 /* reset() (:106-112) for the lanes in mask (NULL = all): current_step = 0, obs of row 0. */
 int rlks_env_reset(rlks_env* env, const uint8_t* mask_dev, float* obs_dev, void* stream);
@@ -88,6 +94,14 @@ int rlks_env_step(rlks_env* env, const int32_t* actions_dev, float* obs_dev, dou
 int rlks_env_sample_step(rlks_env* env, const float* logits_dev, int explore, int32_t* actions_dev,
                          float* logp_dev, float* obs_next_dev, float* reward_dev, uint8_t* done_dev,
                          void* stream);
+
+/* TorchCategorical sample (explore != 0) or argmax of rows i < n of logits_dev[n][A]: the draw of
+ * row i is Philox4x32-10 of the counter {ids[3i], ids[3i + 1], ids[3i + 2], RLKS_PURPOSE_ACTION << 16}
+ * under key = seed, turned into an action exactly as rlks_env_sample_step does (ids may be NULL
+ * when explore = 0); logp_dev (may be NULL) gets log pi(action).  compute_single_action(obs) with
+ * exploration (eval_ppo.py:27) keys its draw by (config seed, call counter). */
+int rlks_sample_categorical(const float* logits_dev, int n, int A, const uint32_t* ids_dev, unsigned long long seed,
+                            int explore, int32_t* actions_dev, float* logp_dev, void* stream);
 
 /* Sum of completed-episode returns and their count over all lanes (double[2]); clear != 0
  * zeroes the accumulators (PPO result "episode_reward_mean", train_ppo.py:29-30). */
@@ -244,10 +258,6 @@ int rlks_ppo_grad(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, cons
 int rlks_ppo_grad_phases(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
                          const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
                          void* workspace_dev, int64_t workspace_bytes, int phases, void* stream);
-
-/* 1 when the split-fp16 F1 runs as the k_sf_fwd + k_sf_bwd pair (the default; RLKS_F1_SPLIT=0 selects
- * the fused one-wave-per-SIMD k_sf_fwdbwd), 0 otherwise.  Profiling / reporting only. */
-int rlks_sf_f1_split(void);
 
 /* torch.optim.Adam step (lerp form of exp_avg, bias-corrected), in place on n floats */
 int rlks_adam_step(float* params_dev, const float* grad_dev, float* m_dev, float* v_dev, int64_t n,

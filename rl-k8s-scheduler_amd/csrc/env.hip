@@ -144,13 +144,9 @@ __global__ void k_env_step(EnvView v, const double* __restrict__ cost, const dou
 // (cfg.skip_returns = 0) and 1 + 4 for the optional truncated / step outputs.
 // Outputs are written with non-temporal (streaming) stores: nothing reads them back before they
 // leave the cache, and at 16M lanes that took the step from 0.195 to 0.130 ms (4.2 -> 6.3 TB/s).
-#ifndef RLKS_ENV_NT
-#define RLKS_ENV_NT 1
-#endif
 template <typename V>
 __device__ __forceinline__ void st_stream(V* p, V x) {
-  if constexpr (RLKS_ENV_NT) __builtin_nontemporal_store(x, p);
-  else *p = x;
+  __builtin_nontemporal_store(x, p);
 }
 
 __device__ __forceinline__ void obs_row2(const EnvView& v, const double* __restrict__ cost,
@@ -483,6 +479,44 @@ __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __re
   if (status && (threadIdx.x & 63) == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
 }
 
+// TorchCategorical over the A logits l[0..A): explore -> u = f32(u53(Philox(ctr, key) words 0, 1)) *
+// sum exp(l - max), the first a with u < cumsum; else argmax.  logp of the choice.  Shared by the
+// rollout's fused sample + step and the standalone sampler (oracle.sample_actions restates it).
+__device__ __forceinline__ int categorical(const float* __restrict__ l, int A, bool explore, u32x4 ctr, uint32_t k0,
+                                          uint32_t k1, float& logp) {
+  float mx = l[0];
+  int amax = 0;
+  for (int a = 1; a < A; ++a)
+    if (l[a] > mx) { mx = l[a]; amax = a; }
+  float s = 0.f;
+  for (int a = 0; a < A; ++a) s += expf(l[a] - mx);
+  int act = amax;
+  if (explore) {
+    const u32x4 x = philox4x32_10(ctr, k0, k1);
+    const float u = (float)u53(x.x, x.y) * s;
+    float c = 0.f;
+    act = A - 1;
+    for (int a = 0; a < A; ++a) {
+      c += expf(l[a] - mx);
+      if (u < c) { act = a; break; }
+    }
+  }
+  logp = l[act] - mx - logf(s);
+  return act;
+}
+
+// rows i < n: ctr = {ids[3i], ids[3i + 1], ids[3i + 2], ACTION << 16}
+__global__ void k_sample_categorical(const float* __restrict__ logits, int n, int A, const uint32_t* __restrict__ ids,
+                                     uint32_t k0, uint32_t k1, int explore, int32_t* __restrict__ actions,
+                                     float* __restrict__ logp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float lp;
+  const u32x4 ctr{ids[3 * i], ids[3 * i + 1], ids[3 * i + 2], (uint32_t)RLKS_PURPOSE_ACTION << 16};
+  actions[i] = categorical(logits + (size_t)i * A, A, explore != 0, ctr, k0, k1, lp);
+  if (logp) logp[i] = lp;
+}
+
 // TorchCategorical sample / argmax over A logits, then step
 __global__ void k_sample_step(EnvView v, const double* __restrict__ cost, const double* __restrict__ lat,
                               const float* __restrict__ logits, int explore, int32_t* __restrict__ actions,
@@ -492,31 +526,12 @@ __global__ void k_sample_step(EnvView v, const double* __restrict__ cost, const 
   stage_tables(s_tab, cost, lat, v.T * v.C);
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= v.N) return;
-  const int A = v.C;
-  const float* l = logits + (size_t)lane * A;
-  float mx = l[0];
-  int amax = 0;
-  for (int a = 1; a < A; ++a)
-    if (l[a] > mx) { mx = l[a]; amax = a; }
-  float s = 0.f;
-  for (int a = 0; a < A; ++a) s += expf(l[a] - mx);
-  int act = amax;
-  if (explore) {
-    const int t = v.step[lane];
-    const int ep = v.episode[lane];
-    u32x4 x = philox4x32_10(u32x4{(uint32_t)(v.env_offset + lane), (uint32_t)ep, (uint32_t)t,
-                                  (uint32_t)RLKS_PURPOSE_ACTION << 16},
-                            v.k0, v.k1);
-    const float u = (float)u53(x.x, x.y) * s;
-    float c = 0.f;
-    act = A - 1;
-    for (int a = 0; a < A; ++a) {
-      c += expf(l[a] - mx);
-      if (u < c) { act = a; break; }
-    }
-  }
+  const u32x4 ctr{(uint32_t)(v.env_offset + lane), (uint32_t)v.episode[lane], (uint32_t)v.step[lane],
+                  (uint32_t)RLKS_PURPOSE_ACTION << 16};
+  float lp;
+  const int act = categorical(logits + (size_t)lane * v.C, v.C, explore != 0, ctr, v.k0, v.k1, lp);
   actions[lane] = act;
-  logp[lane] = l[act] - mx - logf(s);
+  logp[lane] = lp;
   StepOut r = step_lane(v, s_tab, lane, act, obs + (size_t)lane * 3 * v.C, nullptr);
   rew[lane] = (float)r.reward;
   done[lane] = (uint8_t)r.done;
@@ -839,6 +854,33 @@ int rlks_env_lane_state(rlks_env* e, int32_t* steps, int32_t* episodes, void* st
   hipLaunchKernelGGL(k_lane_state, dim3(cdiv(e->cfg.n_envs, ENV_BLOCK)), dim3(ENV_BLOCK), 0,
                      (hipStream_t)stream, e->cfg.n_envs, e->d_step, e->d_episode, steps, episodes);
   RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_sample_categorical(const float* logits, int n, int A, const uint32_t* ids, unsigned long long seed, int explore,
+                            int32_t* actions, float* logp, void* stream) {
+  RLKS_REQUIRE(logits && actions && n >= 0 && A >= 1 && (ids || !explore), RLKS_ERR_ARG,
+               "rlks_sample_categorical: bad argument");
+  if (n == 0) return RLKS_OK;
+  hipLaunchKernelGGL(k_sample_categorical, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, logits, n, A, ids,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), explore, actions, logp);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int rlks_env_mt_words(rlks_env* e, int lane, uint32_t* words, int to_env, void* stream) {
+  RLKS_REQUIRE(e && words, RLKS_ERR_ARG, "rlks_env_mt_words: null argument");
+  RLKS_REQUIRE(e->d_mt, RLKS_ERR_ARG, "rlks_env_mt_words: the env is not in MT19937 noise mode");
+  RLKS_REQUIRE(lane >= 0 && lane < e->cfg.n_envs, RLKS_ERR_ARG, "rlks_env_mt_words: lane out of range");
+  // lane's word k at d_mt[k * n_envs + lane]: a 625-row column, 4 bytes wide
+  const size_t pitch = (size_t)e->cfg.n_envs * sizeof(uint32_t);
+  uint32_t* col = e->d_mt + lane;
+  if (to_env)
+    RLKS_HIP(hipMemcpy2DAsync(col, pitch, words, sizeof(uint32_t), sizeof(uint32_t), MT_N + 1, hipMemcpyDeviceToDevice,
+                              (hipStream_t)stream));
+  else
+    RLKS_HIP(hipMemcpy2DAsync(words, sizeof(uint32_t), col, pitch, sizeof(uint32_t), MT_N + 1, hipMemcpyDeviceToDevice,
+                              (hipStream_t)stream));
   return RLKS_OK;
 }
 

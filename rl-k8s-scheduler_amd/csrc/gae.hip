@@ -18,13 +18,8 @@ namespace rlks {
 constexpr int GAE_BLOCK = 256;
 // 64 lanes (256-byte rows) per scan workgroup: 128 x 131,072 (c4) in 56 us vs 68 us at 32 lanes,
 // 128 x 4,096 (c2) in 6.1 vs 5.5 us
-#ifndef RLKS_GAE_LANES
-#define RLKS_GAE_LANES 64
-#endif
-#ifndef RLKS_GAE_SERIAL_T
-#define RLKS_GAE_SERIAL_T 256
-#endif
-constexpr int GAE_LANES = RLKS_GAE_LANES;  // lanes per advantage-sum partial (and per scan workgroup)
+constexpr int GAE_LANES = 64;       // lanes per advantage-sum partial (and per scan workgroup)
+constexpr int GAE_SERIAL_T = 256;   // longer rollouts (c1's single 4,000-step lane) run the serial recurrence
 constexpr int GAE_MAX_SEG = 16;  // time segments per scan workgroup
 
 // per-partial (GAE_LANES-lane group) sums of a and a^2: scan workgroups are one group (thread =
@@ -185,7 +180,7 @@ int rlks_gae(const float* rewards, const float* values, const uint8_t* dones, fl
   RLKS_REQUIRE(T > 0 && N > 0, RLKS_ERR_ARG, "rlks_gae: T and N must be positive");
   hipStream_t s = (hipStream_t)stream;
   const float gl = gamma * lam;
-  if (T > RLKS_GAE_SERIAL_T) {
+  if (T > GAE_SERIAL_T) {
     hipLaunchKernelGGL(k_gae, dim3(cdiv(N, GAE_BLOCK)), dim3(GAE_BLOCK), 0, s, rewards, values, dones, gamma, gl, T,
                        N, adv, vtarg, partials);
   } else if (T <= 8 * GAE_MAX_SEG) {

@@ -152,10 +152,8 @@ struct Reducer {
     t.mslot = mslot;
     t.mbase = 0;
     int G = 1;
-#ifndef RLKS_RED_PPT
-#define RLKS_RED_PPT 32  // partials per thread (c4 reduce: 16 -> 19.0 us, 32 -> 19.0 us, 8 -> 23.9 us)
-#endif
-    while (G < 256 && G * RLKS_RED_PPT < P) G *= 2;
+    constexpr int PPT = 32;  // partials per thread (c4 reduce: 16 -> 19.0 us, 32 -> 19.0 us, 8 -> 23.9 us)
+    while (G < 256 && G * PPT < P) G *= 2;
     const bool vec = len % 4 == 0 && pstride % 4 == 0 && ((uintptr_t)part & 15) == 0;
     t.part = part; t.out = out; t.out64 = out64; t.pstride = pstride; t.P = P; t.len = len; t.G = G;
     t.V = vec ? 4 : 1;
@@ -455,13 +453,11 @@ struct SfWs {
 
 static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   SfWs w{};
-  const int KD = sf_kd(D), tiles = M / 32;
-  w.blocks = M / (32 * SF_F1_W);  // F1 workgroups of SF_F1_W x 32 rows
+  const int KD = sf_kd(D), tiles = M / 32;  // F2's 32-row tiles
+  w.blocks = M / (16 * SF_F1_W);  // F1 workgroups of SF_F1_W x 16 rows
   w.splits = 1;
-#ifndef RLKS_F2_MAX_SPLITS
-#define RLKS_F2_MAX_SPLITS 128
-#endif
-  while (w.splits * 2 <= RLKS_F2_MAX_SPLITS && tiles % (w.splits * 2) == 0) w.splits *= 2;
+  constexpr int F2_MAX_SPLITS = 128;  // F2 row splits per net (one 512-thread workgroup each)
+  while (w.splits * 2 <= F2_MAX_SPLITS && tiles % (w.splits * 2) == 0) w.splits *= 2;
   w.tiles_per_split = tiles > 0 ? tiles / w.splits : 0;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -494,12 +490,12 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     const int An = net == 0 ? A : 1;
     SfNet& n = w.n[net];
     n.dz2t = (float*)take(4LL * M * HID);
-    n.tile_edz = (int*)take(4LL * tiles);
+    n.tile_edz = (int*)take(4LL * (M / 16));
     n.part_w1 = (float*)take(4LL * w.blocks * HID * D);
     n.part_b1 = (float*)take(4LL * w.blocks * HID);
-    n.part_w3 = (float*)take(4LL * tiles * An * HID);
-    n.part_b3 = (float*)take(4LL * tiles * An);
-    n.part_stat = (float*)take(4LL * tiles * 4);
+    n.part_w3 = (float*)take(4LL * w.blocks * An * HID);
+    n.part_b3 = (float*)take(4LL * w.blocks * An);
+    n.part_stat = (float*)take(4LL * w.blocks * 4);
     n.part_w2 = (float*)take(4LL * w.splits * SF_W2_PSTRIDE);
     n.part_b2 = (float*)take(4LL * w.splits * HID);
   }
@@ -807,11 +803,11 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     R.add(n.part_b1, grad + o[1], nullptr, H, w.blocks, H, 2 * net + 1);
     R.add(n.part_w2, grad + o[2], nullptr, SF_W2_PSTRIDE, w.splits, H * H, 2 * net);
     R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
-    R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, M / 32, An * H);
-    R.add(n.part_b3, grad + o[5], nullptr, An, M / 32, An);
+    R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, w.blocks, An * H);
+    R.add(n.part_b3, grad + o[5], nullptr, An, w.blocks, An);
   }
-  if (stats) {  // per-tile columns [policy loss, vf loss, kl, entropy] -> RLKS_STAT_* directly
-    const int tiles = M / 32;
+  if (stats) {  // per-block columns [policy loss, vf loss, kl, entropy] -> RLKS_STAT_* directly
+    const int tiles = w.blocks;
     R.add(w.n[0].part_stat + 0, nullptr, stats + RLKS_STAT_POLICY_LOSS, 4, tiles, 1);
     R.add(w.n[1].part_stat + 1, nullptr, stats + RLKS_STAT_VF_LOSS, 4, tiles, 1);
     R.add(w.n[0].part_stat + 2, nullptr, stats + RLKS_STAT_KL, 4, tiles, 1);
@@ -932,8 +928,6 @@ int rlks_ppo_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float
                   void* stream) {
   return rlks_ppo_grad_phases(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, stream);
 }
-
-int rlks_sf_f1_split(void) { return sf_f1_split() ? 1 : 0; }
 
 static AdamCo adam_co(float lr, float beta1, float beta2, float eps, int step) {
   const double bc1 = 1.0 - std::pow((double)beta1, step);

@@ -4,10 +4,7 @@
 #include "mlp_common.h"
 
 namespace rlks {
-#ifndef RLKS_F1_W
-#define RLKS_F1_W 4
-#endif
-constexpr int SF_F1_W = RLKS_F1_W;  // waves per F1 workgroup (one per SIMD); 32 rows each
+constexpr int SF_F1_W = 8;          // waves per F1 workgroup (two workgroups per CU); 16 rows each
 constexpr int SF_PMAX = 1024;       // weight-max entries per (parity, kind)
 constexpr int SF_DZ_SLOTS = 64, SF_DZ_STRIDE = 16;
 constexpr int SF_W2_PSTRIDE = 256 * 256;  // floats between F2's dW2 partials (padding them apart: no gain)  // max |dZ2| partial maxima (sgd_sf16.hip dz_slot)
@@ -41,10 +38,10 @@ struct SfNet {
   const _Float16 *w1h, *w1l, *w2ph, *w2pl, *w2th, *w2tl;
   const float* sc;
   unsigned* dzmax;
-  float* dz2t;  // [M/32][HID][32]
-  int* tile_edz;  // [M/32] split F1: each tile's dZ2 split exponent (F1a -> F1b)
-  float *part_w1, *part_b1;                 // [F1 blocks][...]
-  float *part_w3, *part_b3, *part_stat;     // [tiles of 32 rows][...]
+  float* dz2t;    // [M/16 tiles][8 n-steps][64 lanes][8]: dZ2 in F1a's lane order (sgd_sf16.hip F1)
+  int* tile_edz;  // [M/16]: each 16-row tile's dZ2 split exponent (F1a -> F1b)
+  float *part_w1, *part_b1;                 // [F1 blocks of 128 rows][...] (F1b)
+  float *part_w3, *part_b3, *part_stat;     // [F1 blocks of 128 rows][...] (F1a)
   float *part_w2, *part_b2;                                   // [splits][...]
 };
 struct SfArgs {
@@ -82,14 +79,9 @@ struct SfRollArgs {
 };
 int launch_sf_roll(const SfRollArgs& a, int mode, hipStream_t s);
 
-size_t sf_f1_lds_bytes(int A_, int NG, int KD, int W);
-#ifndef RLKS_F1_SPLIT_DEFAULT
-#define RLKS_F1_SPLIT_DEFAULT 1
-#endif
-bool sf_f1_split();
 int sf_kd(int D);
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
-// halves (split F1 only): 1 = k_sf_fwd, 2 = k_sf_bwd, 3 = both; the fused kernel ignores it
+// halves: 1 = F1a (k_sf_fwd), 2 = F1b (k_sf_bwd), 3 = both
 int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int halves = 3);  // needs M % 256 == 0
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
 

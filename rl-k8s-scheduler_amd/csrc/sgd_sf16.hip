@@ -39,12 +39,6 @@ using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
 using v4u = __attribute__((ext_vector_type(4))) unsigned;  // 16-byte staging register (a vector, not HIP's uint4 struct, so it stays in VGPRs)
 
-#ifndef RLKS_F1B_ONEPASS
-#define RLKS_F1B_ONEPASS 1
-#endif
-#ifndef RLKS_F2_PHASES
-#define RLKS_F2_PHASES 1
-#endif
 constexpr int SF_ROWS = 256;        // minibatch rows must be a multiple of this
 constexpr int SF_CH = 8192;         // halves per staged chunk (per hi / lo array)
 constexpr float SF_H1_SCALE = 16384.f;  // tanh outputs (|h| < 1) scaled by 2^14
@@ -56,6 +50,8 @@ __device__ __forceinline__ unsigned* dz_slot(unsigned* base, int tile) {
 }
 
 __device__ __forceinline__ int sf_perm(int s, int h, int j) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
+// P16: element p = 8g + j of a 16x16x32 k-fragment taken from two stacked accumulator tiles
+__device__ __forceinline__ int p16(int p) { return 16 * ((p >> 2) & 1) + 4 * (p >> 3) + (p & 3); }
 
 __device__ __forceinline__ f32x16 mma(h8 a, h8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -185,7 +181,7 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
   for (int j = 0; j < 4; ++j) {
     const int i = base + j * 256 + tid;
     const int row = i >> 8, c = i & 255, blk = c >> 5, rem = c & 31;
-    const int src = 32 * blk + sf_perm(rem >> 4, (rem >> 3) & 1, rem & 7);
+    const int src = 32 * blk + p16(rem);  // F1's P16 fragment order (k_sf_fwd / k_sf_bwd)
     vp[j] = N.w2[row * HID + src];  // w2p[n = row][k perm]
     vt[j] = N.w2[src * HID + row];  // w2t[k = row][n perm]
     vr[j] = 0.f;
@@ -269,54 +265,14 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
     N.sc[2] = s2; N.sc[3] = 1.f / s2; N.sc[5] = (float)e2;
     for (int i = 0; i < SF_DZ_SLOTS; ++i) N.dzmax[i * SF_DZ_STRIDE] = 0u;
   }
-  if (blockIdx.y == 0) {  // the other parity's entries: the coming fused reduce writes some of them
+  // the other parity's entries: the coming fused reduce writes some of them.  The rollout's prep
+  // (write_roll) has slots of its own and leaves the SGD steps' parity state (entries and tags) alone.
+  if (blockIdx.y == 0 && !g.write_roll) {
     float4* z = reinterpret_cast<float4*>(N.pmax + (g.parity ^ 1) * 2 * SF_PMAX);
     for (int i = tid; i < 2 * SF_PMAX / 4; i += 256) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  if (blockIdx.y == 0 && tid == 0) N.tag[g.parity ^ 1] = 0u;
-}
-
-// ----------------------------------------------------------------------------- F1
-// Weight chunks staged through registers: a wave loads its share of chunk c + 1 at the start of
-// a step (global_load_dwordx4 into 32 / W x 16 B per lane) and writes it to the idle LDS buffer at
-// the end.  (LDS-DMA, global_load_lds, would save the registers, but while one is in flight the
-// compiler waits for every outstanding LDS read, lgkmcnt(0), before any LDS result is used, which
-// serialises the fragment pipeline below.)  Chunk c < 8: w2p columns [32c, 32c+32) of all 256
-// rows (Z2 loop, k-tile c); c >= 8: w2t columns [32(c-8), +32) of all 256 rows (dH1 loop, n-tile
-// c - 8).  Both are [256 rows][32 halves] images with 16-byte pieces XOR-swizzled by
-// (row >> 2) & 3, read by sf_frag.  A chunk is 2 x 1024 slots of 16 B (hi, lo) = 32 blocks of 64;
-// wave w of W moves blocks (32/W) w + i.
-template <int W>
-__device__ __forceinline__ void chunk_load(const SfNet& N, int c, int w, int l, v4u (&v)[32 / W]) {
-  const bool p = c < 8;
-  const int col = 32 * (p ? c : c - 8);
-#pragma unroll
-  for (int i = 0; i < 32 / W; ++i) {
-    const int blk = (32 / W) * w + i, arr = blk >> 4, sig = (blk & 15) * 64 + l;
-    const int row = sig >> 2, pc = (sig & 3) ^ ((row >> 2) & 3);
-    const _Float16* src = (p ? (arr ? N.w2pl : N.w2ph) : (arr ? N.w2tl : N.w2th)) + row * HID + col + 8 * pc;
-    v[i] = *reinterpret_cast<const v4u*>(src);
+    if (tid == 0) N.tag[g.parity ^ 1] = 0u;
   }
 }
-template <int W>
-__device__ __forceinline__ void chunk_store(_Float16* buf, int w, int l, const v4u (&v)[32 / W]) {
-#pragma unroll
-  for (int i = 0; i < 32 / W; ++i) {
-    const int blk = (32 / W) * w + i, arr = blk >> 4;
-    *reinterpret_cast<v4u*>(buf + arr * SF_CH + ((blk & 15) * 64 + l) * 8) = v[i];
-  }
-}
-// the (hi, lo) fragments of one 32-row block of a chunk for both k-steps s: lane (r, h) of row
-// `row` gets halves [16 s + 8 h, +8) of its 32
-__device__ __forceinline__ void sf_frag(const _Float16* buf, int row, int h, h8 (&f)[2][2]) {
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int off = row * 32 + 8 * ((2 * s + h) ^ ((row >> 2) & 3));
-    f[s][0] = *reinterpret_cast<const h8*>(buf + off);
-    f[s][1] = *reinterpret_cast<const h8*>(buf + SF_CH + off);
-  }
-}
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // PPO loss of one row (RLlib ppo_torch_policy semantics): d loss / d logits (pi) or
 // d loss / d value (vf), scaled by 1 / global rows, and the row's [policy loss, vf loss, kl,
@@ -380,678 +336,325 @@ __device__ __forceinline__ void sf_loss(const SfArgs& g, const float (&out)[A_],
   }
 }
 
+
 #ifdef RLKS_STAMPS
-// diagnostic build only (tools/stamps.sh): per-wave phase clocks of F1, [net][tile][phase]
-__device__ unsigned long long g_sf_stamps[2][4096][8];
-#define SF_STAMP(i) \
-  if (l == 0 && tile < 4096) g_sf_stamps[NET][tile][i] = __builtin_amdgcn_s_memtime()
-// loop-internal clocks: Z2 chunk 3 (top, after the MFMA steps, after the barrier) and dH1 n-tile 3
-__device__ unsigned long long g_sf_stamps2[2][4096][8];
-#define SF_STAMP2(i) \
-  if (l == 0 && tile < 4096) g_sf_stamps2[NET][tile][i] = __builtin_amdgcn_s_memtime()
-// F1a (k_sf_fwd) phase clocks [net][tile][phase]; slot 7 = HW_ID | XCC_ID << 32
-__device__ unsigned long long g_fa_stamps[2][4096][8];
+// diagnostic build only (make -C csrc stamps, tools/stamps.py): F1a (k_sf_fwd) phase clocks of
+// lane 0 of every wave, [net][tile][phase]; slot 7 = HW_ID | XCC_ID << 32
+__device__ unsigned long long g_fa_stamps[2][8192][8];
 #define FA_STAMP(i) \
-  if (l == 0 && tile < 4096) g_fa_stamps[NET][tile][i] = __builtin_amdgcn_s_memtime()
+  if (l == 0 && tile < 8192) g_fa_stamps[NET][tile][i] = __builtin_amdgcn_s_memtime()
 #define FA_HWID()                                                                                   \
-  if (l == 0 && tile < 4096)                                                                        \
+  if (l == 0 && tile < 8192)                                                                        \
   g_fa_stamps[NET][tile][7] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |       \
                               ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32)
 #else
-#define SF_STAMP(i)
-#define SF_STAMP2(i)
 #define FA_STAMP(i)
 #define FA_HWID()
 #endif
 
-// W waves per workgroup, one 32-row tile each; one wave per SIMD (waves_per_eu 1) so that every
-// wave has the full 512-register file: dZ2^T stays split in registers through the dH1 loop and
-// the LDS fragments of the next MFMA step are in flight during the current one.
-template <int A_, int NET, int KD, int NG, int W>
-__device__ __forceinline__ void sf_fwdbwd_body(const SfArgs& g) {
-  constexpr int NTHR = 64 * W;
-  constexpr int KS = KD / 16;   // k-steps of the first layer
-  // NG: accumulator row groups (8 rows each) holding the rows d <= D of dW1a^T.  Each k-tile's
-  // dW1a^T block goes to an LDS slot (the epilogue reuses the chunk buffers) and is summed over the
-  // W waves there, so no accumulator outlives its k-tile.
-  constexpr int DWR = 8 * NG;   // LDS rows per dW1a^T column
-  const SfNet& N = g.n[NET];
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  _Float16* sCh = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][SF_CH]  (64 KB)
-  float* sB2 = lds + 2 * SF_CH;                      // [HID]
-  float* sW3 = sB2 + HID;                            // [A_][HID]
-  _Float16* sW1 = reinterpret_cast<_Float16*>(sW3 + A_ * HID);  // [2 hi/lo][HID k][KD] (swizzled)
-  h8* sXT = reinterpret_cast<h8*>(sW1 + 2 * HID * KD);          // [W][2 s][2 hi/lo][64 lanes]
+// ----------------------------------------------------------------------------- F1 (16-row tiles)
+// One wave per 16-row tile on v_mfma_f32_16x16x32_f16, eight waves per workgroup (128 rows), two
+// workgroups per CU: the per-wave state is the 256 x 16 accumulator block (64 registers), so a
+// kernel fits 128 registers and every SIMD interleaves four waves (the 32-row tiles of round 2
+// needed 256 registers, two waves per SIMD, and waited on their own dependency chains).
+//
+// Fragments (lane l, c = l & 15, g = l >> 4): A[row c][k = 8g + j], B[k = 8g + j][col c] (j < 8),
+// C[row 4g + i][col c] (i < 4).  A 32-row block held as two accumulator tiles gives a lane the rows
+// 4g + i and 16 + 4g + i: as the next product's B (or A) operand, element j of its k-fragment is
+// row P16(8g + j) = 16 (j >> 2) + 4g + (j & 3) of the block.  The prep writes W2 with each 32-block
+// of columns in that order (k_sf_split), so
+//   F1a (k_sf_fwd): Z1^T = W1a Xa^T (two tiles) -> tanh -> split = B of Z2^T = W2 H1^T (A = w2p:
+//     rows n, columns k in P16 order); H2^T, head, PPO loss, dW3 / db3 / stats (workgroup sums),
+//     dZ2^T = (dl W3)(1 - H2^2) -> HBM in the lane's own order, the tile's max |dZ2|;
+//   F1b (k_sf_bwd): dH1 = dZ2 W2 (A = dZ2 read back by the same lane that wrote it, B = w2t: rows
+//     k, columns n in P16 order); Z1 = Xa W1a^T in dH1's layout -> dZ1 = dH1 (1 - H1^2) ->
+//     dW1a^T = Xa^T dZ1 on v_mfma_f32_16x16x16_f16 (B = the dZ1 tile as it stands: K = its rows m).
+using f4 = __attribute__((ext_vector_type(4))) float;
+using v4f = __attribute__((ext_vector_type(4))) float;
 
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
-  const int D = g.D, stride = g.x_stride;
-  const int tile = blockIdx.x * W + w, row0 = tile * 32;
-  SF_STAMP(0);
-
-  {
-    v4u cv[32 / W];
-    chunk_load<W>(N, 0, w, l, cv);
-    chunk_store<W>(sCh, w, l, cv);
-  }
-  for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i];
-  for (int i = tid; i < A_ * HID; i += NTHR) sW3[i] = N.w3[i];
-
-  // ---- this wave's rows: Xa = [X | 1 | 0] fragments, lane row m = r, d = 16ks + 8h + j
-  float xv[KS * 8];
-  const float* xr = g.x + (size_t)(row0 + r) * stride;
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int d = 16 * ks + 8 * h + j;
-      xv[ks * 8 + j] = xa_elem(xr, d, D);
-    }
-  float xm = 0.f;
-#pragma unroll
-  for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
-  const int ex = sf_exp(wave_max(xm));
-  const float sx = pow2(ex);
-  h8 xh[KS], xl[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) split8(xv, ks * 8, sx, xh[ks], xl[ks]);
-  const float inv_w1 = N.sc[1], inv_w2 = N.sc[3];
-  const int e_w2 = (int)N.sc[5];
-  const float inv_z1 = inv_w1 / sx;  // Z1 accumulators carry s_x s_w1
-
-  // W1a (hi, lo) in LDS: row k of KD halves, 16-byte pieces XOR-swizzled by (k >> 3) so that the
-  // fragment reads of 16 consecutive rows are conflict-free
-  for (int p = tid; p < 2 * HID * KD / 8; p += NTHR) {
-    const int arr = p / (HID * KD / 8), q = p - arr * (HID * KD / 8), k = q / (KD / 8), pc = q - k * (KD / 8);
-    const uint4 v = *reinterpret_cast<const uint4*>((arr ? N.w1l : N.w1h) + k * KD + 8 * pc);
-    *reinterpret_cast<uint4*>(sW1 + arr * HID * KD + k * KD + 8 * (pc ^ ((k >> 3) & 1))) = v;
-  }
-  h8 wh[KS], wl[KS];
-  auto w1_frag = [&](int kt) {
-    const int k = 32 * kt + r;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int off = k * KD + 8 * ((2 * ks + h) ^ ((k >> 3) & 1));
-      wh[ks] = *reinterpret_cast<const h8*>(sW1 + off);
-      wl[ks] = *reinterpret_cast<const h8*>(sW1 + HID * KD + off);
-    }
-  };
-  vm_drain();
-  __syncthreads();
-  SF_STAMP(1);
-
-  // ---- Z2^T = W2 H1^T over 8 k-tiles; H1^T tile kt recomputed from Xa just before its use
-  f32x16 acc[8];
-#pragma unroll
-  for (int nt = 0; nt < 8; ++nt)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
-  // H1^T tile kt (rows k = 32 kt + perm) as split B fragments; software-pipelined one k-tile
-  // ahead so that its MFMA + tanh + split overlap the current tile's 48 MFMAs
-  auto h1t_tile = [&](int kt, h8 (&bh)[2], h8 (&bl)[2]) {
-    w1_frag(kt);
-    f32x16 z;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) z = mma3(wh[ks], wl[ks], xh[ks], xl[ks], z);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
-    split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
-    split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
-  };
-  h8 bh[2], bl[2];
-  h1t_tile(0, bh, bl);
-  for (int c = 0; c < 8; ++c) {
-    const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
-    v4u cv[32 / W];
-    chunk_load<W>(N, c + 1, w, l, cv);
-    // n-tile steps fenced by sched_barrier: step nt issues the LDS reads of n-tile nt + 1's W2
-    // fragments, then n-tile nt's six MFMAs, so every read has a whole step (192 MFMA cycles) to
-    // land and only two fragment sets are live (the register budget goes to the accumulators).
-    // The next k-tile's H1^T (kn = c + 1; the last is discarded) is computed in the MFMA shadows.
-    if (c == 3) SF_STAMP2(0);
-    const int kn = c + 1 < 8 ? c + 1 : 7;
-    h8 fc[2][2], fn[2][2], nbh[2], nbl[2];
-    f32x16 z;
-    sf_frag(buf, r, h, fc);
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-      if (nt < 7) sf_frag(buf, 32 * (nt + 1) + r, h, fn);
-      if (nt == 0) w1_frag(kn);
-#ifndef RLKS_Z2_NOFENCE
-      __builtin_amdgcn_sched_barrier(0);  // the reads issue before this step's MFMAs
-#endif
-      if (nt == 1) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) z[q] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) z = mma3(wh[ks], wl[ks], xh[ks], xl[ks], z);
-      }
-      if (nt >= 2 && nt < 6) {
-#pragma unroll
-        for (int q = 4 * (nt - 2); q < 4 * (nt - 1); ++q) z[q] = tanh_abs(z[q] * inv_z1);
-      }
-      if (nt == 6) {
-        split16(z, 0, SF_H1_SCALE, nbh[0], nbl[0]);
-        split16(z, 8, SF_H1_SCALE, nbh[1], nbl[1]);
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        acc[nt] = mma(fc[s][1], bh[s], acc[nt]);
-        acc[nt] = mma(fc[s][0], bl[s], acc[nt]);
-        acc[nt] = mma(fc[s][0], bh[s], acc[nt]);
-      }
-#ifndef RLKS_Z2_NOFENCE
-      __builtin_amdgcn_sched_barrier(0);
-#endif
-      if (nt < 7)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) { fc[s][0] = fn[s][0]; fc[s][1] = fn[s][1]; }
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) { bh[s] = nbh[s]; bl[s] = nbl[s]; }
-    if (c == 3) SF_STAMP2(1);
-    chunk_store<W>(sCh + ((c + 1) & 1) * 2 * SF_CH, w, l, cv);
-    if (c == 3) SF_STAMP2(2);
-    __syncthreads();
-    if (c == 3) SF_STAMP2(3);
-  }
-
-  SF_STAMP(2);
-  // Xa^T values for dW1a^T = Xa^T dZ1 (lane row d = r, m = perm(s, h, j)), loaded before the
-  // head so that their latency hides behind it; split after dZ2
-  float xtv[16];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = sf_perm(s, h, j);
-      xtv[s * 8 + j] = xa_elem(g.x + (size_t)(row0 + m) * stride, r, D);
-    }
-  // ---- H2^T = tanh(Z2^T + b2), head out[a] = b3 + sum_n W3[a][n] H2[n]
-  const float inv_z2 = inv_w2 / SF_H1_SCALE;
-  float out[A_];
-#pragma unroll
-  for (int a = 0; a < A_; ++a) out[a] = 0.f;
-#pragma unroll
-  for (int nt = 0; nt < 8; ++nt)
-#pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      const int n0 = 32 * nt + 8 * gq + 4 * h;
-      const float4 bb = *reinterpret_cast<const float4*>(sB2 + n0);
-      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
-      float wv[A_][4];
-#pragma unroll
-      for (int a = 0; a < A_; ++a) {
-        const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
-        wv[a][0] = t.x; wv[a][1] = t.y; wv[a][2] = t.z; wv[a][3] = t.w;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = 4 * gq + i;
-        const float h2 = tanh_abs(fmaf(acc[nt][q], inv_z2, bv[i]));
-        acc[nt][q] = h2;
-#pragma unroll
-        for (int a = 0; a < A_; ++a) out[a] = fmaf(h2, wv[a][i], out[a]);
-      }
-    }
-#pragma unroll
-  for (int a = 0; a < A_; ++a) out[a] += __shfl_xor(out[a], 32, 64) + N.b3[a];
-
-  // ---- PPO loss for row m = row0 + r (both half-waves compute it; stats from h = 0)
-  float dl[A_];
-  float stv[4];
-  sf_loss<A_, NET>(g, out, row0 + r, dl, stv);
-  const float st_pl = stv[0], st_vf = stv[1], st_kl = stv[2], st_ent = stv[3];
-
-  SF_STAMP(3);
-  // ---- per-tile partials straight to HBM: dW3[a][n] = sum_m dl[m][a] H2[m][n] (half-wave
-  // reduce), db3, loss stats
-#pragma unroll
-  for (int a = 0; a < A_; ++a)
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-      float v[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = dl[a] * acc[nt][q];
-      const float t = half_wave_reduce16(v, l);
-      if ((l & 1) == 0) N.part_w3[((size_t)tile * A_ + a) * HID + 32 * nt + acc_row((l >> 1) & 15, l)] = t;
-    }
-  {
-    float sv[A_ + 4];
-#pragma unroll
-    for (int a = 0; a < A_; ++a) sv[a] = h ? 0.f : dl[a];
-    sv[A_] = h ? 0.f : st_pl; sv[A_ + 1] = h ? 0.f : st_vf; sv[A_ + 2] = h ? 0.f : st_kl; sv[A_ + 3] = h ? 0.f : st_ent;
-#pragma unroll
-    for (int i = 0; i < A_ + 4; ++i) {
-      const float t = wave_sum_f(sv[i]);
-      if (l == 0) {
-        if (i < A_) N.part_b3[(size_t)tile * A_ + i] = t;
-        else N.part_stat[(size_t)tile * 4 + i - A_] = t;
-      }
-    }
-  }
-
-  SF_STAMP(4);
-  // ---- dZ2^T = (dl W3) (1 - H2^2): to HBM (F2), tile max |dZ2| (this wave's split + F2's scale)
-  float dmx = 0.f;
-  {
-    // one base per n-tile, so every store of the n-tile takes an immediate offset (< 4 KB)
-    float* dst0 = N.dz2t + (size_t)tile * HID * 32 + 4 * h * 32 + r;
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        float* dst = dst0 + (size_t)nt * 32 * 32 + (size_t)8 * gq * 32;
-        const int n0 = 32 * nt + 8 * gq + 4 * h;
-        float wv[A_][4];
-#pragma unroll
-        for (int a = 0; a < A_; ++a) {
-          const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
-          wv[a][0] = t.x; wv[a][1] = t.y; wv[a][2] = t.z; wv[a][3] = t.w;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int q = 4 * gq + i;
-          float gsum = 0.f;
-#pragma unroll
-          for (int a = 0; a < A_; ++a) gsum = fmaf(dl[a], wv[a][i], gsum);
-          const float h2 = acc[nt][q];
-          const float dz = gsum * (1.f - h2 * h2);
-          acc[nt][q] = dz;
-          dmx = fmaxf(dmx, fabsf(dz));
-          dst[i * 32] = dz;
-        }
-      }
-  }
-  dmx = wave_max(dmx);
-  if (l == 0) atomicMax(dz_slot(N.dzmax, tile), __float_as_uint(dmx));
-  const int edz = sf_exp(dmx);
-  const float sdz = pow2(edz);
-  {
-    h8 a, b;
-    split8(xtv, 0, sx, a, b);
-    sXT[(w * 4 + 0) * 64 + l] = a;
-    sXT[(w * 4 + 1) * 64 + l] = b;
-    split8(xtv, 8, sx, a, b);
-    sXT[(w * 4 + 2) * 64 + l] = a;
-    sXT[(w * 4 + 3) * 64 + l] = b;
-  }
-  SF_STAMP(5);
-  // ---- dH1 = dZ2 W2, n-tile outer: chunk 8 + nt holds W2's n-tile nt (w2t columns) for every
-  // k-tile, the n-tile's dZ2^T accumulator is split into the A fragments just before its MFMAs,
-  // and all eight dH1 k-tile accumulators stay live (AGPRs) until the last n-tile.  Fragment
-  // reads run one k-tile step ahead of the MFMAs (sched_barrier fences), so only two fragment sets
-  // and one n-tile's dZ2 split are live instead of the whole split dZ2^T.
-  f32x16 dh[8];
-#pragma unroll
-  for (int kt = 0; kt < 8; ++kt)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) dh[kt][q] = 0.f;
-#pragma unroll
-  for (int nt = 0; nt < 8; ++nt) {
-    const int c = 8 + nt;
-    const _Float16* buf = sCh + (c & 1) * 2 * SF_CH;
-    v4u cv[32 / W];
-    if (nt == 3) SF_STAMP2(4);
-    if (nt < 7) chunk_load<W>(N, c + 1, w, l, cv);
-    h8 ah[2], al[2], fc[2][2], fn[2][2];
-    split16(acc[nt], 0, sdz, ah[0], al[0]);
-    split16(acc[nt], 8, sdz, ah[1], al[1]);
-    sf_frag(buf, r, h, fc);
-#pragma unroll
-    for (int kt = 0; kt < 8; ++kt) {
-      if (kt < 7) sf_frag(buf, 32 * (kt + 1) + r, h, fn);
-      __builtin_amdgcn_sched_barrier(0);  // the reads issue before this step's MFMAs
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        dh[kt] = mma(al[s], fc[s][0], dh[kt]);
-        dh[kt] = mma(ah[s], fc[s][1], dh[kt]);
-        dh[kt] = mma(ah[s], fc[s][0], dh[kt]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt < 7)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) { fc[s][0] = fn[s][0]; fc[s][1] = fn[s][1]; }
-    }
-    if (nt == 3) SF_STAMP2(5);
-    if (nt < 7) chunk_store<W>(sCh + ((c + 1) & 1) * 2 * SF_CH, w, l, cv);
-    if (nt == 3) SF_STAMP2(6);
-    __syncthreads();
-    if (nt == 3) SF_STAMP2(7);
-  }
-  SF_STAMP(6);
-  // ---- dZ1 = dH1 (1 - H1^2) -> dW1a^T = Xa^T dZ1 per k-tile; dZ1 enters the split at
-  // 2^(e_dz + e_w2 - 23): |dH1 2^(e_dz + e_w2)| <= 256 2^15 2^15.  Each wave's dW1a^T blocks go to
-  // LDS slots in the (now idle) chunk buffers, KPR k-tiles per round, and the workgroup sums them
-  // over the W waves in a fixed order after one barrier per round.
-  constexpr int SLOT = W * 32 * DWR;                       // floats per k-tile
-  constexpr int KPR = (2 * SF_CH) / SLOT >= 8 ? 8 : (2 * SF_CH) / SLOT;  // 64 KB of chunk buffers
-  static_assert(KPR >= 1 && 8 % KPR == 0, "dW1 epilogue slots");
-  float* sEp = reinterpret_cast<float*>(sCh);
-  const int blk = blockIdx.x;
-  auto dw1_flush = [&](int kt0) {  // k-tiles kt0 .. kt0 + KPR - 1: (k, d) elements, fixed wave order
-    const int nd = D + 1;
-    for (int e = tid; e < KPR * 32 * nd; e += NTHR) {
-      const int j = e / (32 * nd), e2 = e - j * 32 * nd, kk = e2 / nd, d = e2 - kk * nd, k = 32 * (kt0 + j) + kk;
-      float s = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < W; ++ww) s += sEp[j * SLOT + (ww * 32 + kk) * DWR + d];
-      if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = s;
-      else N.part_b1[(size_t)blk * HID + k] = s;
-    }
-  };
-  const float sz1 = pow2(-23);
-  const float u1 = pow2(23 - ex - edz - e_w2);
-  // derivative (1 - H1^2) of k-tile kt, rows m in registers (Z1 = Xa W1a^T)
-  auto h1_der = [&](int kt, f32x16& der) {
-    w1_frag(kt);
-    f32x16 z;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) z = mma3(xh[ks], xl[ks], wh[ks], wl[ks], z);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const float h1 = tanh_abs(z[q] * inv_z1);
-      der[q] = 1.f - h1 * h1;
-    }
-  };
-  // dZ1 -> split -> dW1a^T of k-tile kt into this wave's part of slot kt mod KPR
-  auto dw1_tile = [&](int kt, const f32x16& dhk, const f32x16& der) {
-    f32x16 dz;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) dz[q] = dhk[q] * der[q];
-    h8 zh[2], zl[2];
-    split16(dz, 0, sz1, zh[0], zl[0]);
-    split16(dz, 8, sz1, zh[1], zl[1]);
-    f32x16 wacc, wacc2;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) { wacc[q] = 0.f; wacc2[q] = 0.f; }
-    const h8 x0h = sXT[(w * 4 + 0) * 64 + l], x0l = sXT[(w * 4 + 1) * 64 + l];
-    const h8 x1h = sXT[(w * 4 + 2) * 64 + l], x1l = sXT[(w * 4 + 3) * 64 + l];
-    wacc = mma(x0l, zh[0], wacc);
-    wacc2 = mma(x1l, zh[1], wacc2);
-    wacc = mma(x0h, zl[0], wacc);
-    wacc2 = mma(x1h, zl[1], wacc2);
-    wacc = mma(x0h, zh[0], wacc);
-    wacc2 = mma(x1h, zh[1], wacc2);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) wacc[q] += wacc2[q];
-    // rows d = 8g + 4h + 0..3 of column k: 16-byte stores
-#pragma unroll
-    for (int gq = 0; gq < NG; ++gq) {
-      float4 v = {wacc[4 * gq] * u1, wacc[4 * gq + 1] * u1, wacc[4 * gq + 2] * u1, wacc[4 * gq + 3] * u1};
-      *reinterpret_cast<float4*>(sEp + (kt % KPR) * SLOT + (w * 32 + r) * DWR + 8 * gq + 4 * h) = v;
-    }
-  };
-  // software-pipelined: the next k-tile's derivative (MFMAs + tanh) overlaps this one's dW1a
-  f32x16 der;
-  h1_der(0, der);
-#pragma unroll
-  for (int kt = 0; kt < 8; ++kt) {
-    f32x16 nder;
-    if (kt < 7) h1_der(kt + 1, nder);
-    dw1_tile(kt, dh[kt], der);
-    if (kt % KPR == KPR - 1) {
-      __syncthreads();
-      dw1_flush(kt + 1 - KPR);
-      if (kt < 7) __syncthreads();  // slots free for the next round
-    }
-    if (kt < 7) der = nder;
-  }
-  SF_STAMP(7);
+__device__ __forceinline__ f4 mm16(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ f4 mm16x3(h8 ah, h8 al, h8 bh, h8 bl, f4 c) {
+  c = mm16(al, bh, c);
+  c = mm16(ah, bl, c);
+  return mm16(ah, bh, c);
 }
+__device__ __forceinline__ f4 mk16(h4 a, h4 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ f4 mk16x3(h4 ah, h4 al, h4 bh, h4 bl, f4 c) {
+  c = mk16(al, bh, c);
+  c = mk16(ah, bl, c);
+  return mk16(ah, bh, c);
+}
+__device__ __forceinline__ f4 f4zero() { return f4{0.f, 0.f, 0.f, 0.f}; }
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// ----------------------------------------------------------------------------- split F1
-// The fused F1 needs ~460 registers (the Z2^T / dZ2^T accumulators plus the eight dH1 k-tile
-// accumulators), so it runs one wave per SIMD and its ~9k VALU instructions per tile (tanh and
-// splits, head, dW3, dZ2, dZ1) cannot hide behind another wave's MFMAs.  Split at the dZ2 hand-off
-// (which F2 needs in HBM anyway), each half fits 256 registers and ~50-80 KB of LDS, so two
-// independent workgroups share every CU and each SIMD interleaves two waves in different phases:
-//   F1a (k_sf_fwd): Z1, Z2^T = W2 H1^T, head, loss, dW3 / db3 / stats, dZ2^T -> HBM, tile scale;
-//   F1b (k_sf_bwd): dH1 = dZ2 W2 (dZ2^T n-tiles from HBM, W2 chunks per k-half), dZ1, dW1a.
-// W2 chunks are single-buffered: a step computes from LDS while its successor is loaded into
-// registers, then barrier / store / barrier.
-// Half-chunk of the Z2 loop: w2p rows n in [128 p, +128), columns [32 c, +32) -> [128][32] image;
-// of the dH1 loop: w2t rows k in [128 p, +128), columns [32 nt, +32).  1024 slots of 16 B (hi,
-// lo): 16 blocks of 64 lanes, wave w of W moves blocks (16 / W) w + i.
+// half-chunk image: 128 rows x 32 halves (64-byte rows), hi and lo; 16-byte piece q of row r at
+// slot q ^ SW16(r), which makes the A / B fragment reads (ds_read_b128: rows 16j + c, piece g)
+// conflict-free in each of the instruction's four 16-lane groups
+constexpr int H16 = 4096;  // halves per [128][32] image
+__device__ __forceinline__ int sw16(int r) { return 2 * ((r >> 2) & 1); }
+
+// LDS-DMA of rows [r0, r0 + 128), columns [col, col + 32) of a [256][256] split weight: 2 x 512
+// 16-byte slots (hi, lo) = 16 blocks of 64 lanes, wave w of W moves blocks (16 / W) w + i
 template <int W>
-__device__ __forceinline__ void half_load(const _Float16* hi, const _Float16* lo, int p, int col, int w, int l,
-                                          v4u (&v)[16 / W]) {
+__device__ __forceinline__ void hc_dma(const _Float16* hi, const _Float16* lo, int r0, int col, _Float16* buf, int w,
+                                       int l) {
 #pragma unroll
   for (int i = 0; i < 16 / W; ++i) {
     const int blk = (16 / W) * w + i, arr = blk >> 3, sig = (blk & 7) * 64 + l;
-    const int row = sig >> 2, pc = (sig & 3) ^ ((row >> 2) & 3);
-    v[i] = *reinterpret_cast<const v4u*>((arr ? lo : hi) + (128 * p + row) * HID + col + 8 * pc);
-  }
-}
-template <int W>
-__device__ __forceinline__ void half_store(_Float16* buf, int w, int l, const v4u (&v)[16 / W]) {
-  constexpr int HALF = SF_CH / 2;  // halves per [128][32] image
-#pragma unroll
-  for (int i = 0; i < 16 / W; ++i) {
-    const int blk = (16 / W) * w + i, arr = blk >> 3;
-    *reinterpret_cast<v4u*>(buf + arr * HALF + ((blk & 7) * 64 + l) * 8) = v[i];
-  }
-}
-// the same half-chunk by LDS-DMA (no staging registers; the split kernels run two waves per SIMD,
-// which hide the LDS waits the DMA brings with it)
-template <int W>
-__device__ __forceinline__ void half_dma(const _Float16* hi, const _Float16* lo, int p, int col, _Float16* buf, int w,
-                                         int l) {
-  constexpr int HALF = SF_CH / 2;
-#pragma unroll
-  for (int i = 0; i < 16 / W; ++i) {
-    const int blk = (16 / W) * w + i, arr = blk >> 3, sig = (blk & 7) * 64 + l;
-    const int row = sig >> 2, pc = (sig & 3) ^ ((row >> 2) & 3);
-    const _Float16* src = (arr ? lo : hi) + (128 * p + row) * HID + col + 8 * pc;
-    _Float16* dst = buf + arr * HALF + (blk & 7) * 64 * 8;
+    const int r = sig >> 2, q = (sig & 3) ^ sw16(r);
+    const _Float16* src = (arr ? lo : hi) + (r0 + r) * HID + col + 8 * q;
+    _Float16* dst = buf + arr * H16 + (blk & 7) * 512;
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
   }
 }
-__device__ __forceinline__ void half_frag(const _Float16* buf, int row, int h, h8 (&f)[2][2]) {
-  constexpr int HALF = SF_CH / 2;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int off = row * 32 + 8 * ((2 * s + h) ^ ((row >> 2) & 3));
-    f[s][0] = *reinterpret_cast<const h8*>(buf + off);
-    f[s][1] = *reinterpret_cast<const h8*>(buf + HALF + off);
+// (hi, lo) fragment of image row 16 j + c, piece g
+__device__ __forceinline__ void hc_frag(const _Float16* buf, int j, int c, int g, h8& fh, h8& fl) {
+  const int off = (16 * j + c) * 32 + 8 * (g ^ sw16(c));
+  fh = *reinterpret_cast<const h8*>(buf + off);
+  fl = *reinterpret_cast<const h8*>(buf + H16 + off);
+}
+
+// W1a = [W1 | b1] (hi, lo) in LDS: [2][HID k][KD] halves; at KD = 32 the 16-byte pieces of a row
+// are swizzled like the weight images (conflict-free); at KD = 16 the plain 32-byte rows already are
+template <int KD>
+__device__ __forceinline__ int w1_off(int k, int q) {
+  return k * KD + 8 * (KD == 32 ? (q ^ sw16(k)) : q);
+}
+template <int KD, int NTHR>
+__device__ __forceinline__ void w1_stage(const SfNet& N, _Float16* sW1, int tid) {
+  for (int p = tid; p < 2 * HID * KD / 8; p += NTHR) {
+    const int arr = p / (HID * KD / 8), e = p - arr * (HID * KD / 8), k = e / (KD / 8), q = e - k * (KD / 8);
+    const v4u v = *reinterpret_cast<const v4u*>((arr ? N.w1l : N.w1h) + k * KD + 8 * q);
+    *reinterpret_cast<v4u*>(sW1 + arr * HID * KD + w1_off<KD>(k, q)) = v;
   }
+}
+// W1a fragment of rows k = 16 kt + c, columns d = 8g + j: lanes with 8g >= KD read a duplicate
+// piece (finite; the Xa fragment is zero there)
+template <int KD>
+__device__ __forceinline__ void w1_frag(const _Float16* sW1, int kt, int c, int g, h8& fh, h8& fl) {
+  const int off = w1_off<KD>(16 * kt + c, g & (KD / 8 - 1));
+  fh = *reinterpret_cast<const h8*>(sW1 + off);
+  fl = *reinterpret_cast<const h8*>(sW1 + HID * KD + off);
+}
+
+// sum over the four 16-lane rows of a wave (lanes c, c + 16, c + 32, c + 48): every lane gets the
+// same bits
+__device__ __forceinline__ float sum_rows4(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+// reduce-scatter of 16 per-lane values over the 16 lanes of a row: lane c of the row ends with the
+// row total of v[c] (DPP row_ror:8, row_half_mirror, quad_perm xor 2, xor 1; 43 VALU)
+__device__ __forceinline__ float row_reduce16(const float (&v)[16], int l) {
+  float u[8], w[4], x[2];
+  const bool b3 = (l >> 3) & 1, b2 = (l >> 2) & 1, b1 = (l >> 1) & 1, b0 = l & 1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) u[i] = (b3 ? v[i + 8] : v[i]) + dpp<0x128>(b3 ? v[i] : v[i + 8]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (b2 ? u[i + 4] : u[i]) + dpp<0x141>(b2 ? u[i] : u[i + 4]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) x[i] = (b1 ? w[i + 2] : w[i]) + dpp<0x4E>(b1 ? w[i] : w[i + 2]);
+  return (b0 ? x[1] : x[0]) + dpp<0xB1>(b0 ? x[0] : x[1]);
+}
+// sum over the 16 lanes of a row (every lane of the row gets it)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp<0x128>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0x4E>(v);
+  return v + dpp<0xB1>(v);
+}
+
+// Xa = [X | 1 | 0] fragment of a 16-row tile: lane (g, c) holds row row0 + c, columns 8g .. 8g + 7,
+// scaled by the wave's power of two (returned: its exponent) and split
+__device__ __forceinline__ int x_frag(const SfArgs& a, int row0, int c, int g, h8& xh, h8& xl) {
+  float xv[8];
+  xa_row8(a.x + (size_t)(row0 + c) * a.x_stride, 8 * g, a.D, a.x_stride, xv);
+  float xm = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) xm = fmaxf(xm, fabsf(xv[j]));
+  const int ex = sf_exp(wave_max(xm));
+  split8(xv, 0, pow2(ex), xh, xl);
+  return ex;
+}
+
+// LDS of F1a: the loop region (two half-chunk buffers + W1a) doubles as the epilogue's workgroup
+// slots (dW3 [W][A][HID], then [W][A + 4] db3 / stats); b2 and W3 follow it
+template <int A_, int KD, int W>
+constexpr int f1a_region_bytes() {
+  constexpr int loop = 4 * H16 * 2 + 2 * HID * KD * 2;
+  constexpr int ep = W * A_ * HID * 4 + W * (A_ + 4) * 4;
+  return ((loop > ep ? loop : ep) + 15) / 16 * 16;
+}
+template <int A_, int KD, int W>
+constexpr int f1a_lds_bytes() {
+  return f1a_region_bytes<A_, KD, W>() + (HID + A_ * HID) * 4;
+}
+template <int KD>
+constexpr int f1b_lds_bytes() {
+  return 4 * H16 * 2 + 2 * HID * KD * 2;
 }
 
 template <int A_, int NET, int KD, int W>
-__device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
+__device__ __forceinline__ void f1a_body(const SfArgs& g) {
   constexpr int NTHR = 64 * W;
-  constexpr int KS = KD / 16;
   const SfNet& N = g.n[NET];
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  _Float16* sCh = reinterpret_cast<_Float16*>(lds);             // [2 buf][2 hi/lo][128][32] (32 KB)
-  float* sB2 = lds + SF_CH;                                     // [HID]
-  float* sW3 = sB2 + HID;                                       // [A_][HID]
-  _Float16* sW1 = reinterpret_cast<_Float16*>(sW3 + A_ * HID);  // [2 hi/lo][HID k][KD] (swizzled)
+  _Float16* sCh = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][128][32]
+  _Float16* sW1 = sCh + 4 * H16;                      // [2 hi/lo][HID][KD]
+  float* sSlot = lds;                                 // epilogue (after the loop's last barrier)
+  float* sB2 = lds + f1a_region_bytes<A_, KD, W>() / 4;
+  float* sW3 = sB2 + HID;
 
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
-  const int D = g.D, stride = g.x_stride;
-  const int tile = blockIdx.x * W + w, row0 = tile * 32;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, c = l & 15, gq = l >> 4;
+  const int tile = blockIdx.x * W + w, row0 = tile * 16;
   FA_STAMP(0);
   FA_HWID();
 
-  half_dma<W>(N.w2ph, N.w2pl, 0, 0, sCh, w, l);
+  hc_dma<W>(N.w2ph, N.w2pl, 0, 0, sCh, w, l);
   for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i];
   for (int i = tid; i < A_ * HID; i += NTHR) sW3[i] = N.w3[i];
-  float xv[KS * 8];
-  const float* xr = g.x + (size_t)(row0 + r) * stride;
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xv[ks * 8 + j] = xa_elem(xr, 16 * ks + 8 * h + j, D);
-  float xm = 0.f;
-#pragma unroll
-  for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
-  const float sx = pow2(sf_exp(wave_max(xm)));
-  h8 xh[KS], xl[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) split8(xv, ks * 8, sx, xh[ks], xl[ks]);
-  const float inv_z1 = N.sc[1] / sx;
-  for (int p = tid; p < 2 * HID * KD / 8; p += NTHR) {
-    const int arr = p / (HID * KD / 8), q = p - arr * (HID * KD / 8), k = q / (KD / 8), pc = q - k * (KD / 8);
-    const v4u v = *reinterpret_cast<const v4u*>((arr ? N.w1l : N.w1h) + k * KD + 8 * pc);
-    *reinterpret_cast<v4u*>(sW1 + arr * HID * KD + k * KD + 8 * (pc ^ ((k >> 3) & 1))) = v;
-  }
-  h8 wh[KS], wl[KS];
-  auto w1_frag = [&](int kt) {
-    const int k = 32 * kt + r;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int off = k * KD + 8 * ((2 * ks + h) ^ ((k >> 3) & 1));
-      wh[ks] = *reinterpret_cast<const h8*>(sW1 + off);
-      wl[ks] = *reinterpret_cast<const h8*>(sW1 + HID * KD + off);
-    }
-  };
-  auto h1t = [&](int kt, h8 (&bh)[2], h8 (&bl)[2]) {
-    w1_frag(kt);
-    f32x16 z;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) z = mma3(wh[ks], wl[ks], xh[ks], xl[ks], z);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
-    split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
-    split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
-  };
+  w1_stage<KD, NTHR>(N, sW1, tid);
+  h8 xh, xl;
+  const int ex = x_frag(g, row0, c, gq, xh, xl);
+  const float inv_z1 = N.sc[1] * pow2(-ex);
   vm_drain();
   __syncthreads();
   FA_STAMP(1);
 
-  // ---- Z2^T = W2 H1^T: 16 steps (k-tile c, n-half p) of 24 MFMAs over double-buffered
-  // half-chunks; H1^T of k-tile c is computed at the start of its first step
-  f32x16 acc[8];
+  // ---- Z2^T = W2 H1^T: 16 steps (k-tile t, n-half ph) of 8 n-tiles x 3 MFMAs over double-
+  // buffered half-chunks; H1^T of k-tile t (two Z1^T tiles, tanh, split) at the start of its first step
+  f4 acc[16];
 #pragma unroll
-  for (int nt = 0; nt < 8; ++nt)
+  for (int nt = 0; nt < 16; ++nt) acc[nt] = f4zero();
+  h8 bh, bl;
+  for (int t = 0; t < 8; ++t) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
-  h8 bh[2], bl[2];
-  for (int c = 0; c < 8; ++c) {
+    for (int ph = 0; ph < 2; ++ph) {
+      const int st = 2 * t + ph;  // reads buffer ph; the next half-chunk -> buffer ph ^ 1
+      if (st < 15) hc_dma<W>(N.w2ph, N.w2pl, 128 * (ph ^ 1), 32 * (t + ph), sCh + (ph ^ 1) * 2 * H16, w, l);
+      if (ph == 0) {
+        f4 z[2];
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {  // step 2c + p reads buffer p; the next half-chunk -> buffer p ^ 1
-      if (!(c == 7 && p == 1)) half_dma<W>(N.w2ph, N.w2pl, p ^ 1, 32 * (c + p), sCh + (p ^ 1) * SF_CH, w, l);
-      if (p == 0) h1t(c, bh, bl);
-      const _Float16* buf = sCh + p * SF_CH;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        h8 fc[2][2];
-        half_frag(buf, 32 * j + r, h, fc);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          acc[4 * p + j] = mma(fc[s][1], bh[s], acc[4 * p + j]);
-          acc[4 * p + j] = mma(fc[s][0], bl[s], acc[4 * p + j]);
-          acc[4 * p + j] = mma(fc[s][0], bh[s], acc[4 * p + j]);
+        for (int b = 0; b < 2; ++b) {
+          h8 wh, wl;
+          w1_frag<KD>(sW1, 2 * t + b, c, gq, wh, wl);
+          z[b] = mm16x3(wh, wl, xh, xl, f4zero());
         }
+        float hv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[j] = tanh_abs(z[j >> 2][j & 3] * inv_z1);
+        split8(hv, 0, SF_H1_SCALE, bh, bl);
+      }
+      // fragments one n-tile ahead of their MFMAs, fenced so that only two sets are live
+      const _Float16* buf = sCh + ph * 2 * H16;
+      h8 ch, cl;
+      hc_frag(buf, 0, c, gq, ch, cl);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        h8 nh, nl;
+        if (j < 7) hc_frag(buf, j + 1, c, gq, nh, nl);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[8 * ph + j] = mm16x3(ch, cl, bh, bl, acc[8 * ph + j]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (j < 7) { ch = nh; cl = nl; }
       }
       vm_drain();
       __syncthreads();
     }
-    if (c == 0) FA_STAMP(2);
+    if (t == 0) FA_STAMP(2);
   }
   FA_STAMP(3);
 
-  // ---- H2^T = tanh(Z2^T + b2), head out[a] = b3 + sum_n W3[a][n] H2[n]
+  // ---- H2^T = tanh(Z2^T + b2) (lane: rows n = 16 nt + 4g + i of column m = c); head
+  // out[a] = b3 + sum_n W3[a][n] H2[n] (partial over the lane's 64 n, then over the four rows)
   const float inv_z2 = N.sc[3] / SF_H1_SCALE;
   float out[A_];
 #pragma unroll
   for (int a = 0; a < A_; ++a) out[a] = 0.f;
 #pragma unroll
-  for (int nt = 0; nt < 8; ++nt)
+  for (int nt = 0; nt < 16; ++nt) {
+    const int n0 = 16 * nt + 4 * gq;
+    const float4 bb = *reinterpret_cast<const float4*>(sB2 + n0);
+    const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+    float hv[4];
 #pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      const int n0 = 32 * nt + 8 * gq + 4 * h;
-      const float4 bb = *reinterpret_cast<const float4*>(sB2 + n0);
-      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
-      float h2v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = 4 * gq + i;
-        h2v[i] = tanh_abs(fmaf(acc[nt][q], inv_z2, bv[i]));
-        acc[nt][q] = h2v[i];
-      }
-      // one action's W3 quad at a time (4 registers live instead of 4 A): the same fma order per
-      // out[a] as element-major
-#pragma unroll
-      for (int a = 0; a < A_; ++a) {
-        const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
-        out[a] = fmaf(h2v[0], t.x, out[a]);
-        out[a] = fmaf(h2v[1], t.y, out[a]);
-        out[a] = fmaf(h2v[2], t.z, out[a]);
-        out[a] = fmaf(h2v[3], t.w, out[a]);
-      }
+    for (int i = 0; i < 4; ++i) {
+      hv[i] = tanh_abs(fmaf(acc[nt][i], inv_z2, bv[i]));
+      acc[nt][i] = hv[i];
     }
 #pragma unroll
-  for (int a = 0; a < A_; ++a) out[a] += __shfl_xor(out[a], 32, 64) + N.b3[a];
+    for (int a = 0; a < A_; ++a) {
+      const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
+      out[a] = fmaf(hv[0], t.x, out[a]);
+      out[a] = fmaf(hv[1], t.y, out[a]);
+      out[a] = fmaf(hv[2], t.z, out[a]);
+      out[a] = fmaf(hv[3], t.w, out[a]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < A_; ++a) out[a] = sum_rows4(out[a]) + N.b3[a];
+  // the dZ2 pass below re-reads W3 from LDS rather than keeping the head's 16 A float4 alive
+  // through the dW3 reductions (the compiler would otherwise reuse them and spill)
+  asm volatile("" ::: "memory");
   FA_STAMP(4);
   float dl[A_];
   float st[4];
-  sf_loss<A_, NET>(g, out, row0 + r, dl, st);
-  // ---- dW3 (half-wave reduce), db3, loss stats
+  sf_loss<A_, NET>(g, out, row0 + c, dl, st);
+
+  // ---- dW3[a][n] over the tile's rows: reduce-scatter over the 16 lanes of a row (lane c ends
+  // with n = 64G + 16 (c >> 2) + 4g + (c & 3) of group G), one slot per wave
+  constexpr int SLOT_B3 = W * A_ * HID;
 #pragma unroll
   for (int a = 0; a < A_; ++a)
 #pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
+    for (int G = 0; G < 4; ++G) {
       float v[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = dl[a] * acc[nt][q];
-      const float t = half_wave_reduce16(v, l);
-      if ((l & 1) == 0) N.part_w3[((size_t)tile * A_ + a) * HID + 32 * nt + acc_row((l >> 1) & 15, l)] = t;
+      for (int k = 0; k < 16; ++k) v[k] = dl[a] * acc[4 * G + (k >> 2)][k & 3];
+      sSlot[(w * A_ + a) * HID + 64 * G + 16 * (c >> 2) + 4 * gq + (c & 3)] = row_reduce16(v, l);
     }
-  {
+  {  // db3 and the loss stats: row sums (the four rows of the wave hold the same 16 rows m)
     float sv[A_ + 4];
 #pragma unroll
-    for (int a = 0; a < A_; ++a) sv[a] = h ? 0.f : dl[a];
+    for (int a = 0; a < A_; ++a) sv[a] = dl[a];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sv[A_ + i] = h ? 0.f : st[i];
-    float tv[A_ + 4];
+    for (int i = 0; i < 4; ++i) sv[A_ + i] = st[i];
 #pragma unroll
-    for (int i = 0; i < A_ + 4; ++i) tv[i] = wave_sum_f(sv[i]);  // independent chains, interleaved
-    if (l == 0) {
+    for (int i = 0; i < A_ + 4; ++i) sv[i] = row_sum16(sv[i]);
+    if (l == 0)
 #pragma unroll
-      for (int i = 0; i < A_ + 4; ++i) {
-        if (i < A_) N.part_b3[(size_t)tile * A_ + i] = tv[i];
-        else N.part_stat[(size_t)tile * 4 + i - A_] = tv[i];
-      }
-    }
+      for (int i = 0; i < A_ + 4; ++i) sSlot[SLOT_B3 + w * (A_ + 4) + i] = sv[i];
   }
   FA_STAMP(5);
-  // ---- dZ2^T = (dl W3) (1 - H2^2) -> HBM; the tile's split exponent for F1b, max for F2
+
+  // ---- dZ2^T = (dl W3) (1 - H2^2) -> HBM: [tile][s = nt >> 1][lane][4 (nt & 1) + i], i.e. each
+  // lane's eight values of an n-step are the A fragment F1b's same lane reads; the tile's max |dZ2|
   float dmx = 0.f;
   {
-    // one base per n-tile, so every store of the n-tile takes an immediate offset (< 4 KB)
-    float* dst0 = N.dz2t + (size_t)tile * HID * 32 + 4 * h * 32 + r;
+    float* dst = N.dz2t + (size_t)tile * (16 * HID) + l * 8;
 #pragma unroll
-    for (int nt = 0; nt < 8; ++nt)
+    for (int nt = 0; nt < 16; ++nt) {
+      const int n0 = 16 * nt + 4 * gq;
+      float gs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        float* dst = dst0 + (size_t)nt * 32 * 32 + (size_t)8 * gq * 32;
-        const int n0 = 32 * nt + 8 * gq + 4 * h;
-        float gs[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int a = 0; a < A_; ++a) {
-          const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
-          gs[0] = fmaf(dl[a], t.x, gs[0]);
-          gs[1] = fmaf(dl[a], t.y, gs[1]);
-          gs[2] = fmaf(dl[a], t.z, gs[2]);
-          gs[3] = fmaf(dl[a], t.w, gs[3]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int q = 4 * gq + i;
-          const float gsum = gs[i];
-          const float h2 = acc[nt][q];
-          const float dz = gsum * (1.f - h2 * h2);
-          dmx = fmaxf(dmx, fabsf(dz));
-          dst[i * 32] = dz;
-        }
+      for (int a = 0; a < A_; ++a) {
+        const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
+        gs[0] = fmaf(dl[a], t.x, gs[0]);
+        gs[1] = fmaf(dl[a], t.y, gs[1]);
+        gs[2] = fmaf(dl[a], t.z, gs[2]);
+        gs[3] = fmaf(dl[a], t.w, gs[3]);
       }
+      v4f dz;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float h2 = acc[nt][i];
+        dz[i] = gs[i] * (1.f - h2 * h2);
+        dmx = fmaxf(dmx, fabsf(dz[i]));
+      }
+      *reinterpret_cast<v4f*>(dst + (nt >> 1) * 512 + 4 * (nt & 1)) = dz;
+    }
   }
   dmx = wave_max(dmx);
   if (l == 0) {
@@ -1059,312 +662,159 @@ __device__ __forceinline__ void sf_fwd_body(const SfArgs& g) {
     N.tile_edz[tile] = sf_exp(dmx);
   }
   FA_STAMP(6);
+  // ---- workgroup sums (fixed wave order) -> this block's partials
+  __syncthreads();
+  const int blk = blockIdx.x;
+  for (int e = tid; e < A_ * HID; e += NTHR) {
+    float s = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) s += sSlot[ww * A_ * HID + e];
+    N.part_w3[(size_t)blk * A_ * HID + e] = s;
+  }
+  if (tid < A_ + 4) {
+    float s = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) s += sSlot[SLOT_B3 + ww * (A_ + 4) + tid];
+    if (tid < A_) N.part_b3[(size_t)blk * A_ + tid] = s;
+    else N.part_stat[(size_t)blk * 4 + tid - A_] = s;
+  }
 }
 
 template <int A_, int KD, int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sf_fwd(SfArgs g) {
-  if (blockIdx.y + g.net0 == 0) sf_fwd_body<A_, 0, KD, W>(g);
-  else sf_fwd_body<1, 1, KD, W>(g);
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_fwd(SfArgs g) {
+  if (blockIdx.y + g.net0 == 0) f1a_body<A_, 0, KD, W>(g);
+  else f1a_body<1, 1, KD, W>(g);
 }
 
-template <int NET, int KD, int NG, int W>
-__device__ __forceinline__ void sf_bwd_body(const SfArgs& g) {
+template <int NET, int KD, int W>
+__device__ __forceinline__ void f1b_body(const SfArgs& g) {
   constexpr int NTHR = 64 * W;
-  constexpr int KS = KD / 16;
-  constexpr int DWR = 8 * NG;
-  constexpr int SLOT = W * 32 * DWR;                           // floats per k-tile of dW1a^T partials
-  constexpr int KPR = SF_CH / SLOT >= 4 ? 4 : SF_CH / SLOT;   // k-tiles per flush round (32-KB buffers)
-  static_assert(KPR >= 1 && 4 % KPR == 0, "dW1 epilogue slots");
+  constexpr int DT = KD / 16;                      // 16-row d-tiles of dW1a^T
+  constexpr int SLOT = W * 16 * 16 * DT;           // floats per k-tile: [W][16 k][16 DT d]
+  constexpr int KPR = (4 * H16 * 2 / 4) / SLOT;    // k-tiles per flush round (the half-chunk buffers)
+  static_assert(KPR >= 1 && 16 % KPR == 0, "dW1 epilogue slots");
   const SfNet& N = g.n[NET];
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  _Float16* sCh = reinterpret_cast<_Float16*>(lds);             // [2 buf][2 hi/lo][128][32] (32 KB)
-  _Float16* sW1 = reinterpret_cast<_Float16*>(lds + SF_CH);    // [2 hi/lo][HID k][KD] (swizzled)
-  h8* sXT = reinterpret_cast<h8*>(sW1 + 2 * HID * KD);          // [W][2 s][2 hi/lo][64 lanes]
-  float* sEp = lds;                                             // epilogue slots (the chunk buffers)
+  _Float16* sCh = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][128][32]
+  _Float16* sW1 = sCh + 4 * H16;                      // [2 hi/lo][HID][KD]
+  float* sEp = lds;                                   // epilogue slots (the chunk buffers)
 
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, c = l & 15, gq = l >> 4;
+  const int tile = blockIdx.x * W + w, row0 = tile * 16, blk = blockIdx.x;
   const int D = g.D, stride = g.x_stride;
-  const int tile = blockIdx.x * W + w, row0 = tile * 32, blk = blockIdx.x;
 
-#if !RLKS_F1B_ONEPASS
-  half_dma<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
-#endif
-  float xv[KS * 8];
-  const float* xr = g.x + (size_t)(row0 + r) * stride;
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xv[ks * 8 + j] = xa_elem(xr, 16 * ks + 8 * h + j, D);
-  float xm = 0.f;
-#pragma unroll
-  for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
-  const int ex = sf_exp(wave_max(xm));
-  const float sx = pow2(ex);
-  h8 xh[KS], xl[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) split8(xv, ks * 8, sx, xh[ks], xl[ks]);
-  const float inv_z1 = N.sc[1] / sx;
-  {  // Xa^T for dW1a^T = Xa^T dZ1 (lane row d = r, m = perm(s, h, j))
-    float xtv[16];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xtv[s * 8 + j] = xa_elem(g.x + (size_t)(row0 + sf_perm(s, h, j)) * stride, r, D);
-    h8 a, b;
-    split8(xtv, 0, sx, a, b);
-    sXT[(w * 4 + 0) * 64 + l] = a;
-    sXT[(w * 4 + 1) * 64 + l] = b;
-    split8(xtv, 8, sx, a, b);
-    sXT[(w * 4 + 2) * 64 + l] = a;
-    sXT[(w * 4 + 3) * 64 + l] = b;
-  }
-  for (int p = tid; p < 2 * HID * KD / 8; p += NTHR) {
-    const int arr = p / (HID * KD / 8), q = p - arr * (HID * KD / 8), k = q / (KD / 8), pc = q - k * (KD / 8);
-    const v4u v = *reinterpret_cast<const v4u*>((arr ? N.w1l : N.w1h) + k * KD + 8 * pc);
-    *reinterpret_cast<v4u*>(sW1 + arr * HID * KD + k * KD + 8 * (pc ^ ((k >> 3) & 1))) = v;
-  }
-  h8 wh[KS], wl[KS];
-  auto w1_frag = [&](int kt) {
-    const int k = 32 * kt + r;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int off = k * KD + 8 * ((2 * ks + h) ^ ((k >> 3) & 1));
-      wh[ks] = *reinterpret_cast<const h8*>(sW1 + off);
-      wl[ks] = *reinterpret_cast<const h8*>(sW1 + HID * KD + off);
-    }
-  };
+  hc_dma<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
+  w1_stage<KD, NTHR>(N, sW1, tid);
   const int edz = N.tile_edz[tile];
   const float sdz = pow2(edz);
-  const float sz1 = pow2(-23);
-  const float u1 = pow2(23 - ex - edz - (int)N.sc[5]);
-  // dZ2^T n-tile nt of this wave's rows in accumulator form (register q <-> row n = acc_row(q, l)):
-  // one base address and constant offsets
-  const float* dzsrc = N.dz2t + (size_t)tile * HID * 32 + 4 * h * 32 + r;
-  auto dz_load = [&](int nt, float (&v)[16]) {
-    const float* b = dzsrc + (size_t)nt * 32 * 32;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = b[((q & 3) + 8 * (q >> 2)) * 32];
-  };
+  const float* dzp = N.dz2t + (size_t)tile * (16 * HID) + l * 8;
+  v4f d0 = *reinterpret_cast<const v4f*>(dzp), d1 = *reinterpret_cast<const v4f*>(dzp + 4);
   vm_drain();
   __syncthreads();
 
-#if RLKS_F1B_ONEPASS
-  // ---- one pass: the eight dH1 k-tile accumulators (AGPRs) over the 8 n-tiles; chunk nt = W2's
-  // w2t columns [32 nt, +32) of all 256 rows k ([256][32] hi / lo image), single-buffered through
-  // registers: a step computes from LDS while the next chunk and dZ2^T n-tile load into registers,
-  // then barrier / store / barrier.  Each dZ2^T element is read and split once.
-  {
-    f32x16 dh[8];
+  // ---- dH1 = dZ2 W2: 16 steps (n-step s, k-half ph) of 8 k-tiles x 3 MFMAs; the dZ2 fragment of
+  // n-step s is split at its first step and the next one loaded
+  f4 acc[16];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+  for (int kt = 0; kt < 16; ++kt) acc[kt] = f4zero();
+  h8 ah, al;
+  for (int s = 0; s < 8; ++s) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) dh[j][q] = 0.f;
-    v4u stg[32 / W];
-    float dzc[16], dzn[16];
-    chunk_load<W>(N, 8, w, l, stg);
-    dz_load(0, dzc);
-    vm_drain();
-    chunk_store<W>(sCh, w, l, stg);
-    __syncthreads();
-    for (int nt = 0; nt < 8; ++nt) {
-      if (nt < 7) {
-        chunk_load<W>(N, 9 + nt, w, l, stg);
-        dz_load(nt + 1, dzn);
+    for (int ph = 0; ph < 2; ++ph) {
+      const int st = 2 * s + ph;
+      if (st < 15) hc_dma<W>(N.w2th, N.w2tl, 128 * (ph ^ 1), 32 * (s + ph), sCh + (ph ^ 1) * 2 * H16, w, l);
+      if (ph == 0) {
+        const float dv[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
+        split8(dv, 0, sdz, ah, al);
+        if (s < 7) {
+          d0 = *reinterpret_cast<const v4f*>(dzp + (s + 1) * 512);
+          d1 = *reinterpret_cast<const v4f*>(dzp + (s + 1) * 512 + 4);
+        }
       }
-      h8 ah[2], al[2];
-      split8(dzc, 0, sdz, ah[0], al[0]);
-      split8(dzc, 8, sdz, ah[1], al[1]);
+      const _Float16* buf = sCh + ph * 2 * H16;
+      h8 ch, cl;
+      hc_frag(buf, 0, c, gq, ch, cl);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        h8 fc[2][2];
-        sf_frag(sCh, 32 * j + r, h, fc);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          dh[j] = mma(al[s], fc[s][0], dh[j]);
-          dh[j] = mma(ah[s], fc[s][1], dh[j]);
-          dh[j] = mma(ah[s], fc[s][0], dh[j]);
-        }
-      }
-      __syncthreads();
-      if (nt < 7) {
-        vm_drain();
-        chunk_store<W>(sCh, w, l, stg);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) dzc[q] = dzn[q];
-      }
-      __syncthreads();
-    }
-    // ---- dZ1 = dH1 (1 - H1^2) -> dW1a^T of the 8 k-tiles; sums over the W waves in the chunk
-    // buffer (free now), KPR k-tiles per round
-    constexpr int KT0 = 0, NKT = 8;
-#pragma unroll
-    for (int j = 0; j < NKT; ++j) {
-      const int kt = KT0 + j;
-      w1_frag(kt);
-      f32x16 z;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) z[q] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) z = mma3(xh[ks], xl[ks], wh[ks], wl[ks], z);
-      f32x16 dz;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float h1 = tanh_abs(z[q] * inv_z1);
-        dz[q] = dh[j][q] * (1.f - h1 * h1);
-      }
-      h8 zh[2], zl[2];
-      split16(dz, 0, sz1, zh[0], zl[0]);
-      split16(dz, 8, sz1, zh[1], zl[1]);
-      f32x16 wacc, wacc2;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) { wacc[q] = 0.f; wacc2[q] = 0.f; }
-      const h8 x0h = sXT[(w * 4 + 0) * 64 + l], x0l = sXT[(w * 4 + 1) * 64 + l];
-      const h8 x1h = sXT[(w * 4 + 2) * 64 + l], x1l = sXT[(w * 4 + 3) * 64 + l];
-      wacc = mma(x0l, zh[0], wacc);
-      wacc2 = mma(x1l, zh[1], wacc2);
-      wacc = mma(x0h, zl[0], wacc);
-      wacc2 = mma(x1h, zl[1], wacc2);
-      wacc = mma(x0h, zh[0], wacc);
-      wacc2 = mma(x1h, zh[1], wacc2);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) wacc[q] += wacc2[q];
-#pragma unroll
-      for (int gq = 0; gq < NG; ++gq) {
-        float4 v = {wacc[4 * gq] * u1, wacc[4 * gq + 1] * u1, wacc[4 * gq + 2] * u1, wacc[4 * gq + 3] * u1};
-        *reinterpret_cast<float4*>(sEp + (j % KPR) * SLOT + (w * 32 + r) * DWR + 8 * gq + 4 * h) = v;
-      }
-      if (j % KPR == KPR - 1) {
-        __syncthreads();
-        const int nd = D + 1, kt0 = kt + 1 - KPR;
-        for (int e = tid; e < KPR * 32 * nd; e += NTHR) {
-          const int jj = e / (32 * nd), e2 = e - jj * 32 * nd, kk = e2 / nd, d = e2 - kk * nd;
-          const int k = 32 * (kt0 + jj) + kk;
-          float sum = 0.f;
-#pragma unroll
-          for (int ww = 0; ww < W; ++ww) sum += sEp[jj * SLOT + (ww * 32 + kk) * DWR + d];
-          if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = sum;
-          else N.part_b1[(size_t)blk * HID + k] = sum;
-        }
-        __syncthreads();
-      }
-    }
-  }
-#else
-  // ---- two passes over the k-halves p: dH1 k-tiles 4p .. 4p+3 accumulate over the 8 n-tiles
-  // (24 MFMAs per n-tile step; half-chunks double-buffered), then their dZ1 and dW1a^T
-#pragma unroll 1
-  for (int p = 0; p < 2; ++p) {
-    f32x16 dh[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) dh[j][q] = 0.f;
-    float dzc[16], dzn[16];
-    dz_load(0, dzc);
-    for (int nt = 0; nt < 8; ++nt) {
-      if (nt < 7) {
-        half_dma<W>(N.w2th, N.w2tl, p, 32 * (nt + 1), sCh + ((nt + 1) & 1) * SF_CH, w, l);
-        dz_load(nt + 1, dzn);
-      }
-      const _Float16* buf = sCh + (nt & 1) * SF_CH;
-      h8 ah[2], al[2];
-      split8(dzc, 0, sdz, ah[0], al[0]);
-      split8(dzc, 8, sdz, ah[1], al[1]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        h8 fc[2][2];
-        half_frag(buf, 32 * j + r, h, fc);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          dh[j] = mma(al[s], fc[s][0], dh[j]);
-          dh[j] = mma(ah[s], fc[s][1], dh[j]);
-          dh[j] = mma(ah[s], fc[s][0], dh[j]);
-        }
+        h8 nh, nl;
+        if (j < 7) hc_frag(buf, j + 1, c, gq, nh, nl);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[8 * ph + j] = mm16x3(ah, al, ch, cl, acc[8 * ph + j]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (j < 7) { ch = nh; cl = nl; }
       }
       vm_drain();
       __syncthreads();
-      if (nt < 7)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) dzc[q] = dzn[q];
     }
-    // ---- dZ1 = dH1 (1 - H1^2) -> dW1a^T of k-tiles 4p + j; sums over the W waves in the chunk
-    // buffers (free now), KPR k-tiles per round
+  }
+
+  // ---- dZ1 = dH1 (1 - H1^2) (lane: rows m = 4g + i, column k = 16 kt + c), dW1a^T = Xa^T dZ1 per
+  // k-tile: dZ1 enters the split at 2^(e_dz + e_w2 - 23) (|dH1 2^(e_dz + e_w2)| <= 256 2^15 2^15)
+  h8 xh, xl;
+  const int ex = x_frag(g, row0, c, gq, xh, xl);
+  const float sx = pow2(ex), inv_z1 = N.sc[1] / sx;
+  h4 xth[DT], xtl[DT];  // Xa^T (16x16x16 A operand): rows d = 16 dt + c, columns m = 4g + j
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int kt = 4 * p + j;
-      w1_frag(kt);
-      f32x16 z;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) z[q] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) z = mma3(xh[ks], xl[ks], wh[ks], wl[ks], z);
-      f32x16 dz;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float h1 = tanh_abs(z[q] * inv_z1);
-        dz[q] = dh[j][q] * (1.f - h1 * h1);
-      }
-      h8 zh[2], zl[2];
-      split16(dz, 0, sz1, zh[0], zl[0]);
-      split16(dz, 8, sz1, zh[1], zl[1]);
-      f32x16 wacc, wacc2;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) { wacc[q] = 0.f; wacc2[q] = 0.f; }
-      const h8 x0h = sXT[(w * 4 + 0) * 64 + l], x0l = sXT[(w * 4 + 1) * 64 + l];
-      const h8 x1h = sXT[(w * 4 + 2) * 64 + l], x1l = sXT[(w * 4 + 3) * 64 + l];
-      wacc = mma(x0l, zh[0], wacc);
-      wacc2 = mma(x1l, zh[1], wacc2);
-      wacc = mma(x0h, zl[0], wacc);
-      wacc2 = mma(x1h, zl[1], wacc2);
-      wacc = mma(x0h, zh[0], wacc);
-      wacc2 = mma(x1h, zh[1], wacc2);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) wacc[q] += wacc2[q];
-#pragma unroll
-      for (int gq = 0; gq < NG; ++gq) {
-        float4 v = {wacc[4 * gq] * u1, wacc[4 * gq + 1] * u1, wacc[4 * gq + 2] * u1, wacc[4 * gq + 3] * u1};
-        *reinterpret_cast<float4*>(sEp + (j % KPR) * SLOT + (w * 32 + r) * DWR + 8 * gq + 4 * h) = v;
-      }
-      if (j % KPR == KPR - 1) {
-        __syncthreads();
-        const int nd = D + 1, kt0 = kt + 1 - KPR;
-        for (int e = tid; e < KPR * 32 * nd; e += NTHR) {
-          const int jj = e / (32 * nd), e2 = e - jj * 32 * nd, kk = e2 / nd, d = e2 - kk * nd;
-          const int k = 32 * (kt0 + jj) + kk;
-          float sum = 0.f;
-#pragma unroll
-          for (int ww = 0; ww < W; ++ww) sum += sEp[jj * SLOT + (ww * 32 + kk) * DWR + d];
-          if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = sum;
-          else N.part_b1[(size_t)blk * HID + k] = sum;
-        }
-        __syncthreads();
-      }
+      _Float16 a, b;
+      split1(xa_elem(g.x + (size_t)(row0 + 4 * gq + j) * stride, 16 * dt + c, D) * sx, a, b);
+      xth[dt][j] = a;
+      xtl[dt][j] = b;
     }
-    if (p == 0) {  // the second pass's first half-chunk (the buffers held the epilogue slots)
-      half_dma<W>(N.w2th, N.w2tl, 1, 0, sCh, w, l);
-      vm_drain();
+  const float sz1 = pow2(-23), u1 = pow2(23 - ex - edz - (int)N.sc[5]);
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt) {
+    h8 wh, wl;
+    w1_frag<KD>(sW1, kt, c, gq, wh, wl);
+    const f4 z = mm16x3(xh, xl, wh, wl, f4zero());  // Z1 rows m = 4g + i, column k = 16 kt + c
+    h4 zh, zl;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float h1 = tanh_abs(z[i] * inv_z1);
+      _Float16 a, b;
+      split1(acc[kt][i] * (1.f - h1 * h1) * sz1, a, b);
+      zh[i] = a;
+      zl[i] = b;
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const f4 dw = mk16x3(xth[dt], xtl[dt], zh, zl, f4zero());  // rows d = 16 dt + 4g + i, column k
+      const float4 v = {dw[0] * u1, dw[1] * u1, dw[2] * u1, dw[3] * u1};
+      *reinterpret_cast<float4*>(sEp + (kt % KPR) * SLOT + (w * 16 + c) * 16 * DT + 16 * dt + 4 * gq) = v;
+    }
+    if (kt % KPR == KPR - 1) {
       __syncthreads();
+      const int nd = D + 1, kt0 = kt + 1 - KPR;
+      for (int e = tid; e < KPR * 16 * nd; e += NTHR) {
+        const int jj = e / (16 * nd), e2 = e - jj * 16 * nd, kk = e2 / nd, d = e2 - kk * nd;
+        const int k = 16 * (kt0 + jj) + kk;
+        float sum = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) sum += sEp[jj * SLOT + (ww * 16 + kk) * 16 * DT + d];
+        if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = sum;
+        else N.part_b1[(size_t)blk * HID + k] = sum;
+      }
+      if (kt < 15) __syncthreads();
     }
   }
-
-#endif
 }
 
-template <int KD, int NG, int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sf_bwd(SfArgs g) {
-  if (blockIdx.y + g.net0 == 0) sf_bwd_body<0, KD, NG, W>(g);
-  else sf_bwd_body<1, KD, NG, W>(g);
-}
-
-// both nets in one grid (blockIdx.y + net0): the hardware backfills CUs across the two nets
-// instead of draining between two launches
-template <int A_, int KD, int NG, int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_sf_fwdbwd(SfArgs g) {
-  if (blockIdx.y + g.net0 == 0) sf_fwdbwd_body<A_, 0, KD, NG, W>(g);
-  else sf_fwdbwd_body<1, 1, KD, NG, W>(g);
+template <int KD, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_bwd(SfArgs g) {
+  if (blockIdx.y + g.net0 == 0) f1b_body<0, KD, W>(g);
+  else f1b_body<1, KD, W>(g);
 }
 
 // ----------------------------------------------------------------------------- F2
+typedef __fp16 hf4_t __attribute__((vector_size(8)));
+// ds_read_b64_tr_b16 (T10): per 16-lane group, 4 rows x 16 columns of 16-bit elements, lane i of
+// the group gets column i (row q in element q); EXEC must be all ones
+__device__ __forceinline__ h4 tr_read(const _Float16* p) {
+  const hf4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) hf4_t*)(p));
+  return __builtin_bit_cast(h4, v);
+}
 // grid (splits, 2 nets), 512 threads; wave w owns dW2 columns k = 32w + r, all 256 rows n.
 template <int KD>
 __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
@@ -1372,7 +822,7 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   const int net = blockIdx.y;
   const SfNet& N = g.n[net];
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  _Float16* sA = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][HID n][32 m perm]
+  _Float16* sA = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][32 m][HID n]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int D = g.D, stride = g.x_stride;
   const int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
@@ -1389,12 +839,14 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
     wl[ks] = *reinterpret_cast<const h8*>(N.w1l + (32 * w + r) * KD + 16 * ks + 8 * h);
   }
 
-  float db2[4] = {0.f, 0.f, 0.f, 0.f};
-  // dZ2^T tile t (32 KB) staged through registers: thread tid loads float4 f = tid + 512 i
-  // (row n = f >> 3, rows m 4 (f & 7) .. +3) one tile ahead, and splits it into an MFMA buffer at
-  // the end of the step.  (LDS-DMA would make the compiler wait for every outstanding LDS read,
-  // lgkmcnt(0), before each fragment's use while a DMA is in flight.)
-  using v4f = __attribute__((ext_vector_type(4))) float;
+  // db2 partial sums of the 8 rows n this thread's loads cover (two n-steps s, four n each)
+  float db2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // dZ2 of 32-row tile t = F1a's 16-row tiles 2t, 2t + 1 in their lane-native order
+  // [T][s][lane (g, c)][8]: float4 f = tid + 512 i holds rows n = 32 s + 16 (f & 1) + 4 g + 0..3 of
+  // row m = 16 T + c, with T = f >> 10, s = (f >> 7) & 7, lane (f >> 1) & 63.  Staged through
+  // registers one tile ahead, split with the step's max |dZ2| scale and stored as an [m][n] image
+  // (32 rows of 256 halves, 8-byte quads of n at quad (n >> 2) ^ 8 (m & 3)) that the fragment reads
+  // transpose (ds_read_b64_tr_b16).
   v4f dv[4];
   auto load = [&](int t) {
 #pragma unroll
@@ -1405,22 +857,33 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
     _Float16* b = sA + buf * 2 * SF_CH;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int f = tid + 512 * i, n = f >> 3, c = f & 7;
+      const int f = tid + 512 * i, lf = (f >> 1) & 63;
+      const int m = 16 * (f >> 10) + (lf & 15), q0 = 8 * ((f >> 7) & 7) + 4 * (f & 1) + (lf >> 4);
       const v4f v = dv[i];
-      db2[i] += (v[0] + v[1]) + (v[2] + v[3]);
       h4 hi, lo;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        db2[(i & 1) * 4 + j] += v[j];
         _Float16 a, bb;
         split1(v[j] * sg, a, bb);
         hi[j] = a;
         lo[j] = bb;
       }
-      const int pc = 2 * (c >> 2) + (c & 1);
-      const int off = n * 32 + 8 * (pc ^ ((n >> 2) & 3)) + 4 * ((c >> 1) & 1);
+      const int off = m * HID + 4 * (q0 ^ (8 * (m & 3)));
       *reinterpret_cast<h4*>(b + off) = hi;
       *reinterpret_cast<h4*>(b + SF_CH + off) = lo;
     }
+  };
+  // A fragment (32x32x16: row n = 32 nt + r, k = m of k-step s in the accumulator row order
+  // 16 s + 8 (j >> 2) + 4 h + (j & 3)): two transposed reads of 4 rows m x 16 columns n per 16-lane
+  // group; lane 4 q + p of the group addresses row m0 + q, columns n_base + 4 p .. + 3
+  const int tq = (l & 15) >> 2, tp = l & 3, tcol = 16 * ((l >> 4) & 1);
+  auto afrag = [&](const _Float16* b, int nt, int s, h8& fh, h8& fl) {
+    const int m0 = 16 * s + 4 * h + tq, qd = ((32 * nt + tcol) >> 2) + tp;
+    const int o0 = m0 * HID + 4 * (qd ^ (8 * tq)), o1 = o0 + 8 * HID;
+    const h4 a0 = tr_read(b + o0), a1 = tr_read(b + o1), c0 = tr_read(b + SF_CH + o0), c1 = tr_read(b + SF_CH + o1);
+    fh = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+    fl = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
   };
 
   f32x16 acc[8];
@@ -1513,12 +976,10 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
     if (NT_H1 < 0) h1(tc, th, nbh, nbl);  // tile t + 1's H1
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
-      const int n = 32 * nt + r;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int off = n * 32 + 8 * ((2 * s + h) ^ ((n >> 2) & 3));
-        const h8 ah = *reinterpret_cast<const h8*>(b + off);
-        const h8 al = *reinterpret_cast<const h8*>(b + SF_CH + off);
+        h8 ah, al;
+        afrag(b, nt, s, ah, al);
         acc[nt] = mma3(ah, al, bh[s], bl[s], acc[nt]);
       }
       if (nt == NT_STORE && more) store(buf ^ 1);              // tile t + 1 -> other buffer
@@ -1529,58 +990,39 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
     for (int s = 0; s < 2; ++s) { bh[s] = nbh[s]; bl[s] = nbl[s]; }
     __syncthreads();
   };
-#if RLKS_F2_PHASES
   if (KD == 16 && (w & 4))
     for (int t = t0; t < t1; ++t) step(std::integral_constant<int, 1>{}, t);
   else
-#endif
     for (int t = t0; t < t1; ++t) step(std::integral_constant<int, 0>{}, t);
   float* out = N.part_w2 + (size_t)blockIdx.x * SF_W2_PSTRIDE;
-#ifdef RLKS_F2_NOSTORE  // timing experiment only: the partials are not written
-  if (acc[0][0] != 12345.f) return;
-#endif
 #pragma unroll
   for (int nt = 0; nt < 8; ++nt)
 #pragma unroll
     for (int q = 0; q < 16; ++q) out[(size_t)(32 * nt + acc_row(q, l)) * HID + 32 * w + r] = acc[nt][q] * unscale;
-  // db2: the 8 threads tid & ~7 .. | 7 hold row n = (tid + 512 i) >> 3
+  // db2: the 16 lanes c = (tid >> 1) & 15 of a wave hold the same rows n = 32 s + 16 (tid & 1) +
+  // 4 ((tid >> 5) & 3) + j, s = (tid >> 7) + 4 (i & 1)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float v = db2[i];
-    v += __shfl_xor(v, 1, 64);
+  for (int k = 0; k < 8; ++k) {
+    float v = db2[k];
     v += __shfl_xor(v, 2, 64);
     v += __shfl_xor(v, 4, 64);
-    if ((tid & 7) == 0) N.part_b2[(size_t)blockIdx.x * HID + ((tid + 512 * i) >> 3)] = v;
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    db2[k] = v;
   }
+  if (((tid >> 1) & 15) == 0)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      N.part_b2[(size_t)blockIdx.x * HID + 32 * ((tid >> 7) + 4 * (k >> 2)) + 16 * (tid & 1) + 4 * ((tid >> 5) & 3) +
+                (k & 3)] = db2[k];
 }
 
 // ----------------------------------------------------------------------------- launchers
 #ifdef RLKS_STAMPS
-extern "C" int rlks_dbg_sf_stamps(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sf_stamps), sizeof(g_sf_stamps)) == hipSuccess ? 0 : 1;
-}
-extern "C" int rlks_dbg_sf_stamps2(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sf_stamps2), sizeof(g_sf_stamps2)) == hipSuccess ? 0 : 1;
-}
 extern "C" int rlks_dbg_fa_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fa_stamps), sizeof(g_fa_stamps)) == hipSuccess ? 0 : 1;
 }
 #endif
-
-size_t sf_f1_lds_bytes(int A_, int NG, int KD, int W) {
-  return (size_t)2 * 2 * SF_CH * sizeof(_Float16) + (size_t)(HID + A_ * HID) * sizeof(float) +
-         (size_t)2 * HID * KD * sizeof(_Float16) + (size_t)W * 4 * 64 * 16;
-}
-
-// F1 as two kernels (F1a k_sf_fwd + F1b k_sf_bwd, two workgroups per CU) or the fused one-wave-
-// per-SIMD kernel: RLKS_F1_SPLIT=0 / 1 overrides the default
-bool sf_f1_split() {
-  static const int v = [] {
-    const char* e = getenv("RLKS_F1_SPLIT");
-    return e ? atoi(e) : RLKS_F1_SPLIT_DEFAULT;
-  }();
-  return v != 0;
-}
 
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
   if (!a.skip_wmax) {
@@ -1592,28 +1034,19 @@ int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
   return RLKS_OK;
 }
 
-template <int A_, int KD, int NG>
+template <int A_, int KD>
 static int launch_f1_net(SfArgs a, int net0, int nets, hipStream_t s, int halves) {
   constexpr int W = SF_F1_W;
   a.net0 = net0;
-  const dim3 grid(a.M / (32 * W), nets);
-  if (sf_f1_split()) {
-    const size_t lds_a = (size_t)2 * SF_CH * sizeof(_Float16) + (size_t)(1 + A_) * HID * sizeof(float) +
-                         (size_t)2 * HID * KD * sizeof(_Float16);
-    const size_t lds_b = (size_t)2 * SF_CH * sizeof(_Float16) + (size_t)2 * HID * KD * sizeof(_Float16) +
-                         (size_t)W * 4 * 64 * 16;
-    if (halves & 1) {
-      hipLaunchKernelGGL((k_sf_fwd<A_, KD, W>), grid, dim3(64 * W), lds_a, s, a);
-      RLKS_LAUNCHED();
-    }
-    if (halves & 2) {
-      hipLaunchKernelGGL((k_sf_bwd<KD, NG, W>), grid, dim3(64 * W), lds_b, s, a);
-      RLKS_LAUNCHED();
-    }
-    return RLKS_OK;
+  const dim3 grid(a.M / (16 * W), nets);
+  if (halves & 1) {  // pi's LDS (A_ >= 1) covers the value net's
+    hipLaunchKernelGGL((k_sf_fwd<A_, KD, W>), grid, dim3(64 * W), (f1a_lds_bytes<A_, KD, W>()), s, a);
+    RLKS_LAUNCHED();
   }
-  hipLaunchKernelGGL((k_sf_fwdbwd<A_, KD, NG, W>), grid, dim3(64 * W), sf_f1_lds_bytes(A_, NG, KD, W), s, a);
-  RLKS_LAUNCHED();
+  if (halves & 2) {
+    hipLaunchKernelGGL((k_sf_bwd<KD, W>), grid, dim3(64 * W), f1b_lds_bytes<KD>(), s, a);
+    RLKS_LAUNCHED();
+  }
   return RLKS_OK;
 }
 
@@ -1624,9 +1057,9 @@ int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int 
   RLKS_REQUIRE(a.M % SF_ROWS == 0, RLKS_ERR_ARG, "split-fp16 SGD step: rows must be a multiple of 256");
   RLKS_REQUIRE(a.D == 3 * A, RLKS_ERR_UNSUPPORTED, "split-fp16 SGD step expects obs_dim = 3 x n_actions");
   switch (A) {
-    case 2: return launch_f1_net<2, 16, 1>(a, net0, nets, s, halves);
-    case 4: return launch_f1_net<4, 16, 2>(a, net0, nets, s, halves);
-    case 8: return launch_f1_net<8, 32, 4>(a, net0, nets, s, halves);
+    case 2: return launch_f1_net<2, 16>(a, net0, nets, s, halves);
+    case 4: return launch_f1_net<4, 16>(a, net0, nets, s, halves);
+    case 8: return launch_f1_net<8, 32>(a, net0, nets, s, halves);
     default: return fail(RLKS_ERR_UNSUPPORTED, "split-fp16 head is built for 2, 4 or 8 actions");
   }
 }

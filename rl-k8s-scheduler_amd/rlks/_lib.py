@@ -91,6 +91,8 @@ SIGNATURES = {
     "rlks_env_config": [_P, C.POINTER(EnvCfg)],
     "rlks_env_seed": [_P, _P, _P, _P, _I, _P],
     "rlks_env_mt_discard": [_P, _P, _P, _P],
+    "rlks_env_mt_words": [_P, C.c_int, _P, C.c_int, _P],
+    "rlks_sample_categorical": [_P, C.c_int, C.c_int, _P, C.c_ulonglong, C.c_int, _P, _P, _P],
     "rlks_env_reset": [_P, _P, _P, _P],
     "rlks_env_step": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "rlks_env_sample_step": [_P, _P, _I, _P, _P, _P, _P, _P, _P],
@@ -133,7 +135,6 @@ SIGNATURES = {
                                 C.POINTER(GatherNext), _P, _I64, _P],
     "rlks_ppo_adam_apply": [C.POINTER(MlpDesc), _P, _P, _P, _P, _I64, _F, _F, _F, _F, _I, _P, _I64, _I, _P],
     "rlks_kl_update": [_P, _P, _F, _P],
-    "rlks_sf_f1_split": [],
 }
 _RESTYPES = {"rlks_last_error": C.c_char_p, "rlks_version": C.c_char_p}
 

@@ -8,11 +8,16 @@
     normal_scheduler_step(obs); render(); close()
     errors: AssertionError("Invalid action ...") (:116), IndexError past the table (:91 via :144),
             FileNotFoundError for a missing table (:56-64)
-and runs on one GPU lane.  Its utilisation noise uses CPython's MT19937 per env (noise="mt19937"),
-so with a seeded reset the observations are bit-identical to the reference.  Deliberate
-difference: the reference draws from the process-global `random` stream; here each env owns its
-generator (needed for batching).  reset(seed) still reseeds `random` and `np.random` as the
-reference does (:109-111), and an env that was never seeded takes its seed from `random`.
+and runs on one GPU lane.  Its utilisation noise is CPython's MT19937 (noise="mt19937"), so with a
+seeded reset the observations are bit-identical to the reference.  The reference draws that noise
+from the process-global `random` stream (:87) and reseeds it in reset (:109-111):
+  noise_stream="global" (or env_config={"noise_stream": "global"}) reproduces exactly that: the
+    lane's MT19937 state is loaded from random.getstate() before every reset / step and written
+    back with random.setstate() after it, so all envs of the process and the caller's own random
+    draws share one stream in call order (tests/golden/global_stream.npz);
+  noise_stream="instance" (the default) gives each env a private generator: no host round trip of
+    the 2.5 KB state per step; an env never seeded takes its seed from `random`.  Both reseed
+    `random` and `np.random` in reset(seed) as the reference does.
 
 `VecK8sMultiCloudEnv` is the batched form over device tensors (one lane per env, auto-reset,
 Philox noise by default) used by the rollout engine.
@@ -259,8 +264,17 @@ class K8sMultiCloudEnv(_EnvBase):
 
     metadata = {"render_modes": []}
 
-    def __init__(self, env_config=None, fast_mode=True, *, data_path=None, device=None, noise="mt19937"):
-        # env_config is accepted and ignored, as in the reference (:46)
+    def __init__(self, env_config=None, fast_mode=True, *, data_path=None, device=None, noise="mt19937",
+                 noise_stream=None):
+        # env_config is accepted as in the reference (:46), which ignores it; here it may carry
+        # "noise_stream" (module docstring)
+        if noise_stream is None:
+            noise_stream = (env_config or {}).get("noise_stream", "instance") if isinstance(env_config, dict) else "instance"
+        if noise_stream not in ("instance", "global"):
+            raise ValueError(f"noise_stream must be 'instance' or 'global', got {noise_stream!r}")
+        if noise_stream == "global" and noise != "mt19937":
+            raise ValueError("noise_stream='global' needs the MT19937 noise mode")
+        self.noise_stream = noise_stream
         self.fast_mode = fast_mode  # slow mode's kubernetes dry-run is out of scope
         self.action_space = Discrete(2)  # 0 = AWS, 1 = Azure (:51)
         self.observation_space = Box(low=0.0, high=1.0, shape=(6,), dtype=np.float32)  # (:52)
@@ -280,23 +294,43 @@ class K8sMultiCloudEnv(_EnvBase):
         self._status = torch.zeros(2, dtype=torch.int32, device=d)
         self._keys = torch.zeros(1, 8, dtype=torch.int32, device=d)
         self._keylen = torch.zeros(1, dtype=torch.int32, device=d)
+        self._mtw = torch.zeros(625, dtype=torch.int32, device=d)  # global stream: the lane's MT19937 state
         self._seeded = False
 
     # ------------------------------------------------------------------ gymnasium surface
     def reset(self, seed=None, options=None):
-        torch = _torch()
         if seed is not None:
             random.seed(seed)       # process-global side effects of the reference (:109-111)
             np.random.seed(seed)
+        if self.noise_stream == "global":
+            self._push_global()
+        elif seed is not None:
             self._seed_lane(seed)
         elif not self._seeded:
             self._seed_lane(random.getrandbits(64))
         s = self._dev.stream
         _lib.call("rlks_env_reset", self._dev.handle, None, _lib.ptr(self._obs), s)
+        if self.noise_stream == "global":
+            self._pull_global()
         self.current_step = 0
         obs = self._obs.cpu().numpy()[0].copy()
-        del torch
         return obs, {}
+
+    def _push_global(self):
+        """the process-global `random` state -> this env's lane (CPython getstate layout: 624 words
+        and the position, rlks_env_mt_words)"""
+        import torch
+
+        words = np.array(random.getstate()[1], dtype=np.uint32)
+        self._mtw.copy_(torch.from_numpy(words.view(np.int32)))
+        _lib.call("rlks_env_mt_words", self._dev.handle, 0, _lib.ptr(self._mtw), 1, self._dev.stream)
+
+    def _pull_global(self):
+        """the lane's state after its draws -> the process-global `random` (gauss_next kept)"""
+        _lib.call("rlks_env_mt_words", self._dev.handle, 0, _lib.ptr(self._mtw), 0, self._dev.stream)
+        words = self._mtw.cpu().numpy().view(np.uint32)
+        version, _, gauss = random.getstate()
+        random.setstate((version, tuple(int(x) for x in words), gauss))
 
     def _seed_lane(self, seed):
         import torch
@@ -316,9 +350,13 @@ class K8sMultiCloudEnv(_EnvBase):
         assert self.action_space.contains(action), f"Invalid action {action}"
         a = int(action)
         self._act.fill_(a)
+        if self.noise_stream == "global":
+            self._push_global()
         _lib.call("rlks_env_step", self._dev.handle, _lib.ptr(self._act), _lib.ptr(self._obs), _lib.ptr(self._rew),
                   None, _lib.ptr(self._term), None, _lib.ptr(self._step), None, _lib.ptr(self._status),
                   self._dev.stream)
+        if self.noise_stream == "global":
+            self._pull_global()
         status = self._status.cpu().numpy()
         self.current_step = int(self._step.item())
         if status[1]:

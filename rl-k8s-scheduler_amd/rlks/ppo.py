@@ -72,7 +72,9 @@ class PPOConfig:
         self.evaluation_interval = None
         self.evaluation_duration = 10
         self.metrics_num_episodes_for_smoothing = 100
-        self.checkpoint_env_state = True  # save() includes the lanes' env state (node state too)
+        # save() includes the lanes' env state: None = yes for table envs (~30 B per lane), no for
+        # node-level envs (C x nodes x 8 B per lane: ~1 GB at c3, written on every save())
+        self.checkpoint_env_state = None
         # minibatches are drawn per block of lanes (rlks_ppo_gather_grouped): None = one block per
         # rank.  A single-rank run with num_lane_groups = W trains exactly like W ranks.
         self.num_lane_groups = None
@@ -142,7 +144,12 @@ class PPOConfig:
 
     def reporting(self, metrics_num_episodes_for_smoothing=None, **kw):
         if metrics_num_episodes_for_smoothing is not None:
-            self.metrics_num_episodes_for_smoothing = int(metrics_num_episodes_for_smoothing)
+            w = int(metrics_num_episodes_for_smoothing)
+            # the window is filled from the device episode log, which keeps RLKS_EPLOG_CAP episodes
+            # per rank and iteration (rlks_env_episode_log)
+            if not 1 <= w <= _lib.RLKS_EPLOG_CAP:
+                raise ValueError(f"metrics_num_episodes_for_smoothing must be in [1, {_lib.RLKS_EPLOG_CAP}], got {w}")
+            self.metrics_num_episodes_for_smoothing = w
         return self
 
     def debugging(self, seed=None, **kw):
@@ -241,9 +248,12 @@ class PPO:
         if self.n_mb == 0:
             raise ValueError("train batch is smaller than one minibatch")
         groups = int(cfg.num_lane_groups or self.world)
-        if groups % self.world or self.N % (groups // self.world) or self.mb % (groups // self.world):
+        if (groups % self.world or self.N % (groups // self.world) or self.mb % (groups // self.world)
+                or groups // self.world > 64):
+            # 64 = the gather's lane-group limit (ppo.hip MAX_GROUPS); shares above 8 (NEXT_GROUPS)
+            # gather in a launch of their own instead of inside the gradient reduce
             raise ValueError(f"num_lane_groups {groups} must be a multiple of the {self.world} ranks and its per-rank "
-                             f"share must divide the {self.N} lanes and the {self.mb}-row minibatch")
+                             f"share (at most 64) must divide the {self.N} lanes and the {self.mb}-row minibatch")
         self.groups = groups // self.world
         self.group0 = self.rank * self.groups
         seed = cfg.seed if cfg.seed is not None else 0
@@ -313,6 +323,8 @@ class PPO:
         # the previous SGD step was a fused one on the current parameters (rlks_ppo_sgd_step)
         self._fused_prev = False
         self._ep_history = collections.deque(maxlen=max(1, int(cfg.metrics_num_episodes_for_smoothing)))
+        self._ar_events = None  # profile_allreduce(): (start, end) events of each gradient all-reduce
+        self.sample_calls = 0   # compute_actions / compute_single_action draws so far (Philox counter)
         self.iteration = 0
         self.timesteps_total = 0
         self.episodes_total = 0
@@ -387,7 +399,14 @@ class PPO:
         _lib.call("rlks_ppo_grad_step_next", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat),
                   _lib.ptr(self.dyn), _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row),
                   self.adam_step, int(self._fused_prev), nxt, _lib.ptr(self.ws), self.ws.numel(), s)
+        if self._ar_events is not None:  # profile_allreduce(): events on the launch stream around it
+            e0 = self.torch.cuda.Event(enable_timing=True)
+            e0.record(self.torch.cuda.current_stream(self.device))
         self._allreduce(self.grad)
+        if self._ar_events is not None:
+            e1 = self.torch.cuda.Event(enable_timing=True)
+            e1.record(self.torch.cuda.current_stream(self.device))
+            self._ar_events.append((e0, e1))
         _lib.call("rlks_ppo_adam_apply", desc, _lib.ptr(self.params.flat), _lib.ptr(self.grad), _lib.ptr(self.adam_m),
                   _lib.ptr(self.adam_v), self.params.padded, float(self.config.lr), float(beta1), float(beta2),
                   float(self.config.adam_eps), self.adam_step, _lib.ptr(self.ws), self.ws.numel(), self.mb, s)
@@ -416,6 +435,33 @@ class PPO:
         _lib.call("rlks_env_episode_stats", self.env.handle, _lib.ptr(self.ep_stats), 1, self.stream)
         self.iteration += 1
         self.timesteps_total += self.samples * self.world
+
+    def profile_allreduce(self):
+        """one PPO iteration with HIP events on the launch stream around every per-SGD-step gradient
+        all-reduce (multi-rank only): where the data-parallel time goes.  Returns None
+        on one rank, else the all-reduce's mean / max duration per SGD step, its total and its share
+        of the iteration, the maximum over ranks of each."""
+        if self.world == 1:
+            return None
+        torch = self.torch
+        st = torch.cuda.current_stream(self.device)
+        self._ar_events = []
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record(st)
+        self.train_step_no_sync()
+        t1.record(st)
+        t1.synchronize()
+        ar = [a.elapsed_time(b) for a, b in self._ar_events]
+        self._ar_events = None
+        it_ms = t0.elapsed_time(t1)
+        v = torch.tensor([sum(ar) / len(ar), max(ar), sum(ar), it_ms], dtype=torch.float64, device=self.device)
+        d = ddp.group()
+        d.all_reduce(v, op=d.ReduceOp.MAX)
+        mean_ms, max_ms, total_ms, it_ms = (float(x) for x in v.cpu())
+        return {"allreduce_ms_per_sgd_step": mean_ms, "allreduce_ms_max": max_ms, "sgd_steps": len(ar),
+                "allreduce_ms_per_iteration": total_ms, "iteration_ms": it_ms,
+                "allreduce_share_of_iteration": total_ms / it_ms if it_ms > 0 else None,
+                "bytes_per_allreduce": int(self.grad.numel() * 4), "backend": d.get_backend()}
 
     # ------------------------------------------------------------------ RLlib surface
     def _episode_returns(self):
@@ -511,26 +557,46 @@ class PPO:
         result["time_this_iter_s"] = time.time() - t0
         return result
 
+    # Philox counter word 0 of policy-side draws (compute_actions / compute_single_action): no env
+    # lane has this id, so these draws never repeat a rollout draw under the same key (config.seed)
+    SAMPLER_ID = 0xFFFFFFFF
+
+    def _sample(self, logits, explore):
+        """TorchCategorical sample (explore) or argmax of logits [n, A] on the device sampler
+        (rlks_sample_categorical): row i draws Philox({SAMPLER_ID, i, call counter, ACTION},
+        key = config.seed), so a run's exploring actions follow from the seed and the number of
+        earlier calls (the counter is checkpointed)"""
+        torch = self.torch
+        n = logits.shape[0]
+        logits = logits.contiguous()
+        act = torch.empty(n, dtype=torch.int32, device=self.device)
+        ids = None
+        if explore:
+            idh = np.zeros((n, 3), np.uint32)
+            idh[:, 0] = self.SAMPLER_ID
+            idh[:, 1] = np.arange(n, dtype=np.uint32)
+            idh[:, 2] = self.sample_calls & 0xFFFFFFFF
+            ids = torch.from_numpy(idh.view(np.int32)).to(self.device)
+            self.sample_calls += 1
+        _lib.call("rlks_sample_categorical", _lib.ptr(logits), n, logits.shape[1], _lib.ptr(ids) if ids is not None else None,
+                  self.seed & 0xFFFFFFFFFFFFFFFF, int(bool(explore)), _lib.ptr(act), None, self.stream)
+        return act
+
     def compute_actions(self, obs, explore=None):
         """batched actions for obs [n, D] (device or host); returns an int32 device tensor"""
         torch = self.torch
         explore = self.config.explore if explore is None else explore
         o = torch.as_tensor(obs, dtype=torch.float32, device=self.device).reshape(-1, self.D)
         logits, _ = self.params.forward(o)
-        if not explore:
-            return torch.argmax(logits, dim=1).to(torch.int32)
-        return torch.distributions.Categorical(logits=logits).sample().to(torch.int32)
+        return self._sample(logits, explore)
 
     def compute_single_action(self, observation=None, state=None, *, explore=None, **kw):
+        """RLlib Algorithm.compute_single_action (eval_ppo.py:27 explores by default,
+        final_evaluation.py:48 passes explore=False): one observation -> int action"""
         explore = self.config.explore if explore is None else explore
         o = np.asarray(observation, dtype=np.float32).reshape(1, self.D)
         logits, _ = self.params.forward(self.torch.from_numpy(o).to(self.device))
-        lg = logits.cpu().numpy()[0].astype(np.float64)
-        if not explore:
-            return int(np.argmax(lg))
-        p = np.exp(lg - lg.max())
-        p /= p.sum()
-        return int(np.random.choice(len(p), p=p))
+        return int(self._sample(logits, explore).item())
 
     def current_obs(self):
         """the lanes' current observations [N, D] (device)"""
@@ -551,18 +617,27 @@ class PPO:
             "iteration": self.iteration, "timesteps_total": self.timesteps_total,
             "episodes_total": self.episodes_total, "lane_steps": steps.cpu(), "lane_episodes": eps.cpu(),
             "episode_history": [float(x) for x in self._ep_history],
+            "sample_calls": self.sample_calls,
             "rank": self.rank, "world": self.world,
         }
-        if self.config.checkpoint_env_state:
+        if self._checkpoint_env_state():
             st["env_state"] = self.env.save_state().cpu()
             st["current_obs"] = self.current_obs().detach().cpu().clone()
         return st
+
+    def _checkpoint_env_state(self):
+        v = self.config.checkpoint_env_state
+        return self.config.nodes is None if v is None else bool(v)
 
     def save(self, checkpoint_dir=None):
         """RLlib Algorithm.save(): writes <dir>/checkpoint_<iter:06d>/ and returns its path.
         Files: state.pt (tensors, weights_only-loadable), algorithm_state.json (config + scalars),
         table.npz (the env table's float64 bits) and, with checkpoint_env_state, env_state.bin
-        (raw device snapshot, rlks_env_save_state; rank-suffixed when world > 1)."""
+        (raw device snapshot, rlks_env_save_state; rank-suffixed when world > 1).  The snapshot is
+        rlks_env_state_bytes per rank: ~30 B per lane for table envs, plus clusters x nodes x 8 B
+        per lane for node-level envs (about 1 GB at c3's 65,536 x 8 x 256, hence off by default
+        there).  Multi-rank: every rank writes its own files, rank 0 the shared ones, then all
+        ranks meet at a barrier."""
         import torch
 
         base = Path(checkpoint_dir) if checkpoint_dir else Path.home() / "rlks_results" / "PPO"
@@ -583,15 +658,21 @@ class PPO:
             self.table.save(path / "table.npz")
             meta = {"state": st, "config": self.config.to_dict()}
             (path / "algorithm_state.json").write_text(json.dumps(meta, indent=1, default=str))
+        if self.world > 1:  # a restore right after save() sees every rank's files
+            ddp.group().barrier()
         return str(path)
 
     def restore(self, checkpoint_path):
         import torch
 
         path = Path(checkpoint_path)
+        meta = json.loads((path / "algorithm_state.json").read_text())["state"]
+        saved_world = int(meta.get("world", 1))
+        if saved_world != self.world:
+            raise ValueError(f"checkpoint {path} was written by {saved_world} rank(s); this run has {self.world} "
+                             "(per-rank env lanes and files do not transfer between world sizes)")
         sfx = f".rank{self.rank}" if self.world > 1 else ""
         tensors = torch.load(path / f"state{sfx}.pt", weights_only=True)
-        meta = json.loads((path / "algorithm_state.json").read_text())["state"]
         sd = {k[len("weights/"):]: v for k, v in tensors.items() if k.startswith("weights/")}
         w = self.params.state_dict()
         for k, v in w.items():
@@ -608,6 +689,7 @@ class PPO:
         self.episodes_total = int(meta["episodes_total"])
         self._ep_history.clear()
         self._ep_history.extend(meta.get("episode_history", []))
+        self.sample_calls = int(meta.get("sample_calls", 0))
         es = path / f"env_state{sfx}.bin"
         if es.exists() and "current_obs" in tensors:
             self.env.load_state(np.fromfile(es, dtype=np.uint8))

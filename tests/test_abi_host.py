@@ -185,3 +185,18 @@ def test_oracle_ppo_grad_matches_finite_differences():
         fm[i] -= eps
         fd = (loss(fp) - loss(fm)) / (2 * eps)
         assert abs(fd - g[i]) <= 1e-6 * max(1.0, abs(g[i])), (i, fd, g[i])
+
+
+def test_reporting_window_is_bounded_by_the_episode_log():
+    """metrics_num_episodes_for_smoothing is filled from the device episode log (RLKS_EPLOG_CAP
+    episodes per rank and iteration): a larger window is rejected instead of silently reporting a
+    shorter mean"""
+    from rlks import _lib
+    from rlks.ppo import PPOConfig
+
+    assert PPOConfig().reporting(metrics_num_episodes_for_smoothing=100).metrics_num_episodes_for_smoothing == 100
+    assert PPOConfig().reporting(metrics_num_episodes_for_smoothing=_lib.RLKS_EPLOG_CAP)
+    with pytest.raises(ValueError):
+        PPOConfig().reporting(metrics_num_episodes_for_smoothing=_lib.RLKS_EPLOG_CAP + 1)
+    c = PPOConfig()
+    assert c.checkpoint_env_state is None  # auto: table envs yes, node-level envs no

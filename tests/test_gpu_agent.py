@@ -235,6 +235,7 @@ def test_checkpoint_resume_is_exact(tmp_path, kind):
     if kind == "nodes":
         cfg.table = synthetic_table(4, 100, seed=3)
         cfg.nodes = NodeSpec(4, 16, arrival_rate=2.0, depart_prob=0.05, reject_penalty=0.1)
+        cfg.checkpoint_env_state = True  # off by default for node-level envs (size)
     a = PPO(config=cfg, device=d)
     a.train()
     a.train()   # episodes complete at step 99: the second iteration crosses them
@@ -417,3 +418,49 @@ def test_sf16_gradient_per_element(rows, D, H, A, precision):
           f"fp32 {b[0]:.2e}/{b[1]:.2e}/{b[2]:.2e}/{r32.max():.2e}")
     for x, y, q in zip(a, b, qs):
         assert x <= 4 * y + 1e-9, f"p{q}: split-fp16 {x:.3e} vs fp32 {y:.3e}"
+
+
+def test_compute_single_action_samples_on_device_philox():
+    """compute_single_action(obs) with exploration (eval_ppo.py:27) draws on the device Philox
+    sampler, keyed by (config seed, call counter): the draws are the oracle's TorchCategorical
+    restatement (oracle.sample_actions) of the same logits and counters, reproducible from the seed,
+    and a checkpoint resumes the counter; explore=False is the argmax (final_evaluation.py:48)"""
+    from rlks.ppo import PPO
+
+    d = _dev()
+    cfg = _cfg(256, 8, 1024, epochs=1, seed=77)
+    a, b = PPO(config=cfg, device=d), PPO(config=cfg, device=d)
+    rng = np.random.default_rng(5)
+    obs = rng.random((300, 6)).astype(np.float32)
+    acts = [a.compute_single_action(o) for o in obs]
+    assert acts == [b.compute_single_action(o) for o in obs]  # same seed, same call sequence
+    logits, _ = a.params.forward(torch.from_numpy(obs).to(d))
+    lg = logits.detach().cpu().numpy()
+    ref, margin = oracle.sample_actions(lg, np.full(300, PPO.SAMPLER_ID, np.uint32), np.zeros(300, np.uint32),
+                                        np.arange(300, dtype=np.uint32), 77)
+    close = margin < 4  # within 4 float32 ulp of a CDF boundary: device expf vs numpy may differ
+    assert close.mean() < 1e-2
+    np.testing.assert_array_equal(np.array(acts)[~close], ref[~close])
+    assert len(set(acts)) == 2  # both actions appear
+    np.testing.assert_array_equal([a.compute_single_action(o, explore=False) for o in obs[:50]], lg[:50].argmax(1))
+    # batched: row i of call k draws counter {SAMPLER_ID, i, k}
+    k0 = a.sample_calls
+    batch = a.compute_actions(obs).cpu().numpy()
+    refb, mb = oracle.sample_actions(lg, np.full(300, PPO.SAMPLER_ID, np.uint32), np.arange(300, dtype=np.uint32),
+                                     np.full(300, k0, np.uint32), 77)
+    np.testing.assert_array_equal(batch[mb >= 4], refb[mb >= 4])
+
+
+def test_restore_rejects_another_world_size(tmp_path):
+    """a checkpoint records its world size; restoring it into a run with another one fails with a
+    clear error before any tensor is loaded"""
+    from rlks.ppo import PPO
+
+    d = _dev()
+    a = PPO(config=_cfg(256, 8, 1024, epochs=1, seed=3), device=d)
+    path = Path(a.save(tmp_path))
+    meta = json.loads((path / "algorithm_state.json").read_text())
+    meta["state"]["world"] = 2
+    (path / "algorithm_state.json").write_text(json.dumps(meta))
+    with pytest.raises(ValueError, match="rank"):
+        a.restore(path)

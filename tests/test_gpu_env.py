@@ -60,14 +60,16 @@ def test_mt19937_device_matches_cpython(mt_draws):
 POLICIES = ["all0", "all1", "rr", "greedy", "rand"]
 
 
+@pytest.mark.parametrize("stream", ["instance", "global"])
 @pytest.mark.parametrize("seed", [0, 7, 42])
 @pytest.mark.parametrize("pol", POLICIES)
-def test_dropin_env_replays_reference(traces, traces_meta, seed, pol):
-    """K8sMultiCloudEnv (GPU lane, MT19937 noise) reproduces the reference env bit for bit"""
+def test_dropin_env_replays_reference(traces, traces_meta, seed, pol, stream):
+    """K8sMultiCloudEnv (GPU lane, MT19937 noise) reproduces the reference env bit for bit, with a
+    private noise generator and on the process-global `random` stream"""
     from rlks import K8sMultiCloudEnv
 
     _dev()
-    env = K8sMultiCloudEnv()
+    env = K8sMultiCloudEnv(noise_stream=stream)
     assert env.max_steps == 99
     obs, info = env.reset(seed=seed)
     assert info == {} and obs.dtype == np.float32 and obs.shape == (6,)
@@ -244,3 +246,34 @@ def test_episode_stats_match_returns():
     s = venv.episode_stats(clear=True).cpu().numpy()
     assert s[1] == 128
     assert abs(s[0] / 128 - 4912.769165045401) < 1e-9
+
+
+def test_global_stream_replays_interleaved_reference_envs():
+    """noise_stream="global": two drop-in envs and the caller's own random.random() draws share the
+    process-global stream in call order, as the reference's random.uniform does
+    (k8s_multi_cloud_env.py:87, :109-111): tests/golden/global_stream.npz (tools/make_goldens.py,
+    two reference envs interleaved after one random.seed, a mid-episode reset(seed) of one of them)
+    replayed bit for bit"""
+    import random
+
+    from rlks import K8sMultiCloudEnv
+
+    _dev()
+    from conftest import GOLDEN
+
+    g = np.load(GOLDEN / "global_stream.npz")
+    random.seed(int(g["seed"]))
+    np.random.seed(int(g["seed"]))
+    envs = [K8sMultiCloudEnv(env_config={"noise_stream": "global"}), K8sMultiCloudEnv(noise_stream="global")]
+    for i in range(len(g["kind"])):
+        kind, e, arg = int(g["kind"][i]), int(g["env"][i]), int(g["arg"][i])
+        if kind == 3:
+            assert random.random() == g["draw"][i], i
+            continue
+        if kind == 2:
+            obs, r, done, _, _ = envs[e].step(arg)
+            assert np.float64(r).view(np.uint64) == g["reward"][i].view(np.uint64), i
+            assert done == bool(g["done"][i]), i
+        else:
+            obs, _ = envs[e].reset(seed=arg if kind == 1 else None)
+        np.testing.assert_array_equal(obs.view(np.uint32), g["obs"][i].view(np.uint32), err_msg=f"event {i}")

@@ -21,6 +21,8 @@ Outputs (all small):
   traces_meta.json    keys of traces.npz, returns per policy, IndexError behaviour
   action_validity.json  which action values the reference accepts / rejects
   gae.npz             GAE goldens from scipy.signal.lfilter (RLlib discount_cumsum form)
+  global_stream.npz   two envs + caller draws interleaved on the process-global `random` stream
+                      (--only-global-stream regenerates just this file)
 """
 from __future__ import annotations
 
@@ -114,10 +116,64 @@ POLICIES = ["all0", "all1", "rr", "greedy", "rand"]
 SEEDS = [0, 7, 42]
 
 
+# event codes of global_stream.npz
+EV_RESET, EV_RESET_SEED, EV_STEP, EV_DRAW = 0, 1, 2, 3
+
+
+def global_stream_golden(Env) -> None:
+    """Two reference envs in one process sharing the process-global `random` stream
+    (k8s_multi_cloud_env.py:87 draws the cpu noise from it, :109-111 reseeds it): after one
+    random.seed(s), env 0 and env 1 are reset and stepped interleaved, the caller draws
+    random.random() in between, one env is reset with a seed mid-episode (reseeding the stream the
+    other is drawing from), and both run past an episode end.  Recorded per event: kind, env,
+    argument, obs f32, reward f64, done, the caller's draw."""
+    ev = []  # (kind, env, arg)
+    rng = np.random.default_rng(2024)
+    ev += [(EV_RESET, 0, 0), (EV_RESET, 1, 0)]
+    steps = [0, 0]
+    for t in range(230):
+        e = int(rng.integers(0, 2))
+        if steps[e] == 99:  # terminated: the next call would raise IndexError (:91)
+            ev.append((EV_RESET, e, 0))
+            steps[e] = 0
+            continue
+        ev.append((EV_STEP, e, int(rng.integers(0, 2))))
+        steps[e] += 1
+        if t % 7 == 3:
+            ev.append((EV_DRAW, -1, 0))
+        if t == 120:
+            ev.append((EV_RESET_SEED, e, 99))
+            steps[e] = 0
+    out = {k: [] for k in ("kind", "env", "arg", "obs", "reward", "done", "draw")}
+    random.seed(31337)
+    np.random.seed(31337)
+    envs = [Env(), Env()]
+    for kind, e, arg in ev:
+        obs, rew, done, draw = np.zeros(6, np.float32), 0.0, False, 0.0
+        if kind == EV_RESET:
+            obs, _ = envs[e].reset()
+        elif kind == EV_RESET_SEED:
+            obs, _ = envs[e].reset(seed=arg)
+        elif kind == EV_STEP:
+            obs, rew, done, _, _ = envs[e].step(arg)
+        else:
+            draw = random.random()
+        for k, v in (("kind", kind), ("env", e), ("arg", arg), ("obs", obs), ("reward", rew), ("done", done),
+                     ("draw", draw)):
+            out[k].append(v)
+    np.savez(OUT / "global_stream.npz", seed=np.array(31337), kind=np.array(out["kind"], np.int32),
+             env=np.array(out["env"], np.int32), arg=np.array(out["arg"], np.int32),
+             obs=np.array(out["obs"], np.float32), reward=np.array(out["reward"], np.float64),
+             done=np.array(out["done"], np.uint8), draw=np.array(out["draw"], np.float64))
+
+
 def main() -> None:
     OUT.mkdir(parents=True, exist_ok=True)
     mod = _load_reference_env()
     Env = mod.K8sMultiCloudEnv
+    if "--only-global-stream" in sys.argv:
+        global_stream_golden(Env)
+        return
 
     # ---- table bits (pandas default parser; SURVEY §7.3: not correctly rounded)
     env = Env()
@@ -261,6 +317,7 @@ def main() -> None:
         gae[f"c{ci}_vt"] = adv + v[:T].astype(np.float64)
         gae[f"c{ci}_params"] = np.array([gamma, lam], np.float64)
     np.savez(OUT / "gae.npz", **gae)
+    global_stream_golden(Env)
     print("wrote", sorted(p.name for p in OUT.iterdir()))
     print("returns", returns)
 
