@@ -38,6 +38,12 @@ extern "C" {
 const char* rlks_last_error(void);
 const char* rlks_version(void);
 
+/* Debug build only (make -C csrc debug -> librlks_debug.so): device-side bounds checks that count
+ * instead of faulting.  out[3] = {violations since the last call, first site (rlks_internal.h
+ * DcheckSite), its value}; synchronises the device and clears the counters.  RLKS_ERR_UNSUPPORTED
+ * in the product library. */
+int rlks_debug_checks(unsigned long long* out);
+
 /* ============================================================== environment (K1 + K2) ==== */
 typedef struct rlks_env rlks_env;
 

@@ -20,6 +20,8 @@
 
 namespace rlks {
 
+RLKS_DCHECK_READER(env)
+
 // ----------------------------------------------------------------------------- kernels
 // Skip n_draws[lane] calls of random() (2 words each) on every masked lane: positions lane e of a
 // batched evaluation at the point of the process-global stream that episode e of the reference's
@@ -296,7 +298,8 @@ __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __re
   bool over = false;
   unsigned long long n_checks = 0, n_placed = 0, n_rej = 0, n_dep = 0, n_wr = 0, n_rd = 0;
   if (lane < v.N) {
-    const int t = v.step[lane], ep = v.episode[lane], a = actions[lane];
+    const int t = v.step[lane], ep = v.episode[lane];
+    int a = actions[lane];
     if (t >= v.T) {  // iloc[t] out of bounds before any change
       over = true;
       if (rew64) rew64[lane] = 0.0;
@@ -341,6 +344,7 @@ __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __re
           pos = idx + 1;
           // pod idx (numbered in node order at the start of the step): its group, chunk, node
           for (;;) {
+            if (!dcheck(8 * grp < (N >> 3), DC_NODE_GROUP, grp)) grp = ((N >> 3) - 1) >> 3;
             if (gsum < 0) gsum = load_tot8(tot + 8 * grp, gt);
             if (idx < gcum + gsum) break;
             gcum += gsum;
@@ -353,6 +357,7 @@ __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __re
             if (j == q && idx >= cj + gt[q]) { cj += gt[q]; j = q + 1; }
 #pragma unroll
           for (int q = 0; q < 8; ++q) tj = (q == j) ? gt[q] : tj;
+          if (!dcheck(8 * grp + j < (N >> 3), DC_NODE_CHUNK, 8 * grp + j)) j = (N >> 3) - 1 - 8 * grp;
           if (8 * grp + j != ch) {
             if (ch >= 0) flush_chunk(col, tot, ch, ctot, f, dep, n_wr);
             ch = 8 * grp + j;
@@ -369,6 +374,7 @@ __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __re
             const int pq = node_pods(v, cc, f[q].x) + dep[q];
             if (qn == q && idx >= cq + pq) { cq += pq; qn = q + 1; }
           }
+          if (!dcheck(qn < 8, DC_NODE_POD, idx)) qn = 7;
 #pragma unroll
           for (int q = 0; q < 8; ++q)
             if (q == qn) {
@@ -388,6 +394,7 @@ __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __re
       // by their totals, the others are loaded and filled node by node in order
       int rem = arrivals(v, gid, ep, t);
       {
+        if (!dcheck(a >= 0 && a < C, DC_NODE_ACTION, a)) a = 0;
         const int32_t cc = v.cap[a], cm = v.cap[C + a];
         const int full = 8 * min(cc / pc, cm / pm);
         int2* col = nodes + (size_t)a * N;
@@ -512,7 +519,12 @@ __global__ void k_sample_categorical(const float* __restrict__ logits, int n, in
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float lp;
-  const u32x4 ctr{ids[3 * i], ids[3 * i + 1], ids[3 * i + 2], (uint32_t)RLKS_PURPOSE_ACTION << 16};
+  u32x4 ctr{0u, 0u, 0u, (uint32_t)RLKS_PURPOSE_ACTION << 16};
+  if (explore) {  // ids may be NULL for argmax
+    ctr.x = ids[3 * i];
+    ctr.y = ids[3 * i + 1];
+    ctr.z = ids[3 * i + 2];
+  }
   actions[i] = categorical(logits + (size_t)i * A, A, explore != 0, ctr, k0, k1, lp);
   if (logp) logp[i] = lp;
 }
@@ -538,19 +550,15 @@ __global__ void k_sample_step(EnvView v, const double* __restrict__ cost, const 
 }
 
 // deterministic single-workgroup reduction of the per-lane episode accumulators
-__global__ void k_episode_stats(EnvView v, double* __restrict__ out, int clear) {
+// fixed-order sum of n (sum, count) pairs from the block's threads: each thread adds items
+// tid, tid + 256, ... of its range, then a pairwise LDS tree (the same bits on every run)
+__device__ __forceinline__ void block_sum2(double sum, double cnt, double* __restrict__ out) {
   __shared__ double s_sum[ENV_BLOCK];
   __shared__ double s_cnt[ENV_BLOCK];
-  double sum = 0.0, cnt = 0.0;
-  for (int i = threadIdx.x; i < v.N; i += blockDim.x) {
-    sum += v.ret_sum[i];
-    cnt += (double)v.ep_cnt[i];
-    if (clear) { v.ret_sum[i] = 0.0; v.ep_cnt[i] = 0; }
-  }
   s_sum[threadIdx.x] = sum;
   s_cnt[threadIdx.x] = cnt;
   __syncthreads();
-  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+  for (int o = ENV_BLOCK / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) {
       s_sum[threadIdx.x] += s_sum[threadIdx.x + o];
       s_cnt[threadIdx.x] += s_cnt[threadIdx.x + o];
@@ -558,6 +566,28 @@ __global__ void k_episode_stats(EnvView v, double* __restrict__ out, int clear) 
     __syncthreads();
   }
   if (threadIdx.x == 0) { out[0] = s_sum[0]; out[1] = s_cnt[0]; }
+}
+// completed-episode sums over the lanes in two fixed-order stages: block b reduces lanes
+// [b EPS_LANES, (b + 1) EPS_LANES) into part[b], then one block sums the parts
+constexpr int EPS_LANES = 8 * ENV_BLOCK;
+__global__ __launch_bounds__(ENV_BLOCK) void k_episode_stats_part(EnvView v, double* __restrict__ part, int clear) {
+  double sum = 0.0, cnt = 0.0;
+  const int i1 = min(v.N, (int)(blockIdx.x + 1) * EPS_LANES);
+  for (int i = blockIdx.x * EPS_LANES + threadIdx.x; i < i1; i += ENV_BLOCK) {
+    sum += v.ret_sum[i];
+    cnt += (double)v.ep_cnt[i];
+    if (clear) { v.ret_sum[i] = 0.0; v.ep_cnt[i] = 0; }
+  }
+  block_sum2(sum, cnt, part + 2 * blockIdx.x);
+}
+__global__ __launch_bounds__(ENV_BLOCK) void k_episode_stats_final(const double* __restrict__ part, int nb,
+                                                                   double* __restrict__ out) {
+  double sum = 0.0, cnt = 0.0;
+  for (int b = threadIdx.x; b < nb; b += ENV_BLOCK) {
+    sum += part[2 * b];
+    cnt += part[2 * b + 1];
+  }
+  block_sum2(sum, cnt, out);
 }
 
 __global__ void k_lane_state(int N, const int32_t* __restrict__ step, const int32_t* __restrict__ ep,
@@ -687,6 +717,7 @@ int rlks_env_create_ext(const rlks_env_cfg* cfg, const double* cost, const doubl
   alloc((void**)&e->d_eplog, RLKS_EPLOG_CAP * sizeof(double));
   alloc((void**)&e->d_eplog_key, RLKS_EPLOG_CAP * sizeof(long long));
   alloc((void**)&e->d_eplog_n, sizeof(unsigned));
+  alloc((void**)&e->d_epstat, 2 * cdiv(N, EPS_LANES) * sizeof(double));
   if (cfg->noise_mode == RLKS_NOISE_MT19937) alloc((void**)&e->d_mt, (size_t)(MT_N + 1) * N * sizeof(uint32_t));
   if (err == hipSuccess) err = hipMemcpy(e->d_cost, cost, TC * sizeof(double), hipMemcpyHostToDevice);
   if (err == hipSuccess) err = hipMemcpy(e->d_lat, lat, TC * sizeof(double), hipMemcpyHostToDevice);
@@ -746,6 +777,7 @@ int rlks_env_destroy(rlks_env* e) {
   (void)hipFree(e->d_ep_ret); (void)hipFree(e->d_ret_sum); (void)hipFree(e->d_ep_cnt); (void)hipFree(e->d_status);
   (void)hipFree(e->d_counters);
   (void)hipFree(e->d_eplog); (void)hipFree(e->d_eplog_key); (void)hipFree(e->d_eplog_n);
+  (void)hipFree(e->d_epstat);
   if (e->d_mt) (void)hipFree(e->d_mt);
   if (e->d_cap) (void)hipFree(e->d_cap);
   if (e->d_lam) (void)hipFree(e->d_lam);
@@ -844,7 +876,11 @@ int rlks_env_sample_step(rlks_env* e, const float* logits, int explore, int32_t*
 
 int rlks_env_episode_stats(rlks_env* e, double* out, int clear, void* stream) {
   RLKS_REQUIRE(e && out, RLKS_ERR_ARG, "rlks_env_episode_stats: null argument");
-  hipLaunchKernelGGL(k_episode_stats, dim3(1), dim3(ENV_BLOCK), 0, (hipStream_t)stream, view(e), out, clear);
+  const int nb = (int)cdiv(e->cfg.n_envs, EPS_LANES);
+  hipLaunchKernelGGL(k_episode_stats_part, dim3(nb), dim3(ENV_BLOCK), 0, (hipStream_t)stream, view(e), e->d_epstat,
+                     clear);
+  RLKS_LAUNCHED();
+  hipLaunchKernelGGL(k_episode_stats_final, dim3(1), dim3(ENV_BLOCK), 0, (hipStream_t)stream, e->d_epstat, nb, out);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }

@@ -44,6 +44,7 @@ struct rlks_env {
   double* d_eplog;
   long long* d_eplog_key;
   unsigned* d_eplog_n;
+  double* d_epstat;  // [ceil(n_envs / EPS_LANES)][2] partial (sum, count) of rlks_env_episode_stats
 };
 
 namespace rlks {

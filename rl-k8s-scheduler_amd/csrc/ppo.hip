@@ -12,6 +12,8 @@
 
 namespace rlks {
 
+RLKS_DCHECK_READER(ppo)
+
 // ----------------------------------------------------------------------------- reduce
 // out[i] = sum_p part[p * pstride + i] (i < len, p < P) in a fixed order with f64 accumulation.
 // A block = 256 threads = OPB output vectors x G partial-groups; a vector is 4 consecutive outputs
@@ -243,8 +245,11 @@ struct GatherArgs {
 // source index t * N + n of minibatch row i: rows [k rows_g, (k+1) rows_g) come from lane group
 // k, whose permutation p -> (t = p / Ng, lane k Ng + p mod Ng)
 __device__ __forceinline__ int64_t gather_src(const Perm* perm, int64_t row0g, int rows_g, int Ng, int N, uint32_t i) {
-  const uint32_t k = i / (uint32_t)rows_g, ii = i - k * (uint32_t)rows_g;
-  const uint64_t p = perm_apply(perm[k], (uint64_t)(row0g + ii));
+  uint32_t k = i / (uint32_t)rows_g;
+  const uint32_t ii = i - k * (uint32_t)rows_g;
+  if (!dcheck(k < (uint32_t)MAX_GROUPS, DC_GATHER_GROUP, k)) k = 0;
+  uint64_t p = perm_apply(perm[k], (uint64_t)(row0g + ii));
+  if (!dcheck(p < perm[k].S, DC_GATHER_SRC, (long long)p)) p = 0;
   uint64_t t, nl;
   if (p >> 32) {
     t = p / (uint64_t)Ng;

@@ -32,6 +32,44 @@ int fail(int code, const std::string& msg);
 
 inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
+// ----------------------------------------------------------------------------- debug checks
+// `make -C csrc debug` (librlks_debug.so, -DRLKS_DEBUG): device-side bounds checks on the indexing
+// a corrupted state or a wrong shape would send out of bounds (node-state chunks and nodes, the
+// minibatch gather's source rows, the SGD step's tiles).  A failed check does not fault the GPU: it
+// counts the violation, records the first site and value in this translation unit's g_dcheck, and
+// the caller clamps the index so that the access stays in bounds.  rlks_debug_checks() reads and
+// clears the counters of every translation unit; in the product build dcheck() is `true` and
+// compiles away.
+enum DcheckSite {
+  DC_NODE_GROUP = 1,   // 8-chunk group of a departure scan within the cluster's chunks
+  DC_NODE_CHUNK = 2,   // chunk of a departing pod
+  DC_NODE_POD = 3,     // node of a departing pod within its chunk
+  DC_NODE_ACTION = 4,  // chosen cluster (trusted actions)
+  DC_GATHER_SRC = 5,   // minibatch gather source sample < T N
+  DC_GATHER_GROUP = 6, // lane group < groups
+  DC_SGD_TILE = 7,     // F1 / F2 tile < M / 16
+};
+#ifdef RLKS_DEBUG
+static __device__ unsigned long long g_dcheck[3];  // violations, first site, first value
+__device__ __forceinline__ bool dcheck(bool ok, int site, long long val) {
+  if (!ok && atomicAdd(&g_dcheck[0], 1ull) == 0ull) {
+    g_dcheck[1] = (unsigned long long)site;
+    g_dcheck[2] = (unsigned long long)val;
+  }
+  return ok;
+}
+// host reader of this translation unit's counters (cleared after reading)
+#define RLKS_DCHECK_READER(tu)                                                                   \
+  int dcheck_read_##tu(unsigned long long* h) {                                                  \
+    const unsigned long long z[3] = {0ull, 0ull, 0ull};                                          \
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dcheck), sizeof(g_dcheck)) != hipSuccess) return 1;  \
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_dcheck), z, sizeof(z)) == hipSuccess ? 0 : 1;          \
+  }
+#else
+__device__ __forceinline__ bool dcheck(bool, int, long long) { return true; }
+#define RLKS_DCHECK_READER(tu)
+#endif
+
 // ----------------------------------------------------------------------------- Philox4x32-10
 // Salmon et al., "Parallel random numbers: as easy as 1, 2, 3" (SC'11). Same constants and
 // round structure as oracle/rlks_oracle.c:ro_philox4x32_10.

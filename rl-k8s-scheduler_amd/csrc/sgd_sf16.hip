@@ -35,6 +35,8 @@
 
 namespace rlks {
 
+RLKS_DCHECK_READER(sgd)
+
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
 using v4u = __attribute__((ext_vector_type(4))) unsigned;  // 16-byte staging register (a vector, not HIP's uint4 struct, so it stays in VGPRs)
@@ -508,7 +510,9 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   float* sW3 = sB2 + HID;
 
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, c = l & 15, gq = l >> 4;
-  const int tile = blockIdx.x * W + w, row0 = tile * 16;
+  int tile = blockIdx.x * W + w;
+  if (!dcheck(tile < g.M / 16, DC_SGD_TILE, tile)) tile = g.M / 16 - 1;
+  const int row0 = tile * 16;
   FA_STAMP(0);
   FA_HWID();
 
@@ -700,7 +704,9 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {
   float* sEp = lds;                                   // epilogue slots (the chunk buffers)
 
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, c = l & 15, gq = l >> 4;
-  const int tile = blockIdx.x * W + w, row0 = tile * 16, blk = blockIdx.x;
+  int tile = blockIdx.x * W + w;
+  if (!dcheck(tile < g.M / 16, DC_SGD_TILE, tile)) tile = g.M / 16 - 1;
+  const int row0 = tile * 16, blk = blockIdx.x;
   const int D = g.D, stride = g.x_stride;
 
   hc_dma<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
@@ -825,7 +831,8 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
   _Float16* sA = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][32 m][HID n]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int D = g.D, stride = g.x_stride;
-  const int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
+  int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
+  if (!dcheck(t1 <= g.M / 32, DC_SGD_TILE, t1)) t0 = t1 = 0;
 
   static_assert(SF_DZ_SLOTS == 64, "one max slot per lane");
   // sg / unscale: from the step's max |dZ2|, read after the first tile's loads are in flight

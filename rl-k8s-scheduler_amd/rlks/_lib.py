@@ -92,6 +92,7 @@ SIGNATURES = {
     "rlks_env_seed": [_P, _P, _P, _P, _I, _P],
     "rlks_env_mt_discard": [_P, _P, _P, _P],
     "rlks_env_mt_words": [_P, C.c_int, _P, C.c_int, _P],
+    "rlks_debug_checks": [_P],
     "rlks_sample_categorical": [_P, C.c_int, C.c_int, _P, C.c_ulonglong, C.c_int, _P, _P, _P],
     "rlks_env_reset": [_P, _P, _P, _P],
     "rlks_env_step": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],

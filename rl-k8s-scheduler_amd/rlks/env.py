@@ -283,7 +283,9 @@ class K8sMultiCloudEnv(_EnvBase):
         self.max_steps = self._table.n_rows - 1  # (:66)
         self.current_step = 0
         torch = _torch()
-        seed0 = random.getrandbits(64)
+        # the global stream must not be advanced here (the reference constructor draws nothing); its
+        # state is loaded into the lane before every reset / step
+        seed0 = random.getrandbits(64) if noise_stream == "instance" else 0
         self._dev = DeviceEnv(make_cfg(1, self._table, noise=noise, seed=seed0, autoreset=False), self._table, device)
         d = self._dev.device
         self._act = torch.zeros(1, dtype=torch.int32, device=d)

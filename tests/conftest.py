@@ -45,3 +45,21 @@ def traces_meta():
 @pytest.fixture(scope="session")
 def mt_draws():
     return np.load(GOLDEN / "mt_draws.npz")
+
+
+@pytest.fixture(autouse=True)
+def _device_bounds_checks(request):
+    """with RLKS_LIB pointing at librlks_debug.so (make -C csrc debug), every GPU test must end
+    with no device-side bounds-check violation (rlks_debug_checks; rlks_internal.h DcheckSite)"""
+    yield
+    import os
+
+    if "debug" not in os.environ.get("RLKS_LIB", "") or request.node.get_closest_marker("gpu") is None:
+        return
+    import ctypes as C
+
+    from rlks import _lib
+
+    out = (C.c_ulonglong * 3)()
+    _lib.call("rlks_debug_checks", out)
+    assert out[0] == 0, f"{out[0]} device bounds-check violations; first at site {out[1]} (value {out[2]})"
