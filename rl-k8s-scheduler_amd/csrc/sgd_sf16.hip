@@ -101,10 +101,15 @@ __device__ __forceinline__ float pow2(int e) { return ldexpf(1.f, e); }
 
 // 1 - 2 / (exp(2x) + 1): 5 VALU ops (2 transcendental); absolute error ~1e-7, which is what the
 // split products see (|h| < 1 carried at a fixed 2^14 scale)
+constexpr float SF_2LOG2E = 2.885390081777927f;  // 2 log2(e): exp(2x) = exp2(x SF_2LOG2E)
 __device__ __forceinline__ float tanh_abs(float x) {
-  const float e = __builtin_amdgcn_exp2f(x * 2.885390081777927f);
+  const float e = __builtin_amdgcn_exp2f(x * SF_2LOG2E);
   return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }
+// r = 1 / (exp(2x) + 1) given kx = x SF_2LOG2E (callers fold SF_2LOG2E into the scale they already
+// multiply by): tanh x = 1 - 2 r, 1 - tanh^2 x = 4 r (1 - r).  4 VALU ops instead of 6 with the
+// separate scale multiply.
+__device__ __forceinline__ float tanh_r(float kx) { return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(kx) + 1.f); }
 
 // interleave the scheduling region: NM x (1 MFMA, NV VALU) (cdna_hip_programming.md T19); an
 // MFMA leaves 24 of its 32 issue cycles for independent vector work of the same wave
@@ -509,7 +514,8 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   float* sB2 = lds + f1a_region_bytes<A_, KD, W>() / 4;
   float* sW3 = sB2 + HID;
 
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, c = l & 15, gq = l >> 4;
+  // w wave-uniform (readfirstlane): tile bases stay in SGPRs, stores use a 32-bit lane offset
+  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
   int tile = blockIdx.x * W + w;
   if (!dcheck(tile < g.M / 16, DC_SGD_TILE, tile)) tile = g.M / 16 - 1;
   const int row0 = tile * 16;
@@ -517,12 +523,12 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   FA_HWID();
 
   hc_dma<W>(N.w2ph, N.w2pl, 0, 0, sCh, w, l);
-  for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i];
+  for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i] * SF_2LOG2E;  // H2 = tanh(Z2 + b2): exp2 argument
   for (int i = tid; i < A_ * HID; i += NTHR) sW3[i] = N.w3[i];
   w1_stage<KD, NTHR>(N, sW1, tid);
   h8 xh, xl;
   const int ex = x_frag(g, row0, c, gq, xh, xl);
-  const float inv_z1 = N.sc[1] * pow2(-ex);
+  const float k_z1 = N.sc[1] * pow2(-ex) * SF_2LOG2E;  // Z1 accumulator -> 2 log2(e) Z1
   vm_drain();
   __syncthreads();
   FA_STAMP(1);
@@ -546,10 +552,10 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
           w1_frag<KD>(sW1, 2 * t + b, c, gq, wh, wl);
           z[b] = mm16x3(wh, wl, xh, xl, f4zero());
         }
-        float hv[8];
+        float hv[8];  // 2^14 tanh = 2^14 - 2^15 r (the split's fixed H1 scale folded in)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hv[j] = tanh_abs(z[j >> 2][j & 3] * inv_z1);
-        split8(hv, 0, SF_H1_SCALE, bh, bl);
+        for (int j = 0; j < 8; ++j) hv[j] = fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
+        split8(hv, 0, 1.f, bh, bl);
       }
       // fragments one n-tile ahead of their MFMAs, fenced so that only two sets are live
       const _Float16* buf = sCh + ph * 2 * H16;
@@ -573,7 +579,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
 
   // ---- H2^T = tanh(Z2^T + b2) (lane: rows n = 16 nt + 4g + i of column m = c); head
   // out[a] = b3 + sum_n W3[a][n] H2[n] (partial over the lane's 64 n, then over the four rows)
-  const float inv_z2 = N.sc[3] / SF_H1_SCALE;
+  const float k_z2 = N.sc[3] / SF_H1_SCALE * SF_2LOG2E;
   float out[A_];
 #pragma unroll
   for (int a = 0; a < A_; ++a) out[a] = 0.f;
@@ -585,7 +591,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
     float hv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      hv[i] = tanh_abs(fmaf(acc[nt][i], inv_z2, bv[i]));
+      hv[i] = fmaf(-2.f, tanh_r(fmaf(acc[nt][i], k_z2, bv[i])), 1.f);
       acc[nt][i] = hv[i];
     }
 #pragma unroll
@@ -596,6 +602,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
       out[a] = fmaf(hv[2], t.z, out[a]);
       out[a] = fmaf(hv[3], t.w, out[a]);
     }
+    if constexpr (A_ > 4) asm volatile("" ::: "memory");  // keep the W3 reads per n-tile (8 actions: spills)
   }
 #pragma unroll
   for (int a = 0; a < A_; ++a) out[a] = sum_rows4(out[a]) + N.b3[a];
@@ -658,6 +665,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
         dmx = fmaxf(dmx, fabsf(dz[i]));
       }
       *reinterpret_cast<v4f*>(dst + (nt >> 1) * 512 + 4 * (nt & 1)) = dz;
+      if constexpr (A_ > 4) asm volatile("" ::: "memory");
     }
   }
   dmx = wave_max(dmx);
@@ -690,8 +698,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   else f1a_body<1, 1, KD, W>(g);
 }
 
-template <int NET, int KD, int W>
-__device__ __forceinline__ void f1b_body(const SfArgs& g) {
+template <int NET, int KD, int ND, int W>
+__device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1 (rows d of dW1a^T)
   constexpr int NTHR = 64 * W;
   constexpr int DT = KD / 16;                      // 16-row d-tiles of dW1a^T
   constexpr int SLOT = W * 16 * 16 * DT;           // floats per k-tile: [W][16 k][16 DT d]
@@ -703,7 +711,8 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {
   _Float16* sW1 = sCh + 4 * H16;                      // [2 hi/lo][HID][KD]
   float* sEp = lds;                                   // epilogue slots (the chunk buffers)
 
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, c = l & 15, gq = l >> 4;
+  // w wave-uniform (readfirstlane): tile bases stay in SGPRs, stores use a 32-bit lane offset
+  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
   int tile = blockIdx.x * W + w;
   if (!dcheck(tile < g.M / 16, DC_SGD_TILE, tile)) tile = g.M / 16 - 1;
   const int row0 = tile * 16, blk = blockIdx.x;
@@ -758,7 +767,7 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {
   // k-tile: dZ1 enters the split at 2^(e_dz + e_w2 - 23) (|dH1 2^(e_dz + e_w2)| <= 256 2^15 2^15)
   h8 xh, xl;
   const int ex = x_frag(g, row0, c, gq, xh, xl);
-  const float sx = pow2(ex), inv_z1 = N.sc[1] / sx;
+  const float sx = pow2(ex), k_z1 = N.sc[1] / sx * SF_2LOG2E;
   h4 xth[DT], xtl[DT];  // Xa^T (16x16x16 A operand): rows d = 16 dt + c, columns m = 4g + j
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
@@ -769,7 +778,8 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {
       xth[dt][j] = a;
       xtl[dt][j] = b;
     }
-  const float sz1 = pow2(-23), u1 = pow2(23 - ex - edz - (int)N.sc[5]);
+  // 1 - H1^2 = 4 r (1 - r): the 4 joins the split's power of two
+  const float sz1 = pow2(-21), u1 = pow2(23 - ex - edz - (int)N.sc[5]);
 #pragma unroll
   for (int kt = 0; kt < 16; ++kt) {
     h8 wh, wl;
@@ -778,9 +788,9 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {
     h4 zh, zl;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float h1 = tanh_abs(z[i] * inv_z1);
+      const float r = tanh_r(z[i] * k_z1);
       _Float16 a, b;
-      split1(acc[kt][i] * (1.f - h1 * h1) * sz1, a, b);
+      split1(acc[kt][i] * fmaf(-r, r, r) * sz1, a, b);
       zh[i] = a;
       zl[i] = b;
     }
@@ -790,16 +800,16 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {
       const float4 v = {dw[0] * u1, dw[1] * u1, dw[2] * u1, dw[3] * u1};
       *reinterpret_cast<float4*>(sEp + (kt % KPR) * SLOT + (w * 16 + c) * 16 * DT + 16 * dt + 4 * gq) = v;
     }
-    if (kt % KPR == KPR - 1) {
+    if (kt % KPR == KPR - 1) {  // (k-tile, k, d) elements; ND a compile-time constant (no runtime division)
       __syncthreads();
-      const int nd = D + 1, kt0 = kt + 1 - KPR;
-      for (int e = tid; e < KPR * 16 * nd; e += NTHR) {
-        const int jj = e / (16 * nd), e2 = e - jj * 16 * nd, kk = e2 / nd, d = e2 - kk * nd;
+      const int kt0 = kt + 1 - KPR;
+      for (int e = tid; e < KPR * 16 * ND; e += NTHR) {
+        const int jj = e / (16 * ND), e2 = e - jj * 16 * ND, kk = e2 / ND, d = e2 - kk * ND;
         const int k = 16 * (kt0 + jj) + kk;
         float sum = 0.f;
 #pragma unroll
         for (int ww = 0; ww < W; ++ww) sum += sEp[jj * SLOT + (ww * 16 + kk) * 16 * DT + d];
-        if (d < D) N.part_w1[((size_t)blk * HID + k) * D + d] = sum;
+        if (d < ND - 1) N.part_w1[((size_t)blk * HID + k) * (ND - 1) + d] = sum;
         else N.part_b1[(size_t)blk * HID + k] = sum;
       }
       if (kt < 15) __syncthreads();
@@ -807,10 +817,10 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {
   }
 }
 
-template <int KD, int W>
+template <int KD, int ND, int W>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_bwd(SfArgs g) {
-  if (blockIdx.y + g.net0 == 0) f1b_body<0, KD, W>(g);
-  else f1b_body<1, KD, W>(g);
+  if (blockIdx.y + g.net0 == 0) f1b_body<0, KD, ND, W>(g);
+  else f1b_body<1, KD, ND, W>(g);
 }
 
 // ----------------------------------------------------------------------------- F2
@@ -944,11 +954,11 @@ __global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
       split8(xv, ks * 8, sx, a, b);
       z = mma3(a, b, wh[ks], wl[ks], z);
     }
-    const float inv_z1 = inv_w1 / sx;
+    const float k_z1 = inv_w1 / sx * SF_2LOG2E;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = tanh_abs(z[q] * inv_z1);
-    split16(z, 0, SF_H1_SCALE, bh[0], bl[0]);
-    split16(z, 8, SF_H1_SCALE, bh[1], bl[1]);
+    for (int q = 0; q < 16; ++q) z[q] = fmaf(-2.f * SF_H1_SCALE, tanh_r(z[q] * k_z1), SF_H1_SCALE);
+    split16(z, 0, 1.f, bh[0], bl[0]);
+    split16(z, 8, 1.f, bh[1], bl[1]);
   };
 
   // Software pipeline: step t runs tile t's 48 MFMAs and, in their shadow, splits tile t + 1's
@@ -1051,7 +1061,7 @@ static int launch_f1_net(SfArgs a, int net0, int nets, hipStream_t s, int halves
     RLKS_LAUNCHED();
   }
   if (halves & 2) {
-    hipLaunchKernelGGL((k_sf_bwd<KD, W>), grid, dim3(64 * W), f1b_lds_bytes<KD>(), s, a);
+    hipLaunchKernelGGL((k_sf_bwd<KD, 3 * A_ + 1, W>), grid, dim3(64 * W), f1b_lds_bytes<KD>(), s, a);
     RLKS_LAUNCHED();
   }
   return RLKS_OK;
