@@ -52,9 +52,9 @@ def flops_per_row(name, D=6, H=256, A=2):
         "k_fwd_head_vf": fwd(1) + head(1),
         "k_dw2": 2 * 2 * H * H,                     # dW2 = dZ2^T H1, both nets
         "k_dh1": 2 * 2 * H * H + 2 * 2 * D * H,     # dH1 = dZ2 W2 and dW1 = dZ1^T X, both nets
-        # split-fp16 F1 (sgd_sf16.hip): forward + head backward + dH1 = dZ2 W2 + dW1 = dZ1^T X, both nets
-        "k_sf_fwdbwd": sum(fwd(An) + head(An) + 2 * H * H + 2 * D * H for An in (A, 1)),
-        # the same F1 as two kernels: forward + head backward (F1a), dH1 = dZ2 W2 + dW1 = dZ1^T X (F1b)
+        # split-fp16 F1 (sgd_sf16.hip) as two kernels: forward + head backward (F1a), dH1 = dZ2 W2 +
+        # dW1 = dZ1^T X (F1b); f1_total is the pair
+        "f1_total": sum(fwd(An) + head(An) + 2 * H * H + 2 * D * H for An in (A, 1)),
         "k_sf_fwd": sum(fwd(An) + head(An) for An in (A, 1)),
         "k_sf_bwd": 2 * (2 * H * H + 2 * D * H),
         "k_sf_dw2": 2 * 2 * H * H,                  # dW2 = dZ2^T H1, both nets
@@ -100,8 +100,19 @@ def env_setup(name):
                          init_occupancy=0.5)
 
 
-ROOFLINE_KERNELS = ("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1", "k_sf_fwdbwd", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2",
-                    "wide_grad")
+ROOFLINE_KERNELS = ("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "wide_grad")
+
+
+def algo_bytes_per_launch(name, rows, D=6, H=256, A=2):
+    """compulsory HBM bytes of one launch of a split-fp16 SGD kernel over `rows` minibatch rows
+    (DESIGN.md "Algorithmic bytes"): each net's pass reads the row's record (fp32, mb_stride
+    floats; F2 only its obs columns), F1a writes both nets' dZ2 (fp32, 2 x H x 4 B a row), F1b
+    and F2 read it back.  Weights (< 0.5 MB) and the per-block weight-gradient partials are not
+    counted: they are the overhead traffic_over_algorithmic exposes."""
+    rec = (D + A + 4 + 3) // 4 * 4 * 4
+    dz = 2 * H * 4
+    per_row = {"k_sf_fwd": 2 * rec + dz, "k_sf_bwd": 2 * rec + dz, "k_sf_dw2": 2 * D * 4 + dz}.get(name)
+    return None if per_row is None else per_row * rows
 ENV_BYTES_PER_STEP = 4 + 8 + 24 + 4 + 1  # action, step r/w, obs, reward, done (SURVEY §8d)
 # what the 2-cloud step kernel must move per env-step: action 4, step r/w 8, episode 4 (Philox
 # counter), obs 24, reward 8 (the reference's float64), terminated 1
@@ -175,7 +186,7 @@ def kernel_timing(algo, torch, config="c2", reps=20):
             rec.update({"tflops": tf, peak_name: tf / peak, "frac_fp32_mfma_peak": tf / FP32_MFMA_PEAK_TFLOPS})
         out[name] = rec
     if "f1_total" in out:
-        tf = flops_per_row("k_sf_fwdbwd", D, H, A) * algo.mb / (out["f1_total"]["ms"] * 1e-3) / 1e12
+        tf = flops_per_row("f1_total", D, H, A) * algo.mb / (out["f1_total"]["ms"] * 1e-3) / 1e12
         out["f1_total"].update({"tflops": tf, peak_name: tf / peak})
     ms = timed(lambda: _lib.call("rlks_ppo_grad", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(),
                                  algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None,
@@ -444,9 +455,13 @@ def main():
             if dom == "wide_grad":
                 roofline["note"] = "generic-width path: the whole SGD-step gradient (a sequence of split-fp16 GEMM launches)"
             pmc = pmc_traffic()
+            ab = algo_bytes_per_launch(dom, algo.mb, algo.D, algo.H, algo.A)
+            roofline["algorithmic_bytes_per_launch"] = ab
             if pmc and args.config in ("c2", "c4") and dom in pmc:
                 roofline["traffic"] = pmc[dom]["hbm_bytes_per_launch"]
                 roofline["traffic_source"] = pmc["source"]
+                if ab:
+                    roofline["traffic_over_algorithmic"] = roofline["traffic"] / ab
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             sys.path.insert(0, str(ROOT / "oracle"))

@@ -6,7 +6,8 @@
 namespace rlks {
 
 enum { GEMM_STORE = RLKS_GEMM_STORE, GEMM_TANH_BIAS = RLKS_GEMM_TANH_BIAS, GEMM_BIAS = RLKS_GEMM_BIAS,
-       GEMM_DTANH = RLKS_GEMM_DTANH };
+       GEMM_DTANH = RLKS_GEMM_DTANH,
+       GEMM_TANH_BIAS_PLANES = 4 };  // internal: tanh(acc + bias) written as fp16 hi / lo planes at 2^14
 
 struct GemmArgs {
   const float *A, *B;
@@ -22,9 +23,41 @@ struct GemmArgs {
   // Epilogue GEMM_STORE only.
   int splits;
   float* part;
+  _Float16 *c_hi, *c_lo;  // GEMM_TANH_BIAS_PLANES: output planes [M][ldc]
 };
 
 int launch_gemm_sf16(const GemmArgs& a, hipStream_t s);
+int launch_split_reduce(const float* part, int splits, int rows, int cols, float* out, int ld, int accumulate,
+                        hipStream_t s);
+
+// ---- pre-split GEMM (gemm_ps.hip): operands as fp16 planes hi / lo of x 2^e in HBM
+struct PsOperand {
+  const _Float16 *hi, *lo;  // element (row, k) at row * ld + k, or k * ld + row when kmajor
+  int ld, kmajor;
+  int rows;                 // extent of the non-K dimension (rows past it are clamped, never stored)
+  const unsigned* maxslot;  // e = exponent with max 2^e in [2^14, 2^15) (float bits); null: fexp
+  int fexp;
+};
+enum { PS_STORE = 0, PS_TANH_BIAS = 1, PS_DTANH = 2 };
+struct PsArgs {
+  PsOperand a, b;           // C[m][n] = sum_k A[m][k] B[n][k]
+  int M, N, K;              // K a multiple of 32
+  int epi;                  // PS_STORE: C (or split-K partials); PS_TANH_BIAS: tanh(acc + bias[n]);
+                            // PS_DTANH: acc (1 - G^2), G = (aux_hi + aux_lo) 2^-14
+  float* C;
+  int ldc;
+  const float* bias;
+  const _Float16 *aux_hi, *aux_lo;
+  int ldaux;
+  unsigned* cmax;           // optional atomicMax of |C|
+  int splits;               // split-K layers (PS_STORE): part[z][M][N], fixed-order f64 reduction into C
+  float* part;
+};
+int launch_gemm_ps(const PsArgs& a, hipStream_t s);
+int gemm_ps_splits(int M, int N, int K);
+// fp32 [rows][ld] -> planes [rows][ldp] of x 2^e (e from maxslot, or fexp when null)
+int launch_split_planes(const float* x, int rows, int cols, int ld, const unsigned* maxslot, int fexp, _Float16* hi,
+                        _Float16* lo, int ldp, hipStream_t s);
 // split count for an M x N x K weight-gradient GEMM (enough workgroups to fill 256 CUs)
 int gemm_splits(int M, int N, int K);
 int launch_absmax(const float* x, int rows, int cols, int ld, unsigned* slot, hipStream_t s);

@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + wn * 64 + 32 * j + r;
     const bool nok = n < g.N;
-    const float bias = (EPI == GEMM_TANH_BIAS || EPI == GEMM_BIAS) && nok ? g.bias[n] : 0.f;
+    const float bias = (EPI == GEMM_TANH_BIAS || EPI == GEMM_BIAS || EPI == GEMM_TANH_BIAS_PLANES) && nok ? g.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -259,6 +259,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const int m = m0 + wm * 64 + 32 * i + acc_row(q, l);
         if (!nok || m >= g.M) continue;
         float v = acc[i][j][q] * unscale;
+        if (EPI == GEMM_TANH_BIAS_PLANES) {  // H1 for the pre-split GEMMs: fp16 planes at 2^14
+          const float hs = tanh_abs(v + bias) * 16384.f;
+          const _Float16 a = (_Float16)hs;
+          g.c_hi[(size_t)m * g.ldc + n] = a;
+          g.c_lo[(size_t)m * g.ldc + n] = (_Float16)(hs - (float)a);
+          continue;
+        }
         if (EPI == GEMM_TANH_BIAS) v = tanh_abs(v + bias);
         if (EPI == GEMM_BIAS) v += bias;
         if (EPI == GEMM_DTANH) {
@@ -338,8 +345,8 @@ __global__ __launch_bounds__(256) void k_split_reduce(const float* __restrict__ 
   }
 }
 
-static int launch_split_reduce(const float* part, int splits, int rows, int cols, float* out, int ld, int accumulate,
-                               hipStream_t s) {
+int launch_split_reduce(const float* part, int splits, int rows, int cols, float* out, int ld, int accumulate,
+                        hipStream_t s) {
   const size_t n = (size_t)rows * cols;
   const unsigned blocks = (unsigned)std::min<size_t>(4096, (n + 255) / 256);
   hipLaunchKernelGGL(k_split_reduce, dim3(blocks), dim3(256), 0, s, part, splits, rows, cols, out, ld, accumulate);
@@ -356,6 +363,9 @@ static int launch_t(const GemmArgs& a, hipStream_t s) {
     case GEMM_TANH_BIAS: hipLaunchKernelGGL((k_gemm_sf16<TA, TB, GEMM_TANH_BIAS>), grid, dim3(256), lds, s, a); break;
     case GEMM_BIAS: hipLaunchKernelGGL((k_gemm_sf16<TA, TB, GEMM_BIAS>), grid, dim3(256), lds, s, a); break;
     case GEMM_DTANH: hipLaunchKernelGGL((k_gemm_sf16<TA, TB, GEMM_DTANH>), grid, dim3(256), lds, s, a); break;
+    case GEMM_TANH_BIAS_PLANES:
+      hipLaunchKernelGGL((k_gemm_sf16<TA, TB, GEMM_TANH_BIAS_PLANES>), grid, dim3(256), lds, s, a);
+      break;
     default: return fail(RLKS_ERR_ARG, "gemm: unknown epilogue");
   }
   RLKS_LAUNCHED();
@@ -377,7 +387,9 @@ int gemm_splits(int M, int N, int K) {
 }
 
 int launch_gemm_sf16(const GemmArgs& a, hipStream_t s) {
-  RLKS_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.A && a.B && a.C && a.amax && a.bmax, RLKS_ERR_ARG, "gemm: bad argument");
+  RLKS_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.A && a.B && a.amax && a.bmax &&
+                   (a.epi == GEMM_TANH_BIAS_PLANES ? (a.c_hi && a.c_lo) : a.C != nullptr),
+               RLKS_ERR_ARG, "gemm: bad argument");
   if (a.splits <= 1) return launch_any(a, s);
   RLKS_REQUIRE(a.part && a.epi == GEMM_STORE, RLKS_ERR_ARG, "gemm: split-K needs a partial buffer and GEMM_STORE");
   // layers beyond the last non-empty K range would write zero partials: trim them

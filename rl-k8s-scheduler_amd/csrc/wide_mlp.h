@@ -6,13 +6,16 @@
 namespace rlks {
 
 struct WideNet {
-  float *h1, *h2, *out, *dout;  // [M][H], [M][H], [M][A_net], [M][A_net]
+  _Float16 *h1h, *h1l;          // H1 as fp16 planes [M][H] at 2^14 (the pre-split GEMMs' operand)
+  float *h2, *out, *dout;       // [M][H], [M][A_net], [M][A_net]
+  _Float16 *w2h, *w2l;          // W2 planes [H][H] (this SGD step's / forward's weights)
   unsigned* slots;              // operand max |x| slots
   float* part_stat;             // [blocks][4]
 };
 struct WideWs {
   WideNet n[2];
   float *dza, *dzb;  // [M][H] dZ2 / dZ1
+  _Float16 *dzh, *dzl;  // dZ2 planes [M][H]
   double* rew64;     // [M] env-step scratch (rollout)
   float* part;       // split-K / split column-sum partials of the weight gradients
   unsigned* stat_slots;

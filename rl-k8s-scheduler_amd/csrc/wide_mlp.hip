@@ -12,8 +12,11 @@
 //   dW3 = dout^T H2 (TN)   db3 = colsum(dout)
 //   dZ2 = (dout W3) * (1 - H2^2) (NN, fused)   dW2 = dZ2^T H1 (TN)   db2 = colsum(dZ2)
 //   dZ1 = (dZ2 W2) * (1 - H1^2) (NN, fused)    dW1 = dZ1^T X  (TN)   db1 = colsum(dZ1)
+// The three H x H GEMMs (Z2, dZ1, dW2) run on the pre-split kernel (gemm_ps.hip): H1 is written as
+// fp16 planes at the fixed scale 2^14 by Z1's epilogue (|tanh| < 1), W2 and dZ2 are split into
+// planes once (rlks split pass) after their max |x| is known; the others use the generic kernel.
 // Operand scales: max |x| slots filled by rlks_absmax (X, weights) or by the producing GEMM's
-// epilogue (H1, H2, dZ2, dZ1), the loss kernel (dout).
+// epilogue (H2, dZ2, dZ1), the loss kernel (dout).
 #include "wide_mlp.h"
 
 #include "gemm_sf16.h"
@@ -33,12 +36,16 @@ WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
     return p;
   };
   w.M = M;
+  const int Mp = (M + 31) / 32 * 32;  // plane rows: the dW2 reduction runs over whole 32-row chunks
   w.blocks = (M + LOSS_ROWS - 1) / LOSS_ROWS;
   for (int net = 0; net < 2; ++net) {
     const int An = net == 0 ? A : 1;
     WideNet& n = w.n[net];
-    n.h1 = (float*)take(4LL * M * H);
+    n.h1h = (_Float16*)take(2LL * Mp * H);
+    n.h1l = (_Float16*)take(2LL * Mp * H);
     n.h2 = (float*)take(4LL * M * H);
+    n.w2h = (_Float16*)take(2LL * H * H);
+    n.w2l = (_Float16*)take(2LL * H * H);
     n.out = (float*)take(4LL * M * An);
     n.dout = (float*)take(4LL * M * An);
     n.slots = (unsigned*)take(4 * SL_N);
@@ -46,11 +53,13 @@ WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
   }
   w.dza = (float*)take(4LL * M * H);
   w.dzb = (float*)take(4LL * M * H);
+  w.dzh = (_Float16*)take(2LL * Mp * H);
+  w.dzl = (_Float16*)take(2LL * Mp * H);
   w.rew64 = (double*)take(8LL * M);
   {  // weight-gradient partials: dW3 [A][H], dW2 [H][H], dW1 [H][D] (K = M), column sums of M rows
     int64_t pf = (int64_t)colsum_splits(M) * H;
     pf = std::max(pf, (int64_t)gemm_splits(A, H, M) * A * H);
-    pf = std::max(pf, (int64_t)gemm_splits(H, H, M) * H * H);
+    pf = std::max(pf, (int64_t)gemm_ps_splits(H, H, Mp) * H * H);
     pf = std::max(pf, (int64_t)gemm_splits(H, D, M) * H * D);
     w.part = (float*)take(4 * pf);
   }
@@ -199,8 +208,10 @@ Net net_of(const float* params, const Layout& L, int net) {
 
 int gemm(const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C, int ldc, int M, int N, int K,
          int epi, const float* bias, const float* aux, int ldaux, const unsigned* amax, const unsigned* bmax,
-         unsigned* cmax, hipStream_t s, float* part = nullptr) {
+         unsigned* cmax, hipStream_t s, float* part = nullptr, _Float16* c_hi = nullptr, _Float16* c_lo = nullptr) {
   GemmArgs g{};
+  g.c_hi = c_hi;
+  g.c_lo = c_lo;
   if (part) {  // weight gradient (K = minibatch rows): split K over workgroup layers
     g.splits = gemm_splits(M, N, K);
     g.part = part;
@@ -212,7 +223,16 @@ int gemm(const float* A, int lda, int ta, const float* B, int ldb, int tb, float
   return launch_gemm_sf16(g, s);
 }
 
-// forward of net `net` over M rows of x (row stride ldx): H1, H2 and out in the workspace
+// pre-split operand: planes (hi, lo), row stride ld, K-major or not, rows, scale slot (null: 2^fexp)
+PsOperand ps_op(const _Float16* hi, const _Float16* lo, int ld, int kmajor, int rows, const unsigned* slot,
+                int fexp = 0) {
+  PsOperand o{};
+  o.hi = hi; o.lo = lo; o.ld = ld; o.kmajor = kmajor; o.rows = rows; o.maxslot = slot; o.fexp = fexp;
+  return o;
+}
+constexpr int H1_EXP = 14;  // H1 planes hold tanh x 2^14
+
+// forward of net `net` over M rows of x (row stride ldx): H1 (planes), H2 and out in the workspace
 int forward_net(const rlks_mlp_desc* d, const Net& P, const WideNet& n, const float* x, int ldx, int M, int net,
                 hipStream_t s) {
   const int D = d->obs_dim, H = d->hidden, An = net == 0 ? d->n_actions : 1;
@@ -221,12 +241,17 @@ int forward_net(const rlks_mlp_desc* d, const Net& P, const WideNet& n, const fl
   if (int rc = launch_absmax(P.w1, H, D, D, sl + SL_W1, s)) return rc;
   if (int rc = launch_absmax(P.w2, H, H, H, sl + SL_W2, s)) return rc;
   if (int rc = launch_absmax(P.w3, An, H, H, sl + SL_W3, s)) return rc;
-  if (int rc = gemm(x, ldx, 0, P.w1, D, 1, n.h1, H, M, H, D, GEMM_TANH_BIAS, P.b1, nullptr, 0, sl + SL_X,
-                    sl + SL_W1, sl + SL_H1, s))
+  if (int rc = launch_split_planes(P.w2, H, H, H, sl + SL_W2, 0, n.w2h, n.w2l, H, s)) return rc;
+  if (int rc = gemm(x, ldx, 0, P.w1, D, 1, nullptr, H, M, H, D, GEMM_TANH_BIAS_PLANES, P.b1, nullptr, 0, sl + SL_X,
+                    sl + SL_W1, nullptr, s, nullptr, n.h1h, n.h1l))
     return rc;
-  if (int rc = gemm(n.h1, H, 0, P.w2, H, 1, n.h2, H, M, H, H, GEMM_TANH_BIAS, P.b2, nullptr, 0, sl + SL_H1,
-                    sl + SL_W2, sl + SL_H2, s))
-    return rc;
+  {  // Z2 = H1 W2^T -> H2 = tanh(Z2 + b2)
+    PsArgs a{};
+    a.a = ps_op(n.h1h, n.h1l, H, 0, M, nullptr, H1_EXP);
+    a.b = ps_op(n.w2h, n.w2l, H, 0, H, sl + SL_W2);
+    a.M = M; a.N = H; a.K = H; a.epi = PS_TANH_BIAS; a.C = n.h2; a.ldc = H; a.bias = P.b2; a.cmax = sl + SL_H2;
+    if (int rc = launch_gemm_ps(a, s)) return rc;
+  }
   return gemm(n.h2, H, 0, P.w3, H, 1, n.out, An, M, An, H, GEMM_BIAS, P.b3, nullptr, 0, sl + SL_H2, sl + SL_W3,
               nullptr, s);
 }
@@ -252,6 +277,12 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
               const float* mb, int M, float* grad, double* stats, const WideWs& w, hipStream_t s) {
   const int D = d->obs_dim, H = d->hidden, A = d->n_actions, stride = mb_stride(D, A);
   const Layout L = make_layout(D, H, A);
+  const int Mp = (M + 31) / 32 * 32;
+  if (Mp != M) {  // zero plane rows [M, Mp): the dW2 reduction over Mp rows then adds exact zeros
+    const size_t off = (size_t)M * H, bytes = 2ull * (Mp - M) * H;
+    for (_Float16* p : {w.n[0].h1h, w.n[0].h1l, w.n[1].h1h, w.n[1].h1l, w.dzh, w.dzl})
+      RLKS_HIP(hipMemsetAsync(p + off, 0, bytes, s));
+  }
   for (int net = 0; net < 2; ++net) {
     const int An = net == 0 ? A : 1;
     const WideNet& n = w.n[net];
@@ -277,14 +308,26 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     if (int rc = gemm(n.dout, An, 0, P.w3, H, 0, w.dza, H, M, H, An, GEMM_DTANH, nullptr, n.h2, H, sl + SL_DOUT,
                       sl + SL_W3, sl + SL_DZ2, s))
       return rc;
-    if (int rc = gemm(w.dza, H, 1, n.h1, H, 0, g + o[2], H, H, H, M, GEMM_STORE, nullptr, nullptr, 0, sl + SL_DZ2,
-                      sl + SL_H1, nullptr, s, w.part))
-      return rc;
+    if (int rc = launch_split_planes(w.dza, M, H, H, sl + SL_DZ2, 0, w.dzh, w.dzl, H, s)) return rc;
+    {  // dW2[n][k] = sum_m dZ2[m][n] H1[m][k]: both operands K-major planes, split over the rows
+      PsArgs a{};
+      a.a = ps_op(w.dzh, w.dzl, H, 1, H, sl + SL_DZ2);
+      a.b = ps_op(n.h1h, n.h1l, H, 1, H, nullptr, H1_EXP);
+      a.M = H; a.N = H; a.K = Mp; a.epi = PS_STORE; a.C = g + o[2]; a.ldc = H;
+      a.splits = gemm_ps_splits(H, H, Mp);
+      a.part = w.part;
+      if (int rc = launch_gemm_ps(a, s)) return rc;
+    }
     if (int rc = launch_colsum(w.dza, M, H, H, g + o[3], 0, w.part, s)) return rc;
-    // dZ1 = (dZ2 W2) (1 - H1^2); dW1 = dZ1^T X; db1
-    if (int rc = gemm(w.dza, H, 0, P.w2, H, 0, w.dzb, H, M, H, H, GEMM_DTANH, nullptr, n.h1, H, sl + SL_DZ2,
-                      sl + SL_W2, sl + SL_DZ1, s))
-      return rc;
+    {  // dZ1[m][k] = (sum_n dZ2[m][n] W2[n][k]) (1 - H1^2): B = W2 planes read K-major
+      PsArgs a{};
+      a.a = ps_op(w.dzh, w.dzl, H, 0, M, sl + SL_DZ2);
+      a.b = ps_op(n.w2h, n.w2l, H, 1, H, sl + SL_W2);
+      a.M = M; a.N = H; a.K = H; a.epi = PS_DTANH; a.C = w.dzb; a.ldc = H;
+      a.aux_hi = n.h1h; a.aux_lo = n.h1l; a.ldaux = H; a.cmax = sl + SL_DZ1;
+      if (int rc = launch_gemm_ps(a, s)) return rc;
+    }
+    // dW1 = dZ1^T X; db1
     if (int rc = gemm(w.dzb, H, 1, mb, stride, 0, g + o[0], D, H, D, M, GEMM_STORE, nullptr, nullptr, 0, sl + SL_DZ1,
                       sl + SL_X, nullptr, s, w.part))
       return rc;

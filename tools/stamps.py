@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
-"""Phase timing of the split-fp16 F1 kernel from in-kernel s_memtime stamps (diagnostic build).
+"""Phase timing of the split-fp16 F1a kernel (k_sf_fwd) from in-kernel s_memtime stamps (diagnostic build).
 
   make -C rl-k8s-scheduler_amd/csrc stamps
   RLKS_LIB=rl-k8s-scheduler_amd/rlks/librlks_stamps.so python tools/stamps.py
 
 Runs a few c2-sized SGD-step gradients (65,536 rows), then prints, per net, the median over waves
-of each phase's shader cycles (the stamps are taken by lane 0 of every wave after the phase)."""
+of each phase's shader cycles (the stamps are taken by lane 0 of every wave after the phase), and how
+the waves that share a SIMD overlap in time.  --roll: the rollout step kernel's phases."""
 import ctypes as C
 import os
 import sys
@@ -15,7 +16,6 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "rl-k8s-scheduler_amd"))
-PHASES = ["prologue", "Z2 loop", "head+loss", "dW3/stats", "dZ2 store+split", "dH1 loop", "epilogue"]
 
 
 def roll():
@@ -44,7 +44,7 @@ def roll():
 
 def fwd_report(lib, tiles):
     """F1a (k_sf_fwd) phases per wave, and how the waves that share a SIMD overlap in time"""
-    st = np.zeros((2, 4096, 8), np.uint64)
+    st = np.zeros((2, 8192, 8), np.uint64)
     assert lib.rlks_dbg_fa_stamps(st.ctypes.data_as(C.c_void_p)) == 0
     names = ["prologue", "Z2 k-tile 0", "Z2 k-tiles 1-7", "H2 + head", "loss + dW3 + stats", "dZ2 store"]
     t = st[:, :tiles, :7].astype(np.int64)
@@ -114,33 +114,7 @@ def main():
         _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
                   rows, grad.data_ptr(), None, ws.data_ptr(), ws.numel(), None)
     torch.cuda.synchronize()
-    tiles = rows // 32
-    if getattr(_lib.lib(), "rlks_dbg_fa_stamps", None) is not None and os.environ.get("RLKS_F1_SPLIT", "1") != "0":
-        fwd_report(_lib.lib(), tiles)  # split F1 (the default): F1a phases
-        return
-    st = np.zeros((2, 4096, 8), np.uint64)
-    assert _lib.lib().rlks_dbg_sf_stamps(st.ctypes.data_as(C.c_void_p)) == 0
-    tiles = rows // 32
-    for net in range(2):
-        s = st[net, :tiles].astype(np.int64)
-        dt = np.diff(s, axis=1)
-        tot = s[:, 7] - s[:, 0]
-        start = s[:, 0] - s[:, 0].min()
-        print(f"net {net}: wave lifetime median {np.median(tot):.0f} cyc, start spread {start.max():.0f} cyc")
-        for i, name in enumerate(PHASES):
-            print(f"  {name:18s} median {np.median(dt[:, i]):8.0f}  p90 {np.percentile(dt[:, i], 90):8.0f}"
-                  f"  share {np.median(dt[:, i]) / np.median(tot):.2f}")
-    fn = getattr(_lib.lib(), "rlks_dbg_sf_stamps2", None)
-    if fn is not None:
-        st2 = np.zeros((2, 4096, 8), np.uint64)
-        assert fn(st2.ctypes.data_as(C.c_void_p)) == 0
-        for net in range(2):
-            s = st2[net, :tiles].astype(np.int64)
-            print(f"net {net} loop internals (one step): Z2 MFMA steps {np.median(s[:, 1] - s[:, 0]):.0f}, "
-                  f"chunk store {np.median(s[:, 2] - s[:, 1]):.0f}, barrier {np.median(s[:, 3] - s[:, 2]):.0f}; "
-                  f"dH1 MFMA steps {np.median(s[:, 5] - s[:, 4]):.0f}, chunk store {np.median(s[:, 6] - s[:, 5]):.0f}, "
-                  f"barrier {np.median(s[:, 7] - s[:, 6]):.0f}")
-
+    fwd_report(_lib.lib(), rows // 16)  # F1a (k_sf_fwd) phases, one wave per 16-row tile
 
 if __name__ == "__main__":
     main()
