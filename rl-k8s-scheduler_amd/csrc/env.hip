@@ -224,6 +224,15 @@ __global__ __launch_bounds__(256) void k_env_step2(EnvView v, const double* __re
 // only the clusters where a pod leaves and the first-fit prefix: per env-step about one cluster of
 // nodes at c3's stationary churn instead of all C x N.
 constexpr int SKIP_LDS_MAX = 4096;  // survival-table entries staged in LDS (16 KB)
+// the lane-per-(env, cluster) step stages the table too: at c3's heavy churn (4,096 entries)
+// 0.398 -> 0.314 ms against reading it through L1/L2 (profiles/r03b/node_ab.txt)
+#ifndef RLKS_NODE_EC_LDS_SKIP_MAX
+#define RLKS_NODE_EC_LDS_SKIP_MAX 4096
+#endif
+constexpr int NODE_EC_LDS_SKIP_MAX = RLKS_NODE_EC_LDS_SKIP_MAX;
+#ifndef RLKS_NODE_EC_MAX_C
+#define RLKS_NODE_EC_MAX_C 64  // (A/B builds set 0: every node env on the lane-per-env kernel)
+#endif
 
 __device__ __forceinline__ int node_pods(const EnvView& v, int32_t cc, int32_t free_cpu) {
   return (int)(__umul24((uint32_t)(cc - free_cpu), v.pod_mag) >> v.pod_shift);
@@ -277,6 +286,262 @@ __device__ __forceinline__ void node_obs_row(const EnvView& v, const double* __r
     o[2 * C + c] = __fdiv_rn((float)v.used_cpu[(size_t)c * v.N + lane], (float)(v.nodes * v.cap[c]));
 }
 
+// step counters of one lane (summed per wave into v.counters when enabled)
+struct NodeCounters {
+  unsigned long long checks = 0, placed = 0, rej = 0, dep = 0, wr = 0, rd = 0;
+};
+
+// 1. departures of cluster c (nodes `col`, chunk totals `tot`, `used` millicores in/out): the pods
+// are numbered in node order at the start of the step; a geometric skip over the survival table S
+// picks the next departing pod, the chunk holding it is located from the chunk totals (8 totals a
+// 16-byte load) and loaded once, and written back when the walk moves past it.  Philox counter
+// {gid, episode, t | draw << 16, DEPART << 16 | c}.
+__device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t* S, uint32_t gid, int ep, int t, int c,
+                                               int2* col, uint16_t* tot, int32_t& used, NodeCounters& k) {
+  const int N = v.nodes;
+  const int32_t pc = v.pod_cpu, pm = v.pod_mem, cc = v.cap[c];
+  const int P = used / pc;
+  if (P == 0) return;
+  int pos = 0, n = 0;
+  int grp = 0, gcum = 0, gsum = -1;  // group of 8 chunk totals holding the next pod
+  int gt[8];
+  int ch = -1, ccum = 0, ctot = 0;    // loaded chunk, pods before it, its pods at the start
+  int2 f[8];
+  int dep[8];
+  u32x4 x{0u, 0u, 0u, 0u};
+  while (pos < P) {
+    if ((n & 3) == 0)
+      x = philox4x32_10_mad(u32x4{gid, (uint32_t)ep, (uint32_t)t | ((uint32_t)(n >> 2) << 16),
+                                  ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)c},
+                            v.k0, v.k1);
+    const uint32_t u = (n & 3) == 0 ? x.x : (n & 3) == 1 ? x.y : (n & 3) == 2 ? x.z : x.w;
+    ++n;
+    const int R = P - pos;
+    if (u < (R < v.n_skip ? S[R] : 0u)) break;  // none of the remaining R pods leaves
+    // surviving pods before the departure: the largest s in [0, min(R, L)) with S[s] > u
+    int lo = 0, hi = min(R, v.n_skip) - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (S[mid] > u) lo = mid;
+      else hi = mid - 1;
+    }
+    const int idx = pos + lo;
+    pos = idx + 1;
+    // pod idx: its group, chunk, node
+    for (;;) {
+      if (!dcheck(8 * grp < (N >> 3), DC_NODE_GROUP, grp)) grp = ((N >> 3) - 1) >> 3;
+      if (gsum < 0) gsum = load_tot8(tot + 8 * grp, gt);
+      if (idx < gcum + gsum) break;
+      gcum += gsum;
+      ++grp;
+      gsum = -1;
+    }
+    int j = 0, cj = gcum, tj = gt[0];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (j == q && idx >= cj + gt[q]) { cj += gt[q]; j = q + 1; }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) tj = (q == j) ? gt[q] : tj;
+    if (!dcheck(8 * grp + j < (N >> 3), DC_NODE_CHUNK, 8 * grp + j)) j = (N >> 3) - 1 - 8 * grp;
+    if (8 * grp + j != ch) {
+      if (ch >= 0) flush_chunk(col, tot, ch, ctot, f, dep, k.wr);
+      ch = 8 * grp + j;
+      ccum = cj;
+      ctot = tj;
+      load_chunk(col + 8 * ch, f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dep[q] = 0;
+      ++k.rd;
+    }
+    int qn = 0, cq = ccum;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int pq = node_pods(v, cc, f[q].x) + dep[q];
+      if (qn == q && idx >= cq + pq) { cq += pq; qn = q + 1; }
+    }
+    if (!dcheck(qn < 8, DC_NODE_POD, idx)) qn = 7;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q == qn) {
+        ++dep[q];
+        f[q].x += pc;
+        f[q].y += pm;
+      }
+    used -= pc;
+    ++k.dep;
+  }
+  if (ch >= 0) flush_chunk(col, tot, ch, ctot, f, dep, k.wr);  // some pod left this cluster
+}
+
+// 2. `rem` arriving pods onto cluster a, first fit: chunks whose 8 nodes are all full are skipped
+// by their totals, the others are loaded and filled node by node in order.  rem: pods left over.
+__device__ __forceinline__ void first_fit_cluster(const EnvView& v, int a, int2* col, uint16_t* tot, int& rem,
+                                                  int32_t& used, NodeCounters& k) {
+  const int N = v.nodes, C = v.C;
+  const int32_t pc = v.pod_cpu, pm = v.pod_mem;
+  const int32_t cc = v.cap[a], cm = v.cap[C + a];
+  const int full = 8 * min(cc / pc, cm / pm);
+  const int NC = N >> 3;
+  int placed = 0, last = -1;
+  for (int g = 0; 8 * g < NC && rem > 0; ++g) {
+    int gt[8];
+    (void)load_tot8(tot + 8 * g, gt);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int chn = 8 * g + j;
+      if (rem > 0 && chn < NC && gt[j] < full) {
+        int2 f[8];
+        load_chunk(col + 8 * chn, f);
+        ++k.rd;
+        int here = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          int put = 0;
+          while (rem > 0 && f[q].x >= pc && f[q].y >= pm) {
+            f[q].x -= pc;
+            f[q].y -= pm;
+            --rem;
+            ++put;
+          }
+          if (put) {
+            col[8 * chn + q] = f[q];
+            ++k.wr;
+            here += put;
+            last = 8 * chn + q;
+          }
+        }
+        if (here) tot[chn] = (uint16_t)(gt[j] + here);
+        placed += here;
+      }
+    }
+  }
+  used += placed * pc;
+  const int nfin = rem > 0 ? N : (placed ? last : 0);
+  k.checks += (unsigned long long)(placed + nfin);
+  k.placed += (unsigned long long)placed;
+  k.rej += (unsigned long long)rem;
+}
+
+__device__ __forceinline__ void node_counters_flush(const EnvView& v, NodeCounters k) {
+  if (!v.counters) return;
+  k.checks = wave_sum_u64(k.checks);
+  k.placed = wave_sum_u64(k.placed);
+  k.rej = wave_sum_u64(k.rej);
+  k.dep = wave_sum_u64(k.dep);
+  k.wr = wave_sum_u64(k.wr);
+  k.rd = wave_sum_u64(k.rd);
+  if ((threadIdx.x & 63) == 0) {
+    if (k.checks) atomicAdd(&v.counters[0], k.checks);
+    if (k.placed) atomicAdd(&v.counters[1], k.placed);
+    if (k.rej) atomicAdd(&v.counters[2], k.rej);
+    if (k.dep) atomicAdd(&v.counters[3], k.dep);
+    if (k.wr) atomicAdd(&v.counters[4], k.wr);
+    if (k.rd) atomicAdd(&v.counters[5], k.rd);
+  }
+}
+
+__device__ __forceinline__ double node_reward(const EnvView& v, const double* __restrict__ cost,
+                                              const double* __restrict__ lat, int t, int a, int rem) {
+  double r = __dmul_rn(v.scale, __dadd_rn(__dmul_rn(v.w_cost, cost[t * v.C + a]), __dmul_rn(v.w_lat, lat[t * v.C + a])));
+  if (v.penalty != 0.0) r = __dsub_rn(r, __dmul_rn(v.penalty, (double)rem));
+  return r;
+}
+
+// One lane per (env, cluster): lane c of env `lane` walks cluster c's departures; the lane of the
+// chosen cluster a also draws the arrivals, places them first fit and does the env's bookkeeping
+// (reward, step, episode return); every lane writes its cluster's three obs columns (cost, latency,
+// utilisation) and, on auto-reset, redraws its cluster's occupancy.  A cluster's nodes are touched
+// by its lane only, so the lanes need no synchronisation; an env's CP = 2^cs lanes (C <= CP <= 64)
+// are adjacent in one wave, whose step/episode loads precede the chosen lane's stores in program
+// order.  Consecutive lanes write consecutive obs floats.  Same results, counters included, as
+// k_node_step's lane per env (the C > 64 path).
+template <bool LDS_SKIP>
+__global__ void __launch_bounds__(256) k_node_step_ec(EnvView v, const double* __restrict__ cost,
+                                                      const double* __restrict__ lat,
+                                                      const int32_t* __restrict__ actions, float* __restrict__ obs,
+                                                      double* __restrict__ rew64, float* __restrict__ rew32,
+                                                      uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                      int32_t* __restrict__ step_out, float* __restrict__ final_obs,
+                                                      int32_t* __restrict__ status, int cs) {
+  if (status && status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
+  __shared__ uint32_t s_skip[LDS_SKIP ? SKIP_LDS_MAX : 1];
+  if (LDS_SKIP) {
+    for (int i = threadIdx.x; i < v.n_skip; i += blockDim.x) s_skip[i] = v.skip[i];
+    __syncthreads();
+  }
+  const uint32_t* S = LDS_SKIP ? s_skip : v.skip;
+  const int c = threadIdx.x & ((1 << cs) - 1);
+  const int lane = blockIdx.x * (blockDim.x >> cs) + (threadIdx.x >> cs);
+  const int C = v.C, N = v.nodes, D = 3 * C;
+  bool over = false;
+  NodeCounters k;
+  if (lane < v.N && c < C) {
+    const int t = v.step[lane], ep = v.episode[lane];
+    int a = actions[lane];
+    if (!dcheck(a >= 0 && a < C, DC_NODE_ACTION, a)) a = 0;
+    if (t >= v.T) {  // iloc[t] out of bounds before any change
+      if (c == 0) {
+        over = true;
+        if (rew64) rew64[lane] = 0.0;
+        if (rew32) rew32[lane] = 0.f;
+        term[lane] = 0;
+        if (step_out) step_out[lane] = t;
+        if (trunc) trunc[lane] = 0;
+      }
+    } else {
+      const uint32_t gid = (uint32_t)(v.env_offset + lane);
+      int2* col = node_col(v, lane) + (size_t)c * N;
+      uint16_t* tot = chunk_tot(v, lane, c);
+      int32_t* usedp = v.used_cpu + (size_t)c * v.N + lane;
+      const int32_t used0 = *usedp;
+      int32_t used = used0;
+      if (v.depart_prob > 0.0) depart_cluster(v, S, gid, ep, t, c, col, tot, used, k);
+      int rem = 0;
+      if (c == a) {
+        rem = arrivals(v, gid, ep, t);
+        first_fit_cluster(v, a, col, tot, rem, used, k);
+      }
+      // 3. step (:115-144): row t1 = t + 1, done, auto-reset, obs
+      const int t1 = t + 1;
+      const bool done = t1 >= v.max_steps;
+      const bool reset = t1 < v.T && done && v.autoreset;
+      if (reset) {
+        if (final_obs) {
+          float* o = final_obs + (size_t)lane * D;
+          o[c] = (float)cost[t1 * C + c];
+          o[C + c] = (float)lat[t1 * C + c];
+          o[2 * C + c] = __fdiv_rn((float)used, (float)(N * v.cap[c]));
+        }
+        used = nodes_reset_cluster(v, col, tot, c, gid, ep + 1);
+      }
+      if (used != used0 || reset) *usedp = used;
+      if (t1 < v.T) {
+        const int row = reset ? 0 : t1;
+        float* o = obs + (size_t)lane * D;
+        o[c] = (float)cost[row * C + c];
+        o[C + c] = (float)lat[row * C + c];
+        o[2 * C + c] = __fdiv_rn((float)used, (float)(N * v.cap[c]));
+      }
+      if (c == a) {
+        const double r = node_reward(v, cost, lat, t, a, rem);
+        v.step[lane] = reset ? 0 : t1;
+        if (t1 >= v.T) over = true;
+        else if (v.track_returns) track_return(v, lane, ep, r, done);
+        if (reset) v.episode[lane] = ep + 1;
+        if (rew64) rew64[lane] = r;
+        if (rew32) rew32[lane] = (float)r;
+        term[lane] = (uint8_t)done;
+        if (step_out) step_out[lane] = t1;
+        if (trunc) trunc[lane] = 0;
+      }
+    }
+  }
+  node_counters_flush(v, k);
+  const unsigned long long m = __ballot(over);
+  if (status && (threadIdx.x & 63) == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
+}
+
+// One lane per env, clusters in turn (C > 64: more clusters than a wave has lanes)
 template <bool LDS_SKIP>
 __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __restrict__ cost,
                                                    const double* __restrict__ lat,
@@ -294,9 +559,8 @@ __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __re
   const uint32_t* S = LDS_SKIP ? s_skip : v.skip;
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   const int C = v.C, N = v.nodes, D = 3 * C;
-  const int32_t pc = v.pod_cpu, pm = v.pod_mem;
   bool over = false;
-  unsigned long long n_checks = 0, n_placed = 0, n_rej = 0, n_dep = 0, n_wr = 0, n_rd = 0;
+  NodeCounters k;
   if (lane < v.N) {
     const int t = v.step[lane], ep = v.episode[lane];
     int a = actions[lane];
@@ -309,139 +573,21 @@ __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __re
     } else {
       const uint32_t gid = (uint32_t)(v.env_offset + lane);
       int2* nodes = node_col(v, lane);
-      // 1. departures
       for (int c = 0; c < C && v.depart_prob > 0.0; ++c) {
         int32_t used = v.used_cpu[(size_t)c * v.N + lane];
-        const int P = used / pc;
-        if (P == 0) continue;
-        const int32_t cc = v.cap[c];
-        int2* col = nodes + (size_t)c * N;
-        uint16_t* tot = chunk_tot(v, lane, c);
-        int pos = 0, k = 0;
-        int grp = 0, gcum = 0, gsum = -1;  // group of 8 chunk totals holding the next pod
-        int gt[8];
-        int ch = -1, ccum = 0, ctot = 0;    // loaded chunk, pods before it, its pods at the start
-        int2 f[8];
-        int dep[8];
-        u32x4 x{0u, 0u, 0u, 0u};
-        while (pos < P) {
-          if ((k & 3) == 0)
-            x = philox4x32_10_mad(u32x4{gid, (uint32_t)ep, (uint32_t)t | ((uint32_t)(k >> 2) << 16),
-                                        ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)c},
-                                  v.k0, v.k1);
-          const uint32_t u = (k & 3) == 0 ? x.x : (k & 3) == 1 ? x.y : (k & 3) == 2 ? x.z : x.w;
-          ++k;
-          const int R = P - pos;
-          if (u < (R < v.n_skip ? S[R] : 0u)) break;  // none of the remaining R pods leaves
-          // surviving pods before the departure: the largest s in [0, min(R, L)) with S[s] > u
-          int lo = 0, hi = min(R, v.n_skip) - 1;
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (S[mid] > u) lo = mid;
-            else hi = mid - 1;
-          }
-          const int idx = pos + lo;
-          pos = idx + 1;
-          // pod idx (numbered in node order at the start of the step): its group, chunk, node
-          for (;;) {
-            if (!dcheck(8 * grp < (N >> 3), DC_NODE_GROUP, grp)) grp = ((N >> 3) - 1) >> 3;
-            if (gsum < 0) gsum = load_tot8(tot + 8 * grp, gt);
-            if (idx < gcum + gsum) break;
-            gcum += gsum;
-            ++grp;
-            gsum = -1;
-          }
-          int j = 0, cj = gcum, tj = gt[0];
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (j == q && idx >= cj + gt[q]) { cj += gt[q]; j = q + 1; }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) tj = (q == j) ? gt[q] : tj;
-          if (!dcheck(8 * grp + j < (N >> 3), DC_NODE_CHUNK, 8 * grp + j)) j = (N >> 3) - 1 - 8 * grp;
-          if (8 * grp + j != ch) {
-            if (ch >= 0) flush_chunk(col, tot, ch, ctot, f, dep, n_wr);
-            ch = 8 * grp + j;
-            ccum = cj;
-            ctot = tj;
-            load_chunk(col + 8 * ch, f);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) dep[q] = 0;
-            ++n_rd;
-          }
-          int qn = 0, cq = ccum;
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int pq = node_pods(v, cc, f[q].x) + dep[q];
-            if (qn == q && idx >= cq + pq) { cq += pq; qn = q + 1; }
-          }
-          if (!dcheck(qn < 8, DC_NODE_POD, idx)) qn = 7;
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (q == qn) {
-              ++dep[q];
-              f[q].x += pc;
-              f[q].y += pm;
-            }
-          used -= pc;
-          ++n_dep;
-        }
-        if (ch >= 0) {  // some pod left this cluster
-          flush_chunk(col, tot, ch, ctot, f, dep, n_wr);
-          v.used_cpu[(size_t)c * v.N + lane] = used;
-        }
+        const int32_t used0 = used;
+        depart_cluster(v, S, gid, ep, t, c, nodes + (size_t)c * N, chunk_tot(v, lane, c), used, k);
+        if (used != used0) v.used_cpu[(size_t)c * v.N + lane] = used;
       }
-      // 2. arrivals at the chosen cluster, first fit: chunks whose 8 nodes are all full are skipped
-      // by their totals, the others are loaded and filled node by node in order
       int rem = arrivals(v, gid, ep, t);
+      if (!dcheck(a >= 0 && a < C, DC_NODE_ACTION, a)) a = 0;
       {
-        if (!dcheck(a >= 0 && a < C, DC_NODE_ACTION, a)) a = 0;
-        const int32_t cc = v.cap[a], cm = v.cap[C + a];
-        const int full = 8 * min(cc / pc, cm / pm);
-        int2* col = nodes + (size_t)a * N;
-        uint16_t* tot = chunk_tot(v, lane, a);
-        const int NC = N >> 3;
-        int placed = 0, last = -1;
-        for (int g = 0; 8 * g < NC && rem > 0; ++g) {
-          int gt[8];
-          (void)load_tot8(tot + 8 * g, gt);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int chn = 8 * g + j;
-            if (rem > 0 && chn < NC && gt[j] < full) {
-              int2 f[8];
-              load_chunk(col + 8 * chn, f);
-              ++n_rd;
-              int here = 0;
-#pragma unroll
-              for (int q = 0; q < 8; ++q) {
-                int put = 0;
-                while (rem > 0 && f[q].x >= pc && f[q].y >= pm) {
-                  f[q].x -= pc;
-                  f[q].y -= pm;
-                  --rem;
-                  ++put;
-                }
-                if (put) {
-                  col[8 * chn + q] = f[q];
-                  ++n_wr;
-                  here += put;
-                  last = 8 * chn + q;
-                }
-              }
-              if (here) tot[chn] = (uint16_t)(gt[j] + here);
-              placed += here;
-            }
-          }
-        }
-        if (placed) v.used_cpu[(size_t)a * v.N + lane] += placed * pc;
-        const int nfin = rem > 0 ? N : (placed ? last : 0);
-        n_checks = (unsigned long long)(placed + nfin);
-        n_placed = (unsigned long long)placed;
-        n_rej = (unsigned long long)rem;
+        int32_t used = v.used_cpu[(size_t)a * v.N + lane];
+        const int32_t used0 = used;
+        first_fit_cluster(v, a, nodes + (size_t)a * N, chunk_tot(v, lane, a), rem, used, k);
+        if (used != used0) v.used_cpu[(size_t)a * v.N + lane] = used;
       }
-      // 3. step (:115-144): reward on row t, t += 1, done, episode bookkeeping, obs
-      double r = __dmul_rn(v.scale, __dadd_rn(__dmul_rn(v.w_cost, cost[t * C + a]), __dmul_rn(v.w_lat, lat[t * C + a])));
-      if (v.penalty != 0.0) r = __dsub_rn(r, __dmul_rn(v.penalty, (double)rem));
+      const double r = node_reward(v, cost, lat, t, a, rem);
       const int t1 = t + 1;
       v.step[lane] = t1;
       const bool done = t1 >= v.max_steps;
@@ -466,22 +612,7 @@ __global__ void __launch_bounds__(256) k_node_step(EnvView v, const double* __re
     }
     if (trunc) trunc[lane] = 0;
   }
-  if (v.counters) {
-    n_checks = wave_sum_u64(n_checks);
-    n_placed = wave_sum_u64(n_placed);
-    n_rej = wave_sum_u64(n_rej);
-    n_dep = wave_sum_u64(n_dep);
-    n_wr = wave_sum_u64(n_wr);
-    n_rd = wave_sum_u64(n_rd);
-    if ((threadIdx.x & 63) == 0) {
-      if (n_checks) atomicAdd(&v.counters[0], n_checks);
-      if (n_placed) atomicAdd(&v.counters[1], n_placed);
-      if (n_rej) atomicAdd(&v.counters[2], n_rej);
-      if (n_dep) atomicAdd(&v.counters[3], n_dep);
-      if (n_wr) atomicAdd(&v.counters[4], n_wr);
-      if (n_rd) atomicAdd(&v.counters[5], n_rd);
-    }
-  }
+  node_counters_flush(v, k);
   const unsigned long long m = __ballot(over);
   if (status && (threadIdx.x & 63) == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
 }
@@ -838,6 +969,20 @@ int rlks_env_step(rlks_env* e, const int32_t* actions, float* obs, double* rew64
     RLKS_LAUNCHED();
   }
   if (e->cfg.nodes_per_cluster > 0) {
+    const int C = e->cfg.n_clouds;
+    if (C <= RLKS_NODE_EC_MAX_C) {  // one lane per (env, cluster): 2^cs >= C lanes per env, 256 / 2^cs envs a block
+      int cs = 0;
+      while ((1 << cs) < C) ++cs;
+      const dim3 grid(cdiv(e->cfg.n_envs, 256 >> cs)), blk(256);
+      if (e->n_skip <= NODE_EC_LDS_SKIP_MAX)
+        hipLaunchKernelGGL(k_node_step_ec<true>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64,
+                           rew32, term, trunc, step_out, final_obs, status, cs);
+      else
+        hipLaunchKernelGGL(k_node_step_ec<false>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64,
+                           rew32, term, trunc, step_out, final_obs, status, cs);
+      RLKS_LAUNCHED();
+      return RLKS_OK;
+    }
     const dim3 grid(cdiv(e->cfg.n_envs, 256)), blk(256);
     if (e->n_skip <= SKIP_LDS_MAX)
       hipLaunchKernelGGL(k_node_step<true>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64, rew32,
