@@ -309,6 +309,7 @@ __device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t*
   int2 f[8];
   int dep[8];
   u32x4 x{0u, 0u, 0u, 0u};
+  const float inv_lg1p = 0.6931471805599453f / log1pf(-(float)v.depart_prob);  // 1 / log2(1 - p) = ln 2 / ln(1 - p) < 0
   while (pos < P) {
     if ((n & 3) == 0)
       x = philox4x32_10_mad(u32x4{gid, (uint32_t)ep, (uint32_t)t | ((uint32_t)(n >> 2) << 16),
@@ -318,14 +319,15 @@ __device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t*
     ++n;
     const int R = P - pos;
     if (u < (R < v.n_skip ? S[R] : 0u)) break;  // none of the remaining R pods leaves
-    // surviving pods before the departure: the largest s in [0, min(R, L)) with S[s] > u
-    int lo = 0, hi = min(R, v.n_skip) - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (S[mid] > u) lo = mid;
-      else hi = mid - 1;
-    }
-    const int idx = pos + lo;
+    // surviving pods before the departure: the largest s in [0, min(R, L)) with S[s] > u (0 if
+    // none), as the oracle's binary search finds it.  S[s] ~ (1 - p)^s 2^32, so s ~ log2(u 2^-32) /
+    // log2(1 - p): start there and step to the exact answer against the table (one or two
+    // independent table reads instead of ~log2 L dependent ones)
+    const int hi = min(R, v.n_skip) - 1;
+    int s = (int)fminf(fmaxf(__log2f((float)u * 0x1p-32f) * inv_lg1p, 0.f), (float)hi);
+    while (s > 0 && S[s] <= u) --s;
+    while (s < hi && S[s + 1] > u) ++s;
+    const int idx = pos + s;
     pos = idx + 1;
     // pod idx: its group, chunk, node
     for (;;) {
