@@ -494,8 +494,9 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   for (int net = 0; net < 2; ++net) {
     const int An = net == 0 ? A : 1;
     SfNet& n = w.n[net];
-    n.dz2t = (float*)take(4LL * M * HID);
+    n.dz2s = (_Float16*)take(4LL * M * HID);
     n.tile_edz = (int*)take(4LL * (M / 16));
+    n.tile_ex = (int*)take(4LL * (M / 16));
     n.part_w1 = (float*)take(4LL * w.blocks * HID * D);
     n.part_b1 = (float*)take(4LL * w.blocks * HID);
     n.part_w3 = (float*)take(4LL * w.blocks * An * HID);

@@ -38,8 +38,10 @@ struct SfNet {
   const _Float16 *w1h, *w1l, *w2ph, *w2pl, *w2th, *w2tl;
   const float* sc;
   unsigned* dzmax;
-  float* dz2t;    // [M/16 tiles][8 n-steps][64 lanes][8]: dZ2 in F1a's lane order (sgd_sf16.hip F1)
-  int* tile_edz;  // [M/16]: each 16-row tile's dZ2 split exponent (F1a -> F1b)
+  _Float16* dz2s;  // [M/16 tiles][8 n-steps][hi, lo][64 lanes][8]: dZ2 of each 16-row tile split at
+                  // 2^tile_edz, in F1a's lane order (sgd_sf16.hip F1)
+  int* tile_edz;  // [M/16]: each 16-row tile's dZ2 split exponent (F1a -> F1b, F2)
+  int* tile_ex;   // [M/16]: each 16-row tile's X split exponent (F1a -> F2)
   float *part_w1, *part_b1;                 // [F1 blocks of 128 rows][...] (F1b)
   float *part_w3, *part_b3, *part_stat;     // [F1 blocks of 128 rows][...] (F1a)
   float *part_w2, *part_b2;                                   // [splits][...]

@@ -42,7 +42,6 @@ using h4 = __attribute__((ext_vector_type(4))) _Float16;
 using v4u = __attribute__((ext_vector_type(4))) unsigned;  // 16-byte staging register (a vector, not HIP's uint4 struct, so it stays in VGPRs)
 
 constexpr int SF_ROWS = 256;        // minibatch rows must be a multiple of this
-constexpr int SF_CH = 8192;         // halves per staged chunk (per hi / lo array)
 constexpr float SF_H1_SCALE = 16384.f;  // tanh outputs (|h| < 1) scaled by 2^14
 // max |dZ2| of an SGD step as SF_DZ_SLOTS partial maxima, one 64-byte line apart: F1a waves update
 // the slot of (tile mod SF_DZ_SLOTS), F2 takes the max over them.  One address for all 4,096 tile
@@ -640,38 +639,54 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   }
   FA_STAMP(5);
 
-  // ---- dZ2^T = (dl W3) (1 - H2^2) -> HBM: [tile][s = nt >> 1][lane][4 (nt & 1) + i], i.e. each
-  // lane's eight values of an n-step are the A fragment F1b's same lane reads; the tile's max |dZ2|
+  // ---- dZ2^T = (dl W3) (1 - H2^2), in place of H2 in the accumulators; the tile's max |dZ2| -> its
+  // split exponent; dZ2 -> HBM split at that scale: [tile][s = nt >> 1][hi, lo][lane][4 (nt & 1) + i],
+  // i.e. each lane's eight values of an n-step are the A fragment F1b's same lane reads (pre-split:
+  // neither F1b nor F2 splits it again)
   float dmx = 0.f;
-  {
-    float* dst = N.dz2t + (size_t)tile * (16 * HID) + l * 8;
 #pragma unroll
-    for (int nt = 0; nt < 16; ++nt) {
-      const int n0 = 16 * nt + 4 * gq;
-      float gs[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int nt = 0; nt < 16; ++nt) {
+    const int n0 = 16 * nt + 4 * gq;
+    float gs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int a = 0; a < A_; ++a) {
-        const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
-        gs[0] = fmaf(dl[a], t.x, gs[0]);
-        gs[1] = fmaf(dl[a], t.y, gs[1]);
-        gs[2] = fmaf(dl[a], t.z, gs[2]);
-        gs[3] = fmaf(dl[a], t.w, gs[3]);
-      }
-      v4f dz;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float h2 = acc[nt][i];
-        dz[i] = gs[i] * (1.f - h2 * h2);
-        dmx = fmaxf(dmx, fabsf(dz[i]));
-      }
-      *reinterpret_cast<v4f*>(dst + (nt >> 1) * 512 + 4 * (nt & 1)) = dz;
-      if constexpr (A_ > 4) asm volatile("" ::: "memory");
+    for (int a = 0; a < A_; ++a) {
+      const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
+      gs[0] = fmaf(dl[a], t.x, gs[0]);
+      gs[1] = fmaf(dl[a], t.y, gs[1]);
+      gs[2] = fmaf(dl[a], t.z, gs[2]);
+      gs[3] = fmaf(dl[a], t.w, gs[3]);
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float h2 = acc[nt][i];
+      acc[nt][i] = gs[i] * (1.f - h2 * h2);
+      dmx = fmaxf(dmx, fabsf(acc[nt][i]));
+    }
+    if constexpr (A_ > 4) asm volatile("" ::: "memory");
   }
   dmx = wave_max(dmx);
+  const int edz = dmx > 0.f ? sf_exp(dmx) : 120;  // an all-zero tile: the largest exponent (F2 takes the min)
+  {
+    const float sdz = pow2(edz);
+    _Float16* dst = N.dz2s + (size_t)tile * (16 * HID * 2) + l * 8;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      h8 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        _Float16 a, b;
+        split1(acc[2 * st + (j >> 2)][j & 3] * sdz, a, b);
+        hi[j] = a;
+        lo[j] = b;
+      }
+      *reinterpret_cast<h8*>(dst + st * 1024) = hi;
+      *reinterpret_cast<h8*>(dst + st * 1024 + 512) = lo;
+    }
+  }
   if (l == 0) {
     atomicMax(dz_slot(N.dzmax, tile), __float_as_uint(dmx));
-    N.tile_edz[tile] = sf_exp(dmx);
+    N.tile_edz[tile] = edz;
+    N.tile_ex[tile] = ex;
   }
   FA_STAMP(6);
   // ---- workgroup sums (fixed wave order) -> this block's partials
@@ -721,14 +736,13 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1
   hc_dma<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
   w1_stage<KD, NTHR>(N, sW1, tid);
   const int edz = N.tile_edz[tile];
-  const float sdz = pow2(edz);
-  const float* dzp = N.dz2t + (size_t)tile * (16 * HID) + l * 8;
-  v4f d0 = *reinterpret_cast<const v4f*>(dzp), d1 = *reinterpret_cast<const v4f*>(dzp + 4);
+  const _Float16* dzp = N.dz2s + (size_t)tile * (16 * HID * 2) + l * 8;  // split by F1a at 2^edz
+  h8 dh = *reinterpret_cast<const h8*>(dzp), dl = *reinterpret_cast<const h8*>(dzp + 512);
   vm_drain();
   __syncthreads();
 
-  // ---- dH1 = dZ2 W2: 16 steps (n-step s, k-half ph) of 8 k-tiles x 3 MFMAs; the dZ2 fragment of
-  // n-step s is split at its first step and the next one loaded
+  // ---- dH1 = dZ2 W2: 16 steps (n-step s, k-half ph) of 8 k-tiles x 3 MFMAs; the (pre-split) dZ2
+  // fragment of n-step s taken at its first step and the next one loaded
   f4 acc[16];
 #pragma unroll
   for (int kt = 0; kt < 16; ++kt) acc[kt] = f4zero();
@@ -739,11 +753,11 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1
       const int st = 2 * s + ph;
       if (st < 15) hc_dma<W>(N.w2th, N.w2tl, 128 * (ph ^ 1), 32 * (s + ph), sCh + (ph ^ 1) * 2 * H16, w, l);
       if (ph == 0) {
-        const float dv[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
-        split8(dv, 0, sdz, ah, al);
+        ah = dh;
+        al = dl;
         if (s < 7) {
-          d0 = *reinterpret_cast<const v4f*>(dzp + (s + 1) * 512);
-          d1 = *reinterpret_cast<const v4f*>(dzp + (s + 1) * 512 + 4);
+          dh = *reinterpret_cast<const h8*>(dzp + (s + 1) * 1024);
+          dl = *reinterpret_cast<const h8*>(dzp + (s + 1) * 1024 + 512);
         }
       }
       const _Float16* buf = sCh + ph * 2 * H16;
@@ -824,6 +838,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 }
 
 // ----------------------------------------------------------------------------- F2
+// dW2 = dZ2^T H1 over a row range as a tiled split-fp16 GEMM: C [256 n][256 k] per workgroup (512
+// threads, 8 waves of 64 n x 128 k = 2 x 4 v_mfma_f32_32x32x16_f16 tiles: 128 accumulator registers,
+// two waves per SIMD), K = the rows, in chunks of 32, double-buffered in LDS:
+//   A = dZ2^T chunk: F1a's fp32 dZ2 (two 16-row tiles in its lane order), loaded into registers one
+//     chunk ahead, split with the step's max |dZ2| scale; db2 from the same loads;
+//   B = H1 chunk, produced by the workgroup: wave w forms Z1 = Xa W1a^T for the chunk's 32 rows and
+//     hidden units k = 32 w + 0..31 (v_mfma_f32_16x16x16_f16, X scaled by F1a's per-tile exponent),
+//     tanh, split at 2^14.
+// Chunk c + 1's operands are produced after chunk c's MFMAs are issued, in the same basic block (the
+// scheduler interleaves the two), into the other buffer; one barrier per chunk.  Round 2's F2 (eight
+// waves of 256 n x 32 k, H1 in registers) read every A fragment -> wait -> MFMA: 30% MFMA-busy
+// (profiles/r03c).  A 1,024-thread version of this kernel (64 x 64 per wave) spilled at its
+// 128-register budget, and each spill reload waited for the prefetches (vmcnt counts in issue order).
 typedef __fp16 hf4_t __attribute__((vector_size(8)));
 // ds_read_b64_tr_b16 (T10): per 16-lane group, 4 rows x 16 columns of 16-bit elements, lane i of
 // the group gets column i (row q in element q); EXEC must be all ones
@@ -831,213 +858,300 @@ __device__ __forceinline__ h4 tr_read(const _Float16* p) {
   const hf4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) hf4_t*)(p));
   return __builtin_bit_cast(h4, v);
 }
-// grid (splits, 2 nets), 512 threads; wave w owns dW2 columns k = 32w + r, all 256 rows n.
+#ifdef RLKS_STAMPS
+// diagnostic build only (tools/stamps.py): F2 phase cycles of lane 0 of every wave,
+// [net][split][wave][prologue, MFMA issue, production, barrier waits, epilogue, start]
+__device__ unsigned long long g_f2_stamps[2][128][16][6];
+#define F2_NOW() __builtin_amdgcn_s_memtime()
+#endif
+constexpr int F2_THREADS = 512;
+// LDS images (halves), per buffer: A = dZ2 chunk [plane hi, lo][32 m][F2_AROW] (n contiguous, rows
+// padded by 32 halves: the transposed fragment reads of 4 rows x 32 columns land on 4 disjoint
+// 16-bank windows without a swizzle), B = H1 chunk [plane][s 2][256 k][16] (16-byte piece h of row k
+// at slot h ^ ((k >> 3) & 1): conflict-free ds_read_b128).  Unswizzled along n, s and k-blocks, every
+// fragment address is one per-lane base plus immediates.
+constexpr int F2_AROW = HID + 32;
+constexpr int F2_APLANE = 32 * F2_AROW;
+constexpr int F2_BPLANE = 2 * HID * 16;
+constexpr int F2_BUF = 2 * F2_APLANE + 2 * F2_BPLANE;
+constexpr int F2_MAX_TILES = 2 * 256;  // 16-row tiles per F2 workgroup (tiles_per_split <= 256 chunks)
+
+// grid (splits, 2 nets) x 512 threads; split z covers 32-row chunks [z tps, (z + 1) tps).
+// dZ2 arrives split by F1a, each 16-row tile T at its own scale 2^e_T; the H1 rows of tile T are
+// split at 2^(14 + E - e_T), E = min over the workgroup's tiles, so that every product carries
+// 2^(14 + E) (unscaled at the end).  Production of chunk c + 1 (copy of its dZ2 pieces into the A
+// image, db2, and H1: wave w forms hidden units k = 32 w + 0..31) is shared by all eight waves and
+// placed ping-pong: per chunk c, phase 1 = {waves 0-3: MFMAs of c, 4-7: production}, phase 2 =
+// {0-3: production, 4-7: MFMAs of c}, a barrier after each, so that each SIMD's VALU work runs
+// beside its partner wave's MFMAs.
 template <int KD>
-__global__ __launch_bounds__(512) void k_sf_dw2(SfArgs g) {
+__global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
   constexpr int KS = KD / 16;
-  const int net = blockIdx.y;
-  const SfNet& N = g.n[net];
+  const SfNet& N = g.n[blockIdx.y];
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  _Float16* sA = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][32 m][HID n]
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  _Float16* sm = reinterpret_cast<_Float16*>(lds);  // [2 buf][F2_BUF]
+  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = l & 15, gq = l >> 4, wm = w >> 1, wn = w & 1, r = l & 31, h = l >> 5;
+  const bool first = w < 4;  // waves 0-3: MFMAs in phase 1; 4-7: in phase 2
   const int D = g.D, stride = g.x_stride;
   int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
   if (!dcheck(t1 <= g.M / 32, DC_SGD_TILE, t1)) t0 = t1 = 0;
+  const int nk = t1 - t0;
 
-  static_assert(SF_DZ_SLOTS == 64, "one max slot per lane");
-  // sg / unscale: from the step's max |dZ2|, read after the first tile's loads are in flight
-  float sg = 0.f, unscale = 0.f;
-  const float inv_w1 = N.sc[1];
-
-  h8 wh[KS], wl[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    wh[ks] = *reinterpret_cast<const h8*>(N.w1h + (32 * w + r) * KD + 16 * ks + 8 * h);
-    wl[ks] = *reinterpret_cast<const h8*>(N.w1l + (32 * w + r) * KD + 16 * ks + 8 * h);
+  // F1a's X and dZ2 exponents of the workgroup's 16-row tiles -> LDS (read per chunk from there, not
+  // by a global load among the prefetches); E = min e_T (F1a stores 120 for an all-zero tile)
+  int* sEx = reinterpret_cast<int*>(sm + 2 * F2_BUF);  // [2 (t1 - t0)] X exponents, then dZ2 exponents
+  int* sEd = sEx + F2_MAX_TILES;
+  int emin = 120;
+  for (int i = tid; i < 2 * nk; i += F2_THREADS) {
+    sEx[i] = N.tile_ex[2 * t0 + i];
+    const int e = N.tile_edz[2 * t0 + i];
+    sEd[i] = e;
+    emin = min(emin, e);
   }
+  __shared__ float s_emin[F2_THREADS / 64];
+  emin = (int)-wave_max((float)-emin);
+  if (l == 0) s_emin[w] = (float)emin;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < F2_THREADS / 64; ++i) emin = min(emin, (int)s_emin[i]);
+  const int E = __builtin_amdgcn_readfirstlane(emin);
+  const float unscale = pow2(-14 - E);
 
-  // db2 partial sums of the 8 rows n this thread's loads cover (two n-steps s, four n each)
-  float db2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  // dZ2 of 32-row tile t = F1a's 16-row tiles 2t, 2t + 1 in their lane-native order
-  // [T][s][lane (g, c)][8]: float4 f = tid + 512 i holds rows n = 32 s + 16 (f & 1) + 4 g + 0..3 of
-  // row m = 16 T + c, with T = f >> 10, s = (f >> 7) & 7, lane (f >> 1) & 63.  Staged through
-  // registers one tile ahead, split with the step's max |dZ2| scale and stored as an [m][n] image
-  // (32 rows of 256 halves, 8-byte quads of n at quad (n >> 2) ^ 8 (m & 3)) that the fragment reads
-  // transpose (ds_read_b64_tr_b16).
-  v4f dv[4];
-  auto load = [&](int t) {
+  // per-lane fragment bases (halves within a buffer):
+  //   A (transposed reads): lane 4 q + p of its 16-lane group addresses row 4 h + q (+ 16 s, + 8 for
+  //   the second read), columns 64 wm + 32 i + 16 ((l >> 4) & 1) + 4 p; K order of k-step s: rows
+  //   16 s + 8 (j >> 2) + 4 h + (j & 3) (the MFMA accumulator row order the B image follows)
+  //   B: column k = 128 wn + 32 j + r, piece h
+  const int abase = (4 * h + ((l & 15) >> 2)) * F2_AROW + 16 * ((l >> 4) & 1) + 4 * (l & 3) + 64 * wm;
+  const int bbase = 2 * F2_APLANE + (128 * wn + r) * 16 + 8 * (h ^ ((r >> 3) & 1));
+  f32x16 acc[2][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dv[i] = *reinterpret_cast<const v4f*>(N.dz2t + (size_t)t * HID * 32 + (size_t)(tid + 512 * i) * 4);
-  };
-  auto store = [&](int buf) {
-    _Float16* b = sA + buf * 2 * SF_CH;
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = tid + 512 * i, lf = (f >> 1) & 63;
-      const int m = 16 * (f >> 10) + (lf & 15), q0 = 8 * ((f >> 7) & 7) + 4 * (f & 1) + (lf >> 4);
-      const v4f v = dv[i];
-      h4 hi, lo;
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  auto mfma_chunk = [&](const _Float16* b) {  // A fragments of both i, then B one j at a time (24 registers)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      h8 ah[2], al[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const _Float16* pa = b + abase + s * 16 * F2_AROW + 32 * i;
+        const h4 a0 = tr_read(pa), a1 = tr_read(pa + 8 * F2_AROW);
+        const h4 c0 = tr_read(pa + F2_APLANE), c1 = tr_read(pa + F2_APLANE + 8 * F2_AROW);
+        ah[i] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+        al[i] = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        db2[(i & 1) * 4 + j] += v[j];
-        _Float16 a, bb;
-        split1(v[j] * sg, a, bb);
-        hi[j] = a;
-        lo[j] = bb;
-      }
-      const int off = m * HID + 4 * (q0 ^ (8 * (m & 3)));
-      *reinterpret_cast<h4*>(b + off) = hi;
-      *reinterpret_cast<h4*>(b + SF_CH + off) = lo;
-    }
-  };
-  // A fragment (32x32x16: row n = 32 nt + r, k = m of k-step s in the accumulator row order
-  // 16 s + 8 (j >> 2) + 4 h + (j & 3)): two transposed reads of 4 rows m x 16 columns n per 16-lane
-  // group; lane 4 q + p of the group addresses row m0 + q, columns n_base + 4 p .. + 3
-  const int tq = (l & 15) >> 2, tp = l & 3, tcol = 16 * ((l >> 4) & 1);
-  auto afrag = [&](const _Float16* b, int nt, int s, h8& fh, h8& fl) {
-    const int m0 = 16 * s + 4 * h + tq, qd = ((32 * nt + tcol) >> 2) + tp;
-    const int o0 = m0 * HID + 4 * (qd ^ (8 * tq)), o1 = o0 + 8 * HID;
-    const h4 a0 = tr_read(b + o0), a1 = tr_read(b + o1), c0 = tr_read(b + SF_CH + o0), c1 = tr_read(b + SF_CH + o1);
-    fh = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
-    fl = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-
-  f32x16 acc[8];
+        const _Float16* pb = b + bbase + s * HID * 16 + 32 * 16 * j;
+        const h8 bh = *reinterpret_cast<const h8*>(pb), bl = *reinterpret_cast<const h8*>(pb + F2_BPLANE);
 #pragma unroll
-  for (int nt = 0; nt < 8; ++nt)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
-
-  // X rows of the next tile are loaded one step ahead (their latency hides behind the MFMAs)
-  float xnext[KD == 16 ? KS * 8 : 1];
-  auto load_x = [&](int t) {
-    if constexpr (KD != 16) return;
-    const float* xr = g.x + (size_t)(t * 32 + r) * stride;
-    // exec-masked loads of the obs columns (measured faster here than xa_row8's vector loads)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int d = 8 * h + j;
-      xnext[j] = d < D ? xr[d] : (d == D ? 1.f : 0.f);
-    }
-  };
-  // H1 tile (rows m in registers, columns k = 32w + r on lanes) of tile tc's X rows, as the B
-  // operand.  Obs 6 / 12 (KD 16): the rows were loaded a step ahead into xnext, and tile tn's are
-  // loaded now; obs 24 (KD 32): loaded here (the prefetch registers would spill)
-  constexpr bool XPRE = KD == 16;
-  auto h1 = [&](int tc, int tn, h8 (&bh)[2], h8 (&bl)[2]) {
-    float xv[KS * 8];
-    if constexpr (XPRE) {
-#pragma unroll
-      for (int i = 0; i < KS * 8; ++i) xv[i] = xnext[i];
-      load_x(tn);
-    } else {
-      const float* xr = g.x + (size_t)(tc * 32 + r) * stride;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        float v[8];
-        xa_row8(xr, 16 * ks + 8 * h, D, stride, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv[ks * 8 + j] = v[j];
+        for (int i = 0; i < 2; ++i) acc[i][j] = mma3(ah[i], al[i], bh, bl, acc[i][j]);
       }
     }
-    float xm = 0.f;
+  };
+
+  // ---- dZ2 pieces: wave w takes n-step w of both 16-row tiles T2 and both planes (hi, lo): piece
+  // i = 2 T2 + plane of lane l holds halves j at row m = 16 T2 + c, columns n = 32 w + 16 (j >> 2) +
+  // 4 gq + (j & 3) (F1a's layout, loaded one chunk ahead).  (Buffer loads: an SGPR resource, the
+  // chunk offset in an SGPR and one 32-bit lane offset, instead of a 64-bit address pair per load,
+  // which cost the registers that made this kernel spill.)
+  const __amdgpu_buffer_rsrc_t dz_rsrc = __builtin_amdgcn_make_buffer_rsrc(N.dz2s, (short)0, 0x7fffffff, 0x00020000);
+  const int dz_lane = 2 * (w * 1024 + l * 8);  // bytes
+  h8 dp[4];
+  auto load_dz = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < KS * 8; ++i) xm = fmaxf(xm, fabsf(xv[i]));
-    const float sx = pow2(sf_exp(wave_max(xm)));
-    f32x16 z;
+    for (int i = 0; i < 4; ++i)
+      dp[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(
+                                         dz_rsrc, dz_lane, t * (32 * HID * 4) + (i >> 1) * (16 * HID * 4) + (i & 1) * 1024, 0));
+  };
+  float db2[8] = {};  // dZ2 of this lane's columns, summed over its rows
+  auto store_dz = [&](_Float16* img, float s0, float s1) {  // s0, s1: 2^-e of the two tiles (0: not counted)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const float sc = (i >> 1) ? s1 : s0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) db2[j] = fmaf((float)dp[i][j], sc, db2[j]);
+      const int off = (i & 1) * F2_APLANE + (16 * (i >> 1) + c) * F2_AROW + 32 * w + 4 * gq;
+      *reinterpret_cast<h4*>(img + off) = __builtin_shufflevector(dp[i], dp[i], 0, 1, 2, 3);
+      *reinterpret_cast<h4*>(img + off + 16) = __builtin_shufflevector(dp[i], dp[i], 4, 5, 6, 7);
+    }
+  };
+
+  // ---- H1: hidden units k = 32 w + 16 kt + c; Xa rows of a chunk (raw 16-byte pieces, the
+  // [X | 1 | 0] selects at use), F1a's X and dZ2 exponents of its two 16-row tiles, loaded a chunk ahead
+  h4 wh[2][KS], wl[2][KS];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      h8 a, b;
-      split8(xv, ks * 8, sx, a, b);
-      z = mma3(a, b, wh[ks], wl[ks], z);
+      wh[kt][ks] = *reinterpret_cast<const h4*>(N.w1h + (32 * w + 16 * kt + c) * KD + 16 * ks + 4 * gq);
+      wl[kt][ks] = *reinterpret_cast<const h4*>(N.w1l + (32 * w + 16 * kt + c) * KD + 16 * ks + 4 * gq);
     }
-    const float k_z1 = inv_w1 / sx * SF_2LOG2E;
+  const float inv_w1 = N.sc[1];
+  v4f xr[2][KS];
+  int2 xe, de;
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.x), (short)0, 0x7fffffff, 0x00020000);
+  auto load_x = [&](int t) {
+    xe = *reinterpret_cast<const int2*>(sEx + 2 * (t - t0));
+    de = *reinterpret_cast<const int2*>(sEd + 2 * (t - t0));
 #pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = fmaf(-2.f * SF_H1_SCALE, tanh_r(z[q] * k_z1), SF_H1_SCALE);
-    split16(z, 0, 1.f, bh[0], bl[0]);
-    split16(z, 8, 1.f, bh[1], bl[1]);
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int base = 16 * ks + 4 * gq, pb = base < stride - 4 ? base : stride - 4;
+        xr[mt][ks] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 x_rsrc, 4 * ((16 * mt + c) * stride + pb), 4 * t * 32 * stride, 0));
+      }
+  };
+  // Z1 rows m = 16 mt + 4 gq + i -> B image k-step mt, positions 8 (gq & 1) + 4 (gq >> 1) + i (bits
+  // 2 and 3 of m swapped)
+  const int hoff = 2 * F2_APLANE + (32 * w + c) * 16 + 8 * ((gq & 1) ^ ((c >> 3) & 1)) + 4 * (gq >> 1);
+  auto store_h1 = [&](_Float16* img) {
+    // X scale of the chunk from F1a's per-tile exponents (the larger max: the smaller exponent)
+    const int ex = min(xe.x, xe.y);
+    const float sx = pow2(ex), k_z1 = inv_w1 * pow2(-ex) * SF_2LOG2E;
+    h4 xh[2][KS], xl[2][KS];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int base = 16 * ks + 4 * gq;
+        const bool inrow = base < stride - 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int d = base + j;
+          _Float16 a, b;
+          split1(fmaf(xr[mt][ks][j], (d < D && inrow) ? sx : 0.f, d == D ? sx : 0.f), a, b);
+          xh[mt][ks][j] = a;
+          xl[mt][ks][j] = b;
+        }
+      }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      // rows of tile 2t + mt: H1 split at 2^(14 + E - e_T) (<= 2^14)
+      const float hs = pow2(14 + E - (mt ? de.y : de.x));
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        f4 z = f4zero();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) z = mk16x3(xh[mt][ks], xl[mt][ks], wh[kt][ks], wl[kt][ks], z);
+        h4 hh, hl;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          _Float16 a, b;
+          split1(fmaf(-2.f * hs, tanh_r(z[i] * k_z1), hs), a, b);
+          hh[i] = a;
+          hl[i] = b;
+        }
+        const int off = hoff + mt * HID * 16 + kt * 16 * 16;
+        *reinterpret_cast<h4*>(img + off) = hh;
+        *reinterpret_cast<h4*>(img + off + F2_BPLANE) = hl;
+      }
+    }
+  };
+  // production of the loaded chunk into img; counted: add its dZ2 to db2
+  auto produce = [&](_Float16* img, bool counted) {
+    const float s0 = counted ? pow2(-de.x) : 0.f, s1 = counted ? pow2(-de.y) : 0.f;
+    store_dz(img, s0, s1);
+    store_h1(img);
+  };
+  // barrier without __syncthreads()'s fence (which would wait for the prefetches in flight: s_waitcnt
+  // vmcnt(0)); the LDS stores need only lgkmcnt(0).  Scheduling barriers on both sides: the scheduler
+  // otherwise moves each phase's VALU into the other phase (e.g. the X split into the MFMA phase,
+  // where it waits for the X loads).
+  auto phase_barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
   };
 
-  // Software pipeline: step t runs tile t's 48 MFMAs and, in their shadow, splits tile t + 1's
-  // dZ2^T (loaded during step t - 1) into the other LDS buffer, loads tile t + 2's and computes
-  // tile t + 1's H1.  The VALU work of a step thus overlaps the same wave's MFMAs instead of
-  // following them: both waves of a SIMD meet at every barrier, so they cannot hide each
-  // other's VALU phases.
-  h8 bh[2], bl[2];
-  load(t0);
-  {  // lane i of every wave loads F1a's max slot i; one wave-wide max
-    const float mxg = wave_max(__uint_as_float(N.dzmax[(threadIdx.x & 63) * SF_DZ_STRIDE]));
-    sg = pow2(sf_exp(mxg));
-    unscale = 1.f / (sg * SF_H1_SCALE);
+#ifdef RLKS_STAMPS
+  unsigned long long ts0 = F2_NOW(), tph[5] = {0ull, 0ull, 0ull, 0ull, 0ull}, tq = ts0;
+#define F2_STAMP(i) { const unsigned long long tn = F2_NOW(); tph[i] += tn - tq; tq = tn; }
+#else
+#define F2_STAMP(i)
+#endif
+  if (nk > 0) {
+    load_dz(t0);
+    load_x(t0);
+    produce(sm, true);
+    load_dz(min(t0 + 1, t1 - 1));
+    load_x(min(t0 + 1, t1 - 1));
   }
-  store(0);
-  if (t0 + 1 < t1) load(t0 + 1);
-  if constexpr (XPRE) load_x(t0);
-  h1(t0, t0 + 1 < t1 ? t0 + 1 : t0, bh, bl);
   __syncthreads();
-  // Waves 4-7 share SIMDs with waves 0-3 (wave i runs on SIMD i mod 4) and run the same step
-  // with the VALU blocks moved (H1 first, the tile split late): the two waves of a SIMD are then
-  // in complementary phases between barriers, and one's VALU issues under the other's MFMAs.
-  auto step = [&](auto PH, int t) {
-    constexpr int ph = decltype(PH)::value;
-    constexpr int NT_STORE = ph ? 5 : 1, NT_LOAD = ph ? 6 : 3, NT_H1 = ph ? -1 : 4;
-    const int buf = (t - t0) & 1;
-    const bool more = t + 1 < t1;
-    const _Float16* b = sA + buf * 2 * SF_CH;
-    h8 nbh[2], nbl[2];
-    const int th = t + 2 < t1 ? t + 2 : t + 1 < t1 ? t + 1 : t;
-    const int tc = t + 1 < t1 ? t + 1 : t;
-    if (NT_H1 < 0) h1(tc, th, nbh, nbl);  // tile t + 1's H1
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        h8 ah, al;
-        afrag(b, nt, s, ah, al);
-        acc[nt] = mma3(ah, al, bh[s], bl[s], acc[nt]);
-      }
-      if (nt == NT_STORE && more) store(buf ^ 1);              // tile t + 1 -> other buffer
-      if (nt == NT_LOAD && t + 2 < t1) load(t + 2);            // tile t + 2 -> registers
-      if (nt == NT_H1) h1(tc, th, nbh, nbl);                   // tile t + 1's H1
+  F2_STAMP(0);
+  // (one loop per half, so that the phases' state stays in registers; the production runs at the last
+  // chunk too, redoing it into the idle buffer uncounted: unconditional, so that the compiler keeps
+  // the prefetches where they are)
+  if (first) {
+    for (int ci = 0; ci < nk; ++ci) {
+      mfma_chunk(sm + (ci & 1) * F2_BUF);
+      F2_STAMP(1);
+      phase_barrier();
+      F2_STAMP(3);
+      produce(sm + ((ci + 1) & 1) * F2_BUF, ci + 1 < nk);
+      load_x(min(t0 + ci + 2, t1 - 1));  // (before the dZ2 pieces: a spill reload for these
+      __builtin_amdgcn_sched_barrier(0);  // addresses would otherwise wait for them)
+      load_dz(min(t0 + ci + 2, t1 - 1));
+      F2_STAMP(2);
+      phase_barrier();
+      F2_STAMP(3);
     }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) { bh[s] = nbh[s]; bl[s] = nbl[s]; }
-    __syncthreads();
-  };
-  if (KD == 16 && (w & 4))
-    for (int t = t0; t < t1; ++t) step(std::integral_constant<int, 1>{}, t);
-  else
-    for (int t = t0; t < t1; ++t) step(std::integral_constant<int, 0>{}, t);
+  } else {
+    for (int ci = 0; ci < nk; ++ci) {
+      produce(sm + ((ci + 1) & 1) * F2_BUF, ci + 1 < nk);
+      load_x(min(t0 + ci + 2, t1 - 1));  // (before the dZ2 pieces: a spill reload for these
+      __builtin_amdgcn_sched_barrier(0);  // addresses would otherwise wait for them)
+      load_dz(min(t0 + ci + 2, t1 - 1));
+      F2_STAMP(2);
+      phase_barrier();
+      F2_STAMP(3);
+      mfma_chunk(sm + (ci & 1) * F2_BUF);
+      F2_STAMP(1);
+      phase_barrier();
+      F2_STAMP(3);
+    }
+  }
+#undef F2_STAMP
+
   float* out = N.part_w2 + (size_t)blockIdx.x * SF_W2_PSTRIDE;
 #pragma unroll
-  for (int nt = 0; nt < 8; ++nt)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) out[(size_t)(32 * nt + acc_row(q, l)) * HID + 32 * w + r] = acc[nt][q] * unscale;
-  // db2: the 16 lanes c = (tid >> 1) & 15 of a wave hold the same rows n = 32 s + 16 (tid & 1) +
-  // 4 ((tid >> 5) & 3) + j, s = (tid >> 7) + 4 (i & 1)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float v = db2[k];
-    v += __shfl_xor(v, 2, 64);
-    v += __shfl_xor(v, 4, 64);
-    v += __shfl_xor(v, 8, 64);
-    v += __shfl_xor(v, 16, 64);
-    db2[k] = v;
+      for (int q = 0; q < 16; ++q)
+        out[(size_t)(64 * wm + 32 * i + acc_row(q, l)) * HID + 128 * wn + 32 * j + r] = acc[i][j][q] * unscale;
+  // db2: sum over the 16 lanes c of the same n
+#pragma unroll
+  for (int j = 0; j < 8; ++j) db2[j] = row_sum16(db2[j]);
+  if (c == 0)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) N.part_b2[(size_t)blockIdx.x * HID + 32 * w + 16 * (j >> 2) + 4 * gq + (j & 3)] = db2[j];
+#ifdef RLKS_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tph[4] = F2_NOW() - tq;
+  if (l == 0 && blockIdx.x < 128) {
+    unsigned long long* o = g_f2_stamps[blockIdx.y][blockIdx.x][w];
+    for (int i = 0; i < 5; ++i) o[i] = tph[i];
+    o[5] = ts0;
   }
-  if (((tid >> 1) & 15) == 0)
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      N.part_b2[(size_t)blockIdx.x * HID + 32 * ((tid >> 7) + 4 * (k >> 2)) + 16 * (tid & 1) + 4 * ((tid >> 5) & 3) +
-                (k & 3)] = db2[k];
+#endif
 }
 
 // ----------------------------------------------------------------------------- launchers
 #ifdef RLKS_STAMPS
 extern "C" int rlks_dbg_fa_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fa_stamps), sizeof(g_fa_stamps)) == hipSuccess ? 0 : 1;
+}
+extern "C" int rlks_dbg_f2_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_f2_stamps), sizeof(g_f2_stamps)) == hipSuccess ? 0 : 1;
 }
 #endif
 
@@ -1082,9 +1196,10 @@ int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int 
 }
 
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {
-  const size_t lds = (size_t)2 * 2 * SF_CH * sizeof(_Float16);
-  if (sf_kd(a.D) == 16) hipLaunchKernelGGL(k_sf_dw2<16>, dim3(splits, 2), dim3(512), lds, s, a);
-  else hipLaunchKernelGGL(k_sf_dw2<32>, dim3(splits, 2), dim3(512), lds, s, a);
+  RLKS_REQUIRE(a.tiles_per_split <= F2_MAX_TILES / 2, RLKS_ERR_ARG, "split-fp16 F2: too many row chunks per split");
+  const size_t lds = (size_t)2 * F2_BUF * sizeof(_Float16) + 2 * F2_MAX_TILES * sizeof(int);  // 140 KB
+  if (sf_kd(a.D) == 16) hipLaunchKernelGGL(k_sf_dw2<16>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+  else hipLaunchKernelGGL(k_sf_dw2<32>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Phase timing of the split-fp16 F1a kernel (k_sf_fwd) from in-kernel s_memtime stamps (diagnostic build).
+"""Phase timing of the split-fp16 F1a (k_sf_fwd) and F2 (k_sf_dw2) kernels from in-kernel s_memtime stamps (diagnostic build).
 
   make -C rl-k8s-scheduler_amd/csrc stamps
   RLKS_LIB=rl-k8s-scheduler_amd/rlks/librlks_stamps.so python tools/stamps.py
@@ -82,6 +82,20 @@ def fwd_report(lib, tiles):
     print("first 12 waves (start, end, simd key):", [(int(start[i]), int(end[i]), int(k[i])) for i in order[:12]])
 
 
+def f2_report(lib):
+    """F2 (k_sf_dw2) per-wave phase cycles summed over its chunks (waves 0-7 of each workgroup)"""
+    st = np.zeros((2, 128, 16, 6), np.uint64)
+    assert lib.rlks_dbg_f2_stamps(st.ctypes.data_as(C.c_void_p)) == 0
+    names = ["prologue", "MFMA issue", "production", "barrier waits", "epilogue"]
+    for net in range(2):
+        for ws, who in ((slice(0, 4), "waves 0-3 (H1)"), (slice(4, 8), "waves 4-7 (dZ2)")):
+            s = st[net, :, ws, :5].astype(np.int64)
+            tot = s.sum(-1)
+            print(f"F2 net {net} {who}: wave lifetime median {np.median(tot):.0f} cyc (p90 {np.percentile(tot, 90):.0f})")
+            for i, n in enumerate(names):
+                print(f"  {n:16s} median {np.median(s[..., i]):8.0f}  p90 {np.percentile(s[..., i], 90):8.0f}")
+
+
 def main():
     if "--roll" in sys.argv:
         return roll()
@@ -115,6 +129,7 @@ def main():
                   rows, grad.data_ptr(), None, ws.data_ptr(), ws.numel(), None)
     torch.cuda.synchronize()
     fwd_report(_lib.lib(), rows // 16)  # F1a (k_sf_fwd) phases, one wave per 16-row tile
+    f2_report(_lib.lib())
 
 if __name__ == "__main__":
     main()
