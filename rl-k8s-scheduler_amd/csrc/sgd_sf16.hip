@@ -867,7 +867,7 @@ __device__ unsigned long long g_f2_stamps[2][128][16][6];
 constexpr int F2_THREADS = 512;
 // LDS images (halves), per buffer: A = dZ2 chunk [plane hi, lo][32 m][F2_AROW] (n contiguous, rows
 // padded by 32 halves: the transposed fragment reads of 4 rows x 32 columns land on 4 disjoint
-// 16-bank windows without a swizzle), B = H1 chunk [plane][s 2][256 k][16] (16-byte piece h of row k
+// 16-bank windows; 8-byte quads XOR 2 ((m >> 2) & 3) within each 32-column block for the stores), B = H1 chunk [plane][s 2][256 k][16] (16-byte piece h of row k
 // at slot h ^ ((k >> 3) & 1): conflict-free ds_read_b128).  Unswizzled along n, s and k-blocks, every
 // fragment address is one per-lane base plus immediates.
 constexpr int F2_AROW = HID + 32;
@@ -923,7 +923,12 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
   //   the second read), columns 64 wm + 32 i + 16 ((l >> 4) & 1) + 4 p; K order of k-step s: rows
   //   16 s + 8 (j >> 2) + 4 h + (j & 3) (the MFMA accumulator row order the B image follows)
   //   B: column k = 128 wn + 32 j + r, piece h
-  const int abase = (4 * h + ((l & 15) >> 2)) * F2_AROW + 16 * ((l >> 4) & 1) + 4 * (l & 3) + 64 * wm;
+  //   (A image quads XOR-swizzled by 2 ((m >> 2) & 3): the 4 rows of a transposed read share one XOR,
+  //   and the dZ2 stores of 16 consecutive rows spread over all banks; profiles/r03k: 20% of CU cycles
+  //   were LDS bank conflicts without it)
+  const int aq = (4 * ((l >> 4) & 1) + (l & 3)) ^ (2 * h);  // quad within the 8-quad block, rows 4 h + q
+  const int abase = (4 * h + ((l & 15) >> 2)) * F2_AROW + 4 * aq + 64 * wm;
+  const int abase8 = (4 * h + ((l & 15) >> 2) + 8) * F2_AROW + 4 * (aq ^ 4) + 64 * wm;  // rows + 8
   const int bbase = 2 * F2_APLANE + (128 * wn + r) * 16 + 8 * (h ^ ((r >> 3) & 1));
   f32x16 acc[2][4];
 #pragma unroll
@@ -939,8 +944,9 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const _Float16* pa = b + abase + s * 16 * F2_AROW + 32 * i;
-        const h4 a0 = tr_read(pa), a1 = tr_read(pa + 8 * F2_AROW);
-        const h4 c0 = tr_read(pa + F2_APLANE), c1 = tr_read(pa + F2_APLANE + 8 * F2_AROW);
+        const _Float16* pa8 = b + abase8 + s * 16 * F2_AROW + 32 * i;
+        const h4 a0 = tr_read(pa), a1 = tr_read(pa8);
+        const h4 c0 = tr_read(pa + F2_APLANE), c1 = tr_read(pa8 + F2_APLANE);
         ah[i] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
         al[i] = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
       }
@@ -975,9 +981,11 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
       const float sc = (i >> 1) ? s1 : s0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) db2[j] = fmaf((float)dp[i][j], sc, db2[j]);
-      const int off = (i & 1) * F2_APLANE + (16 * (i >> 1) + c) * F2_AROW + 32 * w + 4 * gq;
-      *reinterpret_cast<h4*>(img + off) = __builtin_shufflevector(dp[i], dp[i], 0, 1, 2, 3);
-      *reinterpret_cast<h4*>(img + off + 16) = __builtin_shufflevector(dp[i], dp[i], 4, 5, 6, 7);
+      // quads 8 w + gq and 8 w + gq + 4 of row m = 16 T2 + c, XOR 2 ((m >> 2) & 3)
+      const int off = (i & 1) * F2_APLANE + (16 * (i >> 1) + c) * F2_AROW + 32 * w;
+      const int sw = 2 * ((c >> 2) & 3);
+      *reinterpret_cast<h4*>(img + off + 4 * (gq ^ sw)) = __builtin_shufflevector(dp[i], dp[i], 0, 1, 2, 3);
+      *reinterpret_cast<h4*>(img + off + 4 * ((gq + 4) ^ sw)) = __builtin_shufflevector(dp[i], dp[i], 4, 5, 6, 7);
     }
   };
 

@@ -22,7 +22,11 @@ def main():
     fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE"), per_kernel(sys.argv[2], "WRITE_SIZE")
     dst = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
     out = json.load(open(dst))
-    for k, f in fetch.items():
+    # the stationary-churn launch: the survival table read through L2 (k_node_step_ec<false>); the
+    # heavy-churn leg stages it in LDS (<true>)
+    keep = [k for k in fetch if "<false>" in k] or list(fetch)
+    for k in keep[:1]:
+        f = fetch[k]
         key = "k_node_step"
         rd, wr = f * 1024 * 2, write.get(k, 0.0) * 1024
         out[key] = {"kernel": k, "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,

@@ -23,7 +23,7 @@ def main():
                 out[bench_name] = {"kernel": k, "hbm_read_bytes": d["hbm_read_bytes_corrected"],
                                    "hbm_write_bytes": d["hbm_write_bytes"],
                                    "hbm_bytes_per_launch": d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"],
-                                   "avg_us": d.get("avg_ns", 0) / 1e3}
+                                   "avg_us": d.get("avg_us", d.get("avg_ns", 0) / 1e3)}
                 break
     dst = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
     json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
