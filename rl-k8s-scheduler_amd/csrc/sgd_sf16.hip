@@ -886,7 +886,6 @@ constexpr int F2_MAX_TILES = 2 * 256;  // 16-row tiles per F2 workgroup (tiles_p
 // beside its partner wave's MFMAs.
 template <int KD>
 __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
-  constexpr int KS = KD / 16;
   const SfNet& N = g.n[blockIdx.y];
   extern __shared__ __attribute__((aligned(16))) float lds[];
   _Float16* sm = reinterpret_cast<_Float16*>(lds);  // [2 buf][F2_BUF]
@@ -989,80 +988,85 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
     }
   };
 
-  // ---- H1: hidden units k = 32 w + 16 kt + c; Xa rows of a chunk (raw 16-byte pieces, the
-  // [X | 1 | 0] selects at use), F1a's X and dZ2 exponents of its two 16-row tiles, loaded a chunk ahead
-  h4 wh[2][KS], wl[2][KS];
+  // ---- H1 of a chunk as one 32 x 32 block per wave: Z1 (rows m of the chunk, hidden units k =
+  // 32 w + (l & 31)) = Xa W1a^T on v_mfma_f32_32x32x8_f16, K = 8 columns of Xa = [X | 1 | 0] per MFMA
+  // (D + 1 = 7 at 2 actions: one K step, no padding), three products; B = W1a rows k (loaded once),
+  // A = the chunk's X rows (one 16-byte piece per lane and K step, loaded a chunk ahead, the selects
+  // at use); F1a's X and dZ2 exponents of its two 16-row tiles, loaded a chunk ahead
+  constexpr int KB = KD / 8;
+  const int kh = 32 * w + r;  // this lane's hidden unit
+  // (at KD = 32 the fragments are reloaded at every production, ahead of the dZ2 pieces: kept for
+  // the whole kernel they make it spill)
+  h4 wh[KB], wl[KB];
+  auto load_w1 = [&]() {
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      wh[kt][ks] = *reinterpret_cast<const h4*>(N.w1h + (32 * w + 16 * kt + c) * KD + 16 * ks + 4 * gq);
-      wl[kt][ks] = *reinterpret_cast<const h4*>(N.w1l + (32 * w + 16 * kt + c) * KD + 16 * ks + 4 * gq);
+    for (int kb = 0; kb < KB; ++kb) {
+      wh[kb] = *reinterpret_cast<const h4*>(N.w1h + kh * KD + 8 * kb + 4 * h);
+      wl[kb] = *reinterpret_cast<const h4*>(N.w1l + kh * KD + 8 * kb + 4 * h);
     }
+  };
+  if constexpr (KB <= 2) load_w1();
   const float inv_w1 = N.sc[1];
-  v4f xr[2][KS];
+  v4f xr[KB];
   int2 xe, de;
   const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.x), (short)0, 0x7fffffff, 0x00020000);
   auto load_x = [&](int t) {
     xe = *reinterpret_cast<const int2*>(sEx + 2 * (t - t0));
     de = *reinterpret_cast<const int2*>(sEd + 2 * (t - t0));
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int base = 16 * ks + 4 * gq, pb = base < stride - 4 ? base : stride - 4;
-        xr[mt][ks] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 x_rsrc, 4 * ((16 * mt + c) * stride + pb), 4 * t * 32 * stride, 0));
-      }
+    for (int kb = 0; kb < KB; ++kb) {
+      const int base = 8 * kb + 4 * h, pb = base < stride - 4 ? base : stride - 4;
+      xr[kb] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(x_rsrc, 4 * (r * stride + pb), 4 * t * 32 * stride, 0));
+    }
   };
-  // Z1 rows m = 16 mt + 4 gq + i -> B image k-step mt, positions 8 (gq & 1) + 4 (gq >> 1) + i (bits
-  // 2 and 3 of m swapped)
-  const int hoff = 2 * F2_APLANE + (32 * w + c) * 16 + 8 * ((gq & 1) ^ ((c >> 3) & 1)) + 4 * (gq >> 1);
+  // Z1 row m = acc_row(q) -> B image k-step m >> 4, position 8 h + 4 (q >> 2 & 1) + (q & 3) (bits 2 and 3
+  // of m swapped), hidden unit kh (16-byte piece h at slot h ^ ((kh >> 3) & 1))
+  const int hoff = 2 * F2_APLANE + kh * 16 + 8 * (h ^ ((kh >> 3) & 1));
   auto store_h1 = [&](_Float16* img) {
     // X scale of the chunk from F1a's per-tile exponents (the larger max: the smaller exponent)
     const int ex = min(xe.x, xe.y);
     const float sx = pow2(ex), k_z1 = inv_w1 * pow2(-ex) * SF_2LOG2E;
-    h4 xh[2][KS], xl[2][KS];
+    f32x16 z;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int q = 0; q < 16; ++q) z[q] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int base = 16 * ks + 4 * gq;
-        const bool inrow = base < stride - 4;
+    for (int kb = 0; kb < KB; ++kb) {
+      const int base = 8 * kb + 4 * h;
+      const bool inrow = base < stride - 4;
+      h4 xh, xl;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int d = base + j;
-          _Float16 a, b;
-          split1(fmaf(xr[mt][ks][j], (d < D && inrow) ? sx : 0.f, d == D ? sx : 0.f), a, b);
-          xh[mt][ks][j] = a;
-          xl[mt][ks][j] = b;
-        }
+      for (int j = 0; j < 4; ++j) {
+        const int d = base + j;
+        _Float16 a, b;
+        split1(fmaf(xr[kb][j], (d < D && inrow) ? sx : 0.f, d == D ? sx : 0.f), a, b);
+        xh[j] = a;
+        xl[j] = b;
       }
+      z = __builtin_amdgcn_mfma_f32_32x32x8f16(xl, wh[kb], z, 0, 0, 0);
+      z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wl[kb], z, 0, 0, 0);
+      z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wh[kb], z, 0, 0, 0);
+    }
+    // rows of tile 2t + (q >> 3): H1 split at 2^(14 + E - e_T) (<= 2^14)
+    const float hs0 = pow2(14 + E - de.x), hs1 = pow2(14 + E - de.y);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      // rows of tile 2t + mt: H1 split at 2^(14 + E - e_T) (<= 2^14)
-      const float hs = pow2(14 + E - (mt ? de.y : de.x));
+    for (int i = 0; i < 4; ++i) {
+      const float hs = i < 2 ? hs0 : hs1;
+      h4 hh, hl;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        f4 z = f4zero();
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) z = mk16x3(xh[mt][ks], xl[mt][ks], wh[kt][ks], wl[kt][ks], z);
-        h4 hh, hl;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          _Float16 a, b;
-          split1(fmaf(-2.f * hs, tanh_r(z[i] * k_z1), hs), a, b);
-          hh[i] = a;
-          hl[i] = b;
-        }
-        const int off = hoff + mt * HID * 16 + kt * 16 * 16;
-        *reinterpret_cast<h4*>(img + off) = hh;
-        *reinterpret_cast<h4*>(img + off + F2_BPLANE) = hl;
+      for (int j = 0; j < 4; ++j) {
+        _Float16 a, b;
+        split1(fmaf(-2.f * hs, tanh_r(z[4 * i + j] * k_z1), hs), a, b);
+        hh[j] = a;
+        hl[j] = b;
       }
+      const int off = hoff + (i >> 1) * HID * 16 + 4 * (i & 1);
+      *reinterpret_cast<h4*>(img + off) = hh;
+      *reinterpret_cast<h4*>(img + off + F2_BPLANE) = hl;
     }
   };
   // production of the loaded chunk into img; counted: add its dZ2 to db2
   auto produce = [&](_Float16* img, bool counted) {
+    if constexpr (KB > 2) load_w1();
     const float s0 = counted ? pow2(-de.x) : 0.f, s1 = counted ? pow2(-de.y) : 0.f;
     store_dz(img, s0, s1);
     store_h1(img);
