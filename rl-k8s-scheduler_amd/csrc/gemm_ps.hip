@@ -90,7 +90,19 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   _Float16* sm = reinterpret_cast<_Float16*>(lds);  // [2 buf][A hi, A lo, B hi, B lo][PCH]
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), r = l & 31;
   const int wm = w >> 2, wn = w & 3;
-  const int n0 = blockIdx.x * PT, m0 = blockIdx.y * PT;
+  // XCD-aware tile order (no split-K): workgroups are dealt round-robin over the 8 XCDs in dispatch
+  // order (x fastest), so dispatch slot b runs on XCD b % 8.  Give XCD j the tiles [j T/8, (j + 1) T/8)
+  // in row-major order (n fastest): an XCD's concurrent workgroups then cover a few M row blocks with
+  // all their N tiles, and each A row block (the large operand: M x K planes, 512 MB at c5) comes from
+  // HBM once into that XCD's L2 instead of once per N tile into every XCD.
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (gridDim.z == 1 && ((gridDim.x * gridDim.y) & 7) == 0) {
+    const int T = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
+    const int t = (b & 7) * (T >> 3) + (b >> 3);
+    bx = t % gridDim.x;
+    by = t / gridDim.x;
+  }
+  const int n0 = bx * PT, m0 = by * PT;
   const int ea = op_exp(g.a), eb = op_exp(g.b);
   const float unscale = ldexpf(1.f, -ea - eb);
   // this workgroup's K range (split-K: layer z)

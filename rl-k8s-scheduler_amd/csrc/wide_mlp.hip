@@ -194,6 +194,76 @@ __global__ void k_wide_sample(EnvView v, const float* __restrict__ logits, int A
   logp[m] = lg[act] - mx - logf(se);
 }
 
+// dZ2 = (dout W3) (1 - H2^2), K = the head's outputs (64 / 1): too short a reduction for the split
+// GEMM's K pipeline (its tile prologue and epilogue were the whole 0.71 ms), so plain fp32 FMAs in k
+// order on 64-row x 256-column tiles: dout^T and W3 tiles in LDS (K chunks of 32), 8 x 8 outputs per
+// thread, H2 read and dZ2 written as float4 rows; max |dZ2| -> slot (one atomic per block)
+constexpr int DZ_ROWS = 64, DZ_COLS = 256, DZ_K = 32;
+__global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout, const float* __restrict__ w3,
+                                                  const float* __restrict__ h2, float* __restrict__ dz, int M, int H,
+                                                  int K, unsigned* __restrict__ cmax_slot) {
+  __shared__ __attribute__((aligned(16))) float sA[DZ_K][DZ_ROWS + 4];  // dout^T chunk (padded: the transposing stores)
+  __shared__ __attribute__((aligned(16))) float sB[DZ_K][DZ_COLS];  // W3 chunk
+  const int tid = threadIdx.x, cg = tid & 31, rg = tid >> 5;
+  const int m0 = blockIdx.y * DZ_ROWS, n0 = blockIdx.x * DZ_COLS;
+  float acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+  for (int k0 = 0; k0 < K; k0 += DZ_K) {
+    const int kn = min(DZ_K, K - k0);
+    __syncthreads();
+    for (int e = tid; e < DZ_K * DZ_ROWS; e += 256) {  // e = r * DZ_K + k: coalesced along k
+      const int r = e / DZ_K, k = e - r * DZ_K, m = m0 + r;
+      sA[k][r] = (k < kn && m < M) ? dout[(size_t)m * K + k0 + k] : 0.f;
+    }
+    for (int e = tid; e < DZ_K * DZ_COLS / 4; e += 256) {
+      const int k = e / (DZ_COLS / 4), c4 = 4 * (e - k * (DZ_COLS / 4));
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < kn && n0 + c4 < H) v = *reinterpret_cast<const float4*>(w3 + (size_t)(k0 + k) * H + n0 + c4);
+      *reinterpret_cast<float4*>(&sB[k][c4]) = v;
+    }
+    __syncthreads();
+    for (int k = 0; k < kn; ++k) {
+      const float4 a0 = *reinterpret_cast<const float4*>(&sA[k][8 * rg]), a1 = *reinterpret_cast<const float4*>(&sA[k][8 * rg + 4]);
+      const float4 b0 = *reinterpret_cast<const float4*>(&sB[k][8 * cg]), b1 = *reinterpret_cast<const float4*>(&sB[k][8 * cg + 4]);
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+    }
+  }
+  float mx = 0.f;
+  const int n = n0 + 8 * cg;
+  if (n < H) {  // H % 8 == 0 (host check)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + 8 * rg + i;
+      if (m >= M) break;
+      const float4* hp = reinterpret_cast<const float4*>(h2 + (size_t)m * H + n);
+      const float4 g0 = hp[0], g1 = hp[1];
+      const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = acc[i][j] * (1.f - gv[j] * gv[j]);
+        mx = fmaxf(mx, fabsf(o[j]));
+      }
+      float4* dp = reinterpret_cast<float4*>(dz + (size_t)m * H + n);
+      dp[0] = make_float4(o[0], o[1], o[2], o[3]);
+      dp[1] = make_float4(o[4], o[5], o[6], o[7]);
+    }
+  }
+  mx = wave_max(mx);
+  __shared__ float red[4];
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  if (tid == 0) atomicMax(cmax_slot, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
 // ----------------------------------------------------------------------------- host
 namespace {
 
@@ -305,9 +375,10 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
       return rc;
     if (int rc = launch_colsum(n.dout, M, An, An, g + o[5], 0, w.part, s)) return rc;
     // dZ2 = (dout W3) (1 - H2^2); dW2 = dZ2^T H1; db2
-    if (int rc = gemm(n.dout, An, 0, P.w3, H, 0, w.dza, H, M, H, An, GEMM_DTANH, nullptr, n.h2, H, sl + SL_DOUT,
-                      sl + SL_W3, sl + SL_DZ2, s))
-      return rc;
+    RLKS_REQUIRE(H % 8 == 0, RLKS_ERR_UNSUPPORTED, "wide path: hidden width must be a multiple of 8");
+    hipLaunchKernelGGL(k_wide_dz2, dim3(cdiv(H, DZ_COLS), cdiv(M, DZ_ROWS)), dim3(256), 0, s, n.dout, P.w3, n.h2, w.dza, M,
+                       H, An, sl + SL_DZ2);
+    RLKS_LAUNCHED();
     if (int rc = launch_split_planes(w.dza, M, H, H, sl + SL_DZ2, 0, w.dzh, w.dzl, H, s)) return rc;
     {  // dW2[n][k] = sum_m dZ2[m][n] H1[m][k]: both operands K-major planes, split over the rows
       PsArgs a{};
