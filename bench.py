@@ -356,6 +356,30 @@ def cpu_threads() -> int:
     return max(1, min(n, int(omp))) if omp.isdigit() else max(1, n)
 
 
+def mfma_calibration(torch, sf16_tflops):
+    """what this chip's f16 MFMA pipes deliver on a large plain GEMM through the vendor library
+    (torch.matmul -> hipBLASLt, f16 65536 x 2048 x 2048, random data), measured live after the timed
+    region, against the dominant kernel's f16 MFMA rate (3 f16 products per fp32-accurate FLOP).  The
+    2.5 PF spec is not held under dense MFMA load (MI355X_MICROARCH.md, DVFS give-back)."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    a = torch.randn(65536, 2048, device=dev, dtype=torch.float16)
+    b = torch.randn(2048, 2048, device=dev, dtype=torch.float16)
+    for _ in range(3):
+        c = a @ b
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        c = a @ b
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    lib = 2 * 65536 * 2048 * 2048 / (ms * 1e-3) / 1e12
+    del a, b, c
+    return {"hipblaslt_f16_tflops": lib, "shape": "f16 65536x2048x2048 (torch.matmul)",
+            "kernel_f16_mfma_tflops": 3 * sf16_tflops, "frac_of_hipblaslt": 3 * sf16_tflops / lib}
+
+
 def pmc_traffic():
     """per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC summary, if any"""
     p = ROOT / "profiles" / "pmc_traffic.json"
@@ -454,6 +478,8 @@ def main():
                                        "split-fp16: 2.5 PF dense f16 MFMA / 3 products per fp32-accurate FLOP")}
             if dom == "wide_grad":
                 roofline["note"] = "generic-width path: the whole SGD-step gradient (a sequence of split-fp16 GEMM launches)"
+            if algo.precision != "fp32" and not args.no_kernel_timing:
+                roofline["calibration"] = mfma_calibration(torch, k["tflops"])
             pmc = pmc_traffic()
             ab = algo_bytes_per_launch(dom, algo.mb, algo.D, algo.H, algo.A)
             roofline["algorithmic_bytes_per_launch"] = ab

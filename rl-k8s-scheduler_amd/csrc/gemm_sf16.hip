@@ -290,20 +290,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int rows, int cols, int ld,
                                                 unsigned* __restrict__ slot, int flat4) {
   float mx = 0.f;
-  if (flat4) {
-    const size_t n4 = (size_t)rows * cols / 4;
-    const float4* x4 = reinterpret_cast<const float4*>(x);
+  if (flat4) {  // float4 pieces: of the whole array (ld == cols) or of each row (flat4 == 2: ld, cols % 4 == 0)
+    const int c4 = cols / 4;
+    const size_t n4 = (size_t)rows * c4;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
-      const float4 v = x4[i];
+      size_t e = i;
+      if (flat4 == 2) {
+        const size_t rr = i / c4;
+        e = rr * (ld / 4) + (i - rr * c4);
+      }
+      const float4 v = reinterpret_cast<const float4*>(x)[e];
       mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
   } else {
     for (int rr = blockIdx.x; rr < rows; rr += gridDim.x)
       for (int cc = threadIdx.x; cc < cols; cc += 256) mx = fmaxf(mx, fabsf(x[(size_t)rr * ld + cc]));
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(slot, __float_as_uint(mx));
+  // one atomic per block (single-address atomics serialise at their L2 channel)
+  __shared__ float red[4];
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(slot, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 // column sums of a [rows][cols] matrix over the row range of layer blockIdx.y (rows_per rows):
@@ -402,7 +410,8 @@ int launch_gemm_sf16(const GemmArgs& a, hipStream_t s) {
 
 int launch_absmax(const float* x, int rows, int cols, int ld, unsigned* slot, hipStream_t s) {
   const size_t n = (size_t)rows * cols;
-  const int flat4 = ld == cols && n % 4 == 0 && ((uintptr_t)x & 15) == 0;
+  const bool al = ((uintptr_t)x & 15) == 0;
+  const int flat4 = (ld == cols && n % 4 == 0 && al) ? 1 : (ld % 4 == 0 && cols % 4 == 0 && al) ? 2 : 0;
   const size_t units = flat4 ? (n / 4 + 255) / 256 : (size_t)rows;
   const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(2048, units));
   hipLaunchKernelGGL(k_absmax, dim3(blocks), dim3(256), 0, s, x, rows, cols, ld, slot, flat4);

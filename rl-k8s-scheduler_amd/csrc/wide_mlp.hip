@@ -8,7 +8,7 @@
 //
 // Per net and SGD step (M minibatch rows; W1 [H][D], W2 [H][H], W3 [A][H] torch layouts):
 //   H1 = tanh(X W1^T + b1)   H2 = tanh(H1 W2^T + b2)   out = H2 W3^T + b3          (NT GEMMs)
-//   k_wide_loss: dout [M][A] (+ per-block loss stats)
+//   k_wide_loss_pi / _vf: dout [M][A] (+ per-block loss stats)
 //   dW3 = dout^T H2 (TN)   db3 = colsum(dout)
 //   dZ2 = (dout W3) * (1 - H2^2) (NN, fused)   dW2 = dZ2^T H1 (TN)   db2 = colsum(dZ2)
 //   dZ1 = (dZ2 W2) * (1 - H1^2) (NN, fused)    dW1 = dZ1^T X  (TN)   db1 = colsum(dZ1)
@@ -61,6 +61,7 @@ WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
     pf = std::max(pf, (int64_t)gemm_splits(A, H, M) * A * H);
     pf = std::max(pf, (int64_t)gemm_ps_splits(H, H, Mp) * H * H);
     pf = std::max(pf, (int64_t)gemm_splits(H, D, M) * H * D);
+    pf = std::max(pf, (int64_t)((M + 511) / 512) * H);  // k_wide_dz2's db2 partials (DZ_ROWS x DZ_RT rows each)
     w.part = (float*)take(4 * pf);
   }
   w.stat_slots = (unsigned*)take(4 * 4);
@@ -71,81 +72,100 @@ WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
 bool wide_needed(const rlks_mlp_desc* d) { return d->hidden != HID || d->n_actions > 8 || d->obs_dim + 1 > 32; }
 
 // ----------------------------------------------------------------------------- kernels
-// PPO loss per row (same math as k_sf_fwdbwd's, for up to 64 actions); dout -> HBM, per-block
-// stats [policy loss, vf loss, kl, entropy], max |dout| -> slot
-template <int NET>
-__global__ __launch_bounds__(LOSS_ROWS) void k_wide_loss(const float* __restrict__ out, const float* __restrict__ x,
-                                                       int stride, int M, int D, int A, rlks_ppo_coeffs co,
-                                                       const float* __restrict__ dyn, float* __restrict__ dout,
-                                                       float* __restrict__ part_stat, unsigned* __restrict__ dmax) {
-  __shared__ float red[4][LOSS_ROWS / 64];
+// PPO loss per row (same math as sgd_sf16.hip's sf_loss, for up to 64 actions); dout -> HBM, per-block
+// stats [policy loss, vf loss, kl, entropy], max |dout| -> slot.  Value net: one thread per row.
+__global__ __launch_bounds__(LOSS_ROWS) void k_wide_loss_vf(const float* __restrict__ out, const float* __restrict__ x,
+                                                          int stride, int M, int D, int A, rlks_ppo_coeffs co,
+                                                          const float* __restrict__ dyn, float* __restrict__ dout,
+                                                          float* __restrict__ part_stat, unsigned* __restrict__ dmax) {
+  __shared__ float red[LOSS_ROWS / 64];
   const int m = blockIdx.x * LOSS_ROWS + threadIdx.x;
-  float st[4] = {0.f, 0.f, 0.f, 0.f};
-  float mx_d = 0.f;
+  float vl = 0.f, mx_d = 0.f;
   if (m < M) {
     const float* rec = x + (size_t)m * stride;
-    const float inv_count = dyn[RLKS_DYN_INV_COUNT];
-    if (NET == 0) {
-      const float* lg = out + (size_t)m * A;
-      const float* lo = rec + D;
-      const float adv = (rec[D + A] - dyn[RLKS_DYN_ADV_MEAN]) * dyn[RLKS_DYN_ADV_INVSTD];
-      const float logp_old = rec[D + A + 2];
-      const int act = (int)rec[D + A + 3];
-      float mx = lg[0], mo = lo[0];
-      for (int a = 1; a < A; ++a) { mx = fmaxf(mx, lg[a]); mo = fmaxf(mo, lo[a]); }
-      float se = 0.f, so = 0.f;
-      for (int a = 0; a < A; ++a) { se += expf(lg[a] - mx); so += expf(lo[a] - mo); }
-      const float lse = mx + logf(se), lso = mo + logf(so);
-      float kl = 0.f, ent = 0.f;
-      for (int a = 0; a < A; ++a) {
-        const float lp = lg[a] - lse, p = expf(lp), lpo = lo[a] - lso, po = expf(lpo);
-        kl += po * (lpo - lp);
-        ent -= p * lp;
-      }
-      const float lpa = lg[act] - lse;
-      const float ratio = expf(lpa - logp_old);
-      const float lo_c = 1.f - co.clip_param, hi_c = 1.f + co.clip_param;
-      const float rc = fminf(fmaxf(ratio, lo_c), hi_c);
-      const float s1 = adv * ratio, s2 = adv * rc;
-      const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
-      const float inr = (ratio >= lo_c && ratio <= hi_c) ? 1.f : 0.f;
-      const float dr = -adv * (w1 + (1.f - w1) * inr) * ratio;
-      const float klc = dyn[RLKS_DYN_KL_COEFF];
-      for (int a = 0; a < A; ++a) {
-        const float lp = lg[a] - lse, p = expf(lp), po = expf(lo[a] - lso);
-        float d = dr * ((a == act ? 1.f : 0.f) - p);
-        d += klc * (p - po);
-        d += co.entropy_coeff * p * (lp + ent);
-        d *= inv_count;
-        dout[(size_t)m * A + a] = d;
-        mx_d = fmaxf(mx_d, fabsf(d));
-      }
-      st[0] = -fminf(s1, s2);
-      st[2] = kl;
-      st[3] = ent;
-    } else {
-      const float diff = out[m] - rec[D + A + 1];
-      const float sq = diff * diff;
-      st[1] = fminf(sq, co.vf_clip_param);
-      const float d = (sq <= co.vf_clip_param) ? co.vf_loss_coeff * 2.f * diff * inv_count : 0.f;
-      dout[m] = d;
-      mx_d = fabsf(d);
-    }
+    const float diff = out[m] - rec[D + A + 1];
+    const float sq = diff * diff;
+    vl = fminf(sq, co.vf_clip_param);
+    const float d = (sq <= co.vf_clip_param) ? co.vf_loss_coeff * 2.f * diff * dyn[RLKS_DYN_INV_COUNT] : 0.f;
+    dout[m] = d;
+    mx_d = fabsf(d);
   }
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float s = wave_sum(st[i]);
-    if (l == 0) red[i][w] = s;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx_d = fmaxf(mx_d, __shfl_xor(mx_d, o, 64));
+  const float s = wave_sum(vl);
+  if (l == 0) red[w] = s;
+  mx_d = wave_max(mx_d);
   if (l == 0) atomicMax(dmax, __float_as_uint(mx_d));
   __syncthreads();
   if (threadIdx.x < 4) {
+    float t = 0.f;
+    if (threadIdx.x == 1)
+      for (int j = 0; j < LOSS_ROWS / 64; ++j) t += red[j];
+    part_stat[(size_t)blockIdx.x * 4 + threadIdx.x] = t;
+  }
+}
+
+// the policy net's loss with one wave per row and one lane per action (A <= 64): the logits and old
+// logits of a row are one coalesced load each, the softmax sums wave reductions.  (One thread per row,
+// looping over 64 actions with row-strided loads, took 0.29 ms per SGD step at c5: one wave per SIMD
+// and 64 cache lines per load instruction.)  Same per-block stats layout as k_wide_loss_vf.
+__global__ __launch_bounds__(LOSS_ROWS) void k_wide_loss_pi(const float* __restrict__ out, const float* __restrict__ x,
+                                                          int stride, int M, int D, int A, rlks_ppo_coeffs co,
+                                                          const float* __restrict__ dyn, float* __restrict__ dout,
+                                                          float* __restrict__ part_stat, unsigned* __restrict__ dmax) {
+  __shared__ float red[3][LOSS_ROWS / 64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool on = l < A;
+  const float inv_count = dyn[RLKS_DYN_INV_COUNT], klc = dyn[RLKS_DYN_KL_COEFF];
+  const float adv_mean = dyn[RLKS_DYN_ADV_MEAN], adv_invstd = dyn[RLKS_DYN_ADV_INVSTD];
+  const float lo_c = 1.f - co.clip_param, hi_c = 1.f + co.clip_param;
+  float st0 = 0.f, st2 = 0.f, st3 = 0.f, mx_d = 0.f;
+  for (int i = 0; i < 64; ++i) {
+    const int m = blockIdx.x * LOSS_ROWS + w * 64 + i;
+    if (m >= M) break;
+    const float* rec = x + (size_t)m * stride;
+    const float lg = on ? out[(size_t)m * A + l] : -INFINITY, lo = on ? rec[D + l] : -INFINITY;
+    const float adv = (rec[D + A] - adv_mean) * adv_invstd;
+    const float logp_old = rec[D + A + 2];
+    const int act = (int)rec[D + A + 3];
+    const float mx = wave_max(lg), mo = wave_max(lo);
+    const float lse = mx + logf(wave_sum(on ? expf(lg - mx) : 0.f)), lso = mo + logf(wave_sum(on ? expf(lo - mo) : 0.f));
+    const float lp = lg - lse, p = on ? expf(lp) : 0.f, lpo = lo - lso, po = on ? expf(lpo) : 0.f;
+    const float kl = wave_sum(on ? po * (lpo - lp) : 0.f);
+    const float ent = -wave_sum(on ? p * lp : 0.f);
+    const float lpa = wave_sum(l == act ? lp : 0.f);
+    const float ratio = expf(lpa - logp_old);
+    const float rc = fminf(fmaxf(ratio, lo_c), hi_c);
+    const float s1 = adv * ratio, s2 = adv * rc;
+    // torch.min backward splits ties evenly; torch.clamp passes the gradient on [lo, hi]
+    const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+    const float inr = (ratio >= lo_c && ratio <= hi_c) ? 1.f : 0.f;
+    const float dr = -adv * (w1 + (1.f - w1) * inr) * ratio;
+    if (on) {
+      float d = dr * ((l == act ? 1.f : 0.f) - p);
+      d += klc * (p - po);
+      d += co.entropy_coeff * p * (lp + ent);
+      d *= inv_count;
+      dout[(size_t)m * A + l] = d;
+      mx_d = fmaxf(mx_d, fabsf(d));
+    }
+    st0 -= fminf(s1, s2);
+    st2 += kl;
+    st3 += ent;
+  }
+  mx_d = wave_max(mx_d);
+  if (l == 0) {
+    atomicMax(dmax, __float_as_uint(mx_d));
+    red[0][w] = st0;
+    red[1][w] = st2;
+    red[2][w] = st3;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
     float s = 0.f;
-    for (int j = 0; j < LOSS_ROWS / 64; ++j) s += red[threadIdx.x][j];
-    part_stat[(size_t)blockIdx.x * 4 + threadIdx.x] = s;
+    if (k != 1)
+      for (int j = 0; j < LOSS_ROWS / 64; ++j) s += red[k == 0 ? 0 : k - 1][j];
+    part_stat[(size_t)blockIdx.x * 4 + k] = s;
   }
 }
 
@@ -196,72 +216,88 @@ __global__ void k_wide_sample(EnvView v, const float* __restrict__ logits, int A
 
 // dZ2 = (dout W3) (1 - H2^2), K = the head's outputs (64 / 1): too short a reduction for the split
 // GEMM's K pipeline (its tile prologue and epilogue were the whole 0.71 ms), so plain fp32 FMAs in k
-// order on 64-row x 256-column tiles: dout^T and W3 tiles in LDS (K chunks of 32), 8 x 8 outputs per
-// thread, H2 read and dZ2 written as float4 rows; max |dZ2| -> slot (one atomic per block)
-constexpr int DZ_ROWS = 64, DZ_COLS = 256, DZ_K = 32;
+// order on 64-row x 256-column tiles (8 per block): dout^T and W3 tiles in LDS (K chunks of 32), 8 x 8
+// outputs per thread, H2 read and dZ2 written as float4 rows; max |dZ2| -> slot (one atomic per
+// block); db2 as per-block column sums (a fixed order), summed by launch_split_reduce
+constexpr int DZ_ROWS = 64, DZ_COLS = 256, DZ_K = 32, DZ_RT = 8;  // DZ_RT row tiles per block
 __global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout, const float* __restrict__ w3,
                                                   const float* __restrict__ h2, float* __restrict__ dz, int M, int H,
-                                                  int K, unsigned* __restrict__ cmax_slot) {
+                                                  int K, unsigned* __restrict__ cmax_slot, float* __restrict__ part_db2) {
   __shared__ __attribute__((aligned(16))) float sA[DZ_K][DZ_ROWS + 4];  // dout^T chunk (padded: the transposing stores)
-  __shared__ __attribute__((aligned(16))) float sB[DZ_K][DZ_COLS];  // W3 chunk
+  __shared__ __attribute__((aligned(16))) float sB[DZ_K][DZ_COLS];      // W3 chunk; at the end the db2 sums
   const int tid = threadIdx.x, cg = tid & 31, rg = tid >> 5;
-  const int m0 = blockIdx.y * DZ_ROWS, n0 = blockIdx.x * DZ_COLS;
-  float acc[8][8];
+  const int n0 = blockIdx.x * DZ_COLS, n = n0 + 8 * cg;  // this thread's 8 columns (H % 8 == 0: host check)
+  float mx = 0.f, cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // max |dZ2|, db2: this thread's column sums
+  for (int rt = 0; rt < DZ_RT; ++rt) {
+    const int m0 = (blockIdx.y * DZ_RT + rt) * DZ_ROWS;
+    if (m0 >= M) break;
+    float acc[8][8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
-  for (int k0 = 0; k0 < K; k0 += DZ_K) {
-    const int kn = min(DZ_K, K - k0);
-    __syncthreads();
-    for (int e = tid; e < DZ_K * DZ_ROWS; e += 256) {  // e = r * DZ_K + k: coalesced along k
-      const int r = e / DZ_K, k = e - r * DZ_K, m = m0 + r;
-      sA[k][r] = (k < kn && m < M) ? dout[(size_t)m * K + k0 + k] : 0.f;
-    }
-    for (int e = tid; e < DZ_K * DZ_COLS / 4; e += 256) {
-      const int k = e / (DZ_COLS / 4), c4 = 4 * (e - k * (DZ_COLS / 4));
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k < kn && n0 + c4 < H) v = *reinterpret_cast<const float4*>(w3 + (size_t)(k0 + k) * H + n0 + c4);
-      *reinterpret_cast<float4*>(&sB[k][c4]) = v;
-    }
-    __syncthreads();
-    for (int k = 0; k < kn; ++k) {
-      const float4 a0 = *reinterpret_cast<const float4*>(&sA[k][8 * rg]), a1 = *reinterpret_cast<const float4*>(&sA[k][8 * rg + 4]);
-      const float4 b0 = *reinterpret_cast<const float4*>(&sB[k][8 * cg]), b1 = *reinterpret_cast<const float4*>(&sB[k][8 * cg + 4]);
-      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
-    }
-  }
-  float mx = 0.f;
-  const int n = n0 + 8 * cg;
-  if (n < H) {  // H % 8 == 0 (host check)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + 8 * rg + i;
-      if (m >= M) break;
-      const float4* hp = reinterpret_cast<const float4*>(h2 + (size_t)m * H + n);
-      const float4 g0 = hp[0], g1 = hp[1];
-      const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-      float o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] = acc[i][j] * (1.f - gv[j] * gv[j]);
-        mx = fmaxf(mx, fabsf(o[j]));
+      for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+    for (int k0 = 0; k0 < K; k0 += DZ_K) {
+      const int kn = min(DZ_K, K - k0);
+      __syncthreads();
+      for (int e = tid; e < DZ_K * DZ_ROWS; e += 256) {  // e = r * DZ_K + k: coalesced along k
+        const int r = e / DZ_K, k = e - r * DZ_K, m = m0 + r;
+        sA[k][r] = (k < kn && m < M) ? dout[(size_t)m * K + k0 + k] : 0.f;
       }
-      float4* dp = reinterpret_cast<float4*>(dz + (size_t)m * H + n);
-      dp[0] = make_float4(o[0], o[1], o[2], o[3]);
-      dp[1] = make_float4(o[4], o[5], o[6], o[7]);
+      for (int e = tid; e < DZ_K * DZ_COLS / 4; e += 256) {
+        const int k = e / (DZ_COLS / 4), c4 = 4 * (e - k * (DZ_COLS / 4));
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k < kn && n0 + c4 < H) v = *reinterpret_cast<const float4*>(w3 + (size_t)(k0 + k) * H + n0 + c4);
+        *reinterpret_cast<float4*>(&sB[k][c4]) = v;
+      }
+      __syncthreads();
+      for (int k = 0; k < kn; ++k) {
+        const float4 a0 = *reinterpret_cast<const float4*>(&sA[k][8 * rg]), a1 = *reinterpret_cast<const float4*>(&sA[k][8 * rg + 4]);
+        const float4 b0 = *reinterpret_cast<const float4*>(&sB[k][8 * cg]), b1 = *reinterpret_cast<const float4*>(&sB[k][8 * cg + 4]);
+        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+      }
+    }
+    if (n < H) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + 8 * rg + i;
+        if (m >= M) break;
+        const float4* hp = reinterpret_cast<const float4*>(h2 + (size_t)m * H + n);
+        const float4 g0 = hp[0], g1 = hp[1];
+        const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o[j] = acc[i][j] * (1.f - gv[j] * gv[j]);
+          mx = fmaxf(mx, fabsf(o[j]));
+          cs[j] += o[j];
+        }
+        float4* dp = reinterpret_cast<float4*>(dz + (size_t)m * H + n);
+        dp[0] = make_float4(o[0], o[1], o[2], o[3]);
+        dp[1] = make_float4(o[4], o[5], o[6], o[7]);
+      }
     }
   }
   mx = wave_max(mx);
   __shared__ float red[4];
   if ((tid & 63) == 0) red[tid >> 6] = mx;
+  // db2 partial of the block's rows: the 8 row groups' column sums combined in a fixed order
+  __syncthreads();  // (every thread is past its last read of sB)
+  float* sC = &sB[0][0];  // [8 rg][256]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sC[rg * DZ_COLS + 8 * cg + j] = cs[j];
   __syncthreads();
   if (tid == 0) atomicMax(cmax_slot, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+  if (n0 + tid < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += sC[g * DZ_COLS + tid];
+    part_db2[(size_t)blockIdx.y * H + n0 + tid] = t;
+  }
 }
 
 // ----------------------------------------------------------------------------- host
@@ -363,10 +399,10 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     RLKS_HIP(hipMemsetAsync(sl, 0, 4 * SL_N, s));
     if (int rc = forward_net(d, P, n, mb, stride, M, net, s)) return rc;
     if (net == 0)
-      hipLaunchKernelGGL(k_wide_loss<0>, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
+      hipLaunchKernelGGL(k_wide_loss_pi, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
                          n.dout, n.part_stat, sl + SL_DOUT);
     else
-      hipLaunchKernelGGL(k_wide_loss<1>, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
+      hipLaunchKernelGGL(k_wide_loss_vf, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
                          n.dout, n.part_stat, sl + SL_DOUT);
     RLKS_LAUNCHED();
     // head: dW3 = dout^T H2, db3 = colsum(dout)
@@ -376,9 +412,12 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     if (int rc = launch_colsum(n.dout, M, An, An, g + o[5], 0, w.part, s)) return rc;
     // dZ2 = (dout W3) (1 - H2^2); dW2 = dZ2^T H1; db2
     RLKS_REQUIRE(H % 8 == 0, RLKS_ERR_UNSUPPORTED, "wide path: hidden width must be a multiple of 8");
-    hipLaunchKernelGGL(k_wide_dz2, dim3(cdiv(H, DZ_COLS), cdiv(M, DZ_ROWS)), dim3(256), 0, s, n.dout, P.w3, n.h2, w.dza, M,
-                       H, An, sl + SL_DZ2);
+    const int dz_blocks = (int)cdiv(M, DZ_ROWS * DZ_RT);
+    hipLaunchKernelGGL(k_wide_dz2, dim3(cdiv(H, DZ_COLS), dz_blocks), dim3(256), 0, s, n.dout, P.w3, n.h2, w.dza, M, H,
+                       An, sl + SL_DZ2, w.part);
     RLKS_LAUNCHED();
+    // db2 from the dZ2 kernel's per-block column sums (before dW2's split-K reuses the partial buffer)
+    if (int rc = launch_split_reduce(w.part, dz_blocks, 1, H, g + o[3], H, 0, s)) return rc;
     if (int rc = launch_split_planes(w.dza, M, H, H, sl + SL_DZ2, 0, w.dzh, w.dzl, H, s)) return rc;
     {  // dW2[n][k] = sum_m dZ2[m][n] H1[m][k]: both operands K-major planes, split over the rows
       PsArgs a{};
@@ -389,7 +428,6 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
       a.part = w.part;
       if (int rc = launch_gemm_ps(a, s)) return rc;
     }
-    if (int rc = launch_colsum(w.dza, M, H, H, g + o[3], 0, w.part, s)) return rc;
     {  // dZ1[m][k] = (sum_n dZ2[m][n] W2[n][k]) (1 - H1^2): B = W2 planes read K-major
       PsArgs a{};
       a.a = ps_op(w.dzh, w.dzl, H, 0, M, sl + SL_DZ2);
