@@ -165,7 +165,7 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + wn * 64 + 32 * j + r;
     const bool nok = n < g.N;
-    const float bias = EPI == PS_TANH_BIAS && nok ? g.bias[n] : 0.f;
+    const float bias = (EPI == PS_TANH_BIAS || EPI == PS_TANH_BIAS_PLANES) && nok ? g.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -173,7 +173,15 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         const int m = m0 + wm * 64 + 32 * i + acc_row(q, l);
         if (!nok || m >= g.M) continue;
         float v = acc[i][j][q] * unscale;
-        if (EPI == PS_TANH_BIAS) v = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f((v + bias) * 2.885390081777927f) + 1.f), 1.f);
+        if (EPI == PS_TANH_BIAS || EPI == PS_TANH_BIAS_PLANES)
+          v = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f((v + bias) * 2.885390081777927f) + 1.f), 1.f);
+        if (EPI == PS_TANH_BIAS_PLANES) {  // H1 for the pre-split GEMMs: fp16 planes at 2^14
+          const float hs = v * 16384.f;
+          const _Float16 hh = (_Float16)hs;
+          g.c_hi[(size_t)m * ldc + n] = hh;
+          g.c_lo[(size_t)m * ldc + n] = (_Float16)(hs - (float)hh);
+          continue;
+        }
         if (EPI == PS_DTANH) {  // G = (hi + lo) 2^-14 from the aux planes
           const size_t ai = (size_t)m * g.ldaux + n;
           const float gg = ((float)g.aux_hi[ai] + (float)g.aux_lo[ai]) * (1.f / 16384.f);
@@ -224,6 +232,9 @@ static int launch_ps_t(const PsArgs& a, hipStream_t s) {
     case PS_STORE: hipLaunchKernelGGL((k_gemm_ps<AK, BK, PS_STORE>), grid, dim3(PNT), lds, s, a); break;
     case PS_TANH_BIAS: hipLaunchKernelGGL((k_gemm_ps<AK, BK, PS_TANH_BIAS>), grid, dim3(PNT), lds, s, a); break;
     case PS_DTANH: hipLaunchKernelGGL((k_gemm_ps<AK, BK, PS_DTANH>), grid, dim3(PNT), lds, s, a); break;
+    case PS_TANH_BIAS_PLANES:
+      hipLaunchKernelGGL((k_gemm_ps<AK, BK, PS_TANH_BIAS_PLANES>), grid, dim3(PNT), lds, s, a);
+      break;
     default: return fail(RLKS_ERR_ARG, "gemm_ps: unknown epilogue");
   }
   RLKS_LAUNCHED();
@@ -231,8 +242,9 @@ static int launch_ps_t(const PsArgs& a, hipStream_t s) {
 }
 
 int launch_gemm_ps(const PsArgs& a, hipStream_t s) {
-  RLKS_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.K % PK == 0 && a.C, RLKS_ERR_ARG,
-               "gemm_ps: K must be a positive multiple of 32");
+  RLKS_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.K % PK == 0 &&
+                   (a.epi == PS_TANH_BIAS_PLANES ? (a.c_hi && a.c_lo) : a.C != nullptr),
+               RLKS_ERR_ARG, "gemm_ps: K must be a positive multiple of 32");
   RLKS_REQUIRE((!a.a.kmajor || a.a.rows % 8 == 0) && (!a.b.kmajor || a.b.rows % 8 == 0), RLKS_ERR_ARG,
                "gemm_ps: a K-major operand needs a multiple of 8 rows");
   PsArgs b = a;

@@ -38,13 +38,15 @@ struct PsOperand {
   const unsigned* maxslot;  // e = exponent with max 2^e in [2^14, 2^15) (float bits); null: fexp
   int fexp;
 };
-enum { PS_STORE = 0, PS_TANH_BIAS = 1, PS_DTANH = 2 };
+enum { PS_STORE = 0, PS_TANH_BIAS = 1, PS_DTANH = 2, PS_TANH_BIAS_PLANES = 3 };
 struct PsArgs {
   PsOperand a, b;           // C[m][n] = sum_k A[m][k] B[n][k]
   int M, N, K;              // K a multiple of 32
   int epi;                  // PS_STORE: C (or split-K partials); PS_TANH_BIAS: tanh(acc + bias[n]);
-                            // PS_DTANH: acc (1 - G^2), G = (aux_hi + aux_lo) 2^-14
+                            // PS_DTANH: acc (1 - G^2), G = (aux_hi + aux_lo) 2^-14;
+                            // PS_TANH_BIAS_PLANES: tanh(acc + bias[n]) as fp16 planes at 2^14 in c_hi / c_lo
   float* C;
+  _Float16 *c_hi, *c_lo;
   int ldc;
   const float* bias;
   const _Float16 *aux_hi, *aux_lo;

@@ -9,6 +9,7 @@ struct WideNet {
   _Float16 *h1h, *h1l;          // H1 as fp16 planes [M][H] at 2^14 (the pre-split GEMMs' operand)
   float *h2, *out, *dout;       // [M][H], [M][A_net], [M][A_net]
   _Float16 *w2h, *w2l;          // W2 planes [H][H] (this SGD step's / forward's weights)
+  _Float16 *w1h, *w1l;          // W1 planes [H][D] (obs_dim D a multiple of 32: Z1 on the pre-split GEMM)
   unsigned* slots;              // operand max |x| slots
   float* part_stat;             // [blocks][4]
 };
@@ -16,6 +17,7 @@ struct WideWs {
   WideNet n[2];
   float *dza, *dzb;  // [M][H] dZ2 / dZ1
   _Float16 *dzh, *dzl;  // dZ2 planes [M][H]
+  _Float16 *xh, *xl;    // X planes [M][D] (obs_dim D a multiple of 32)
   double* rew64;     // [M] env-step scratch (rollout)
   float* part;       // split-K / split column-sum partials of the weight gradients
   unsigned* stat_slots;

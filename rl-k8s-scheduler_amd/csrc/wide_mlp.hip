@@ -46,6 +46,8 @@ WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
     n.h2 = (float*)take(4LL * M * H);
     n.w2h = (_Float16*)take(2LL * H * H);
     n.w2l = (_Float16*)take(2LL * H * H);
+    n.w1h = (_Float16*)take(2LL * H * D);
+    n.w1l = (_Float16*)take(2LL * H * D);
     n.out = (float*)take(4LL * M * An);
     n.dout = (float*)take(4LL * M * An);
     n.slots = (unsigned*)take(4 * SL_N);
@@ -55,11 +57,14 @@ WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
   w.dzb = (float*)take(4LL * M * H);
   w.dzh = (_Float16*)take(2LL * Mp * H);
   w.dzl = (_Float16*)take(2LL * Mp * H);
+  w.xh = (_Float16*)take(2LL * Mp * D);  // rows [M, Mp) zeroed by wide_grad (dW1's K runs over Mp)
+  w.xl = (_Float16*)take(2LL * Mp * D);
   w.rew64 = (double*)take(8LL * M);
   {  // weight-gradient partials: dW3 [A][H], dW2 [H][H], dW1 [H][D] (K = M), column sums of M rows
     int64_t pf = (int64_t)colsum_splits(M) * H;
     pf = std::max(pf, (int64_t)gemm_splits(A, H, M) * A * H);
     pf = std::max(pf, (int64_t)gemm_ps_splits(H, H, Mp) * H * H);
+    pf = std::max(pf, (int64_t)gemm_ps_splits(H, D, Mp) * H * D);
     pf = std::max(pf, (int64_t)gemm_splits(H, D, M) * H * D);
     pf = std::max(pf, (int64_t)((M + 511) / 512) * H);  // k_wide_dz2's db2 partials (DZ_ROWS x DZ_RT rows each)
     w.part = (float*)take(4 * pf);
@@ -340,7 +345,7 @@ constexpr int H1_EXP = 14;  // H1 planes hold tanh x 2^14
 
 // forward of net `net` over M rows of x (row stride ldx): H1 (planes), H2 and out in the workspace
 int forward_net(const rlks_mlp_desc* d, const Net& P, const WideNet& n, const float* x, int ldx, int M, int net,
-                hipStream_t s) {
+                _Float16* xh, _Float16* xl, hipStream_t s) {
   const int D = d->obs_dim, H = d->hidden, An = net == 0 ? d->n_actions : 1;
   unsigned* sl = n.slots;
   if (int rc = launch_absmax(x, M, D, ldx, sl + SL_X, s)) return rc;
@@ -348,9 +353,19 @@ int forward_net(const rlks_mlp_desc* d, const Net& P, const WideNet& n, const fl
   if (int rc = launch_absmax(P.w2, H, H, H, sl + SL_W2, s)) return rc;
   if (int rc = launch_absmax(P.w3, An, H, H, sl + SL_W3, s)) return rc;
   if (int rc = launch_split_planes(P.w2, H, H, H, sl + SL_W2, 0, n.w2h, n.w2l, H, s)) return rc;
-  if (int rc = gemm(x, ldx, 0, P.w1, D, 1, nullptr, H, M, H, D, GEMM_TANH_BIAS_PLANES, P.b1, nullptr, 0, sl + SL_X,
-                    sl + SL_W1, nullptr, s, nullptr, n.h1h, n.h1l))
+  if (D % 32 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0) {
+    // H1 = tanh(X W1^T + b1) on the pre-split GEMM (K = obs_dim, 192 at c5), written as planes
+    if (int rc = launch_split_planes(x, M, D, ldx, sl + SL_X, 0, xh, xl, D, s)) return rc;
+    if (int rc = launch_split_planes(P.w1, H, D, D, sl + SL_W1, 0, n.w1h, n.w1l, D, s)) return rc;
+    PsArgs a{};
+    a.a = ps_op(xh, xl, D, 0, M, sl + SL_X);
+    a.b = ps_op(n.w1h, n.w1l, D, 0, H, sl + SL_W1);
+    a.M = M; a.N = H; a.K = D; a.epi = PS_TANH_BIAS_PLANES; a.c_hi = n.h1h; a.c_lo = n.h1l; a.ldc = H; a.bias = P.b1;
+    if (int rc = launch_gemm_ps(a, s)) return rc;
+  } else if (int rc = gemm(x, ldx, 0, P.w1, D, 1, nullptr, H, M, H, D, GEMM_TANH_BIAS_PLANES, P.b1, nullptr, 0, sl + SL_X,
+                           sl + SL_W1, nullptr, s, nullptr, n.h1h, n.h1l)) {
     return rc;
+  }
   {  // Z2 = H1 W2^T -> H2 = tanh(Z2 + b2)
     PsArgs a{};
     a.a = ps_op(n.h1h, n.h1l, H, 0, M, nullptr, H1_EXP);
@@ -372,7 +387,7 @@ int wide_forward(const rlks_mlp_desc* d, const float* params, const float* x, in
     if (!dst) continue;
     const WideNet& n = w.n[net];
     RLKS_HIP(hipMemsetAsync(n.slots, 0, 4 * SL_N, s));
-    if (int rc = forward_net(d, net_of(params, L, net), n, x, ldx, M, net, s)) return rc;
+    if (int rc = forward_net(d, net_of(params, L, net), n, x, ldx, M, net, w.xh, w.xl, s)) return rc;
     const int An = net == 0 ? d->n_actions : 1;
     RLKS_HIP(hipMemcpyAsync(dst, n.out, sizeof(float) * M * An, hipMemcpyDeviceToDevice, s));
   }
@@ -388,7 +403,9 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     const size_t off = (size_t)M * H, bytes = 2ull * (Mp - M) * H;
     for (_Float16* p : {w.n[0].h1h, w.n[0].h1l, w.n[1].h1h, w.n[1].h1l, w.dzh, w.dzl})
       RLKS_HIP(hipMemsetAsync(p + off, 0, bytes, s));
+    for (_Float16* p : {w.xh, w.xl}) RLKS_HIP(hipMemsetAsync(p + (size_t)M * D, 0, 2ull * (Mp - M) * D, s));
   }
+  const bool ps_x = D % 32 == 0 && stride % 4 == 0 && ((uintptr_t)mb & 15) == 0;  // X planes (forward_net)
   for (int net = 0; net < 2; ++net) {
     const int An = net == 0 ? A : 1;
     const WideNet& n = w.n[net];
@@ -397,7 +414,7 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     const int64_t* o = L.off + 6 * net;
     unsigned* sl = n.slots;
     RLKS_HIP(hipMemsetAsync(sl, 0, 4 * SL_N, s));
-    if (int rc = forward_net(d, P, n, mb, stride, M, net, s)) return rc;
+    if (int rc = forward_net(d, P, n, mb, stride, M, net, w.xh, w.xl, s)) return rc;
     if (net == 0)
       hipLaunchKernelGGL(k_wide_loss_pi, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
                          n.dout, n.part_stat, sl + SL_DOUT);
@@ -436,10 +453,21 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
       a.aux_hi = n.h1h; a.aux_lo = n.h1l; a.ldaux = H; a.cmax = sl + SL_DZ1;
       if (int rc = launch_gemm_ps(a, s)) return rc;
     }
-    // dW1 = dZ1^T X; db1
-    if (int rc = gemm(w.dzb, H, 1, mb, stride, 0, g + o[0], D, H, D, M, GEMM_STORE, nullptr, nullptr, 0, sl + SL_DZ1,
-                      sl + SL_X, nullptr, s, w.part))
+    // dW1 = dZ1^T X; db1.  With X in planes (obs_dim a multiple of 32): dZ1 split into the dZ2 planes'
+    // buffer (free once dZ1's GEMM has read it) and both read K-major by the pre-split GEMM
+    if (ps_x) {
+      if (int rc = launch_split_planes(w.dzb, M, H, H, sl + SL_DZ1, 0, w.dzh, w.dzl, H, s)) return rc;
+      PsArgs a{};
+      a.a = ps_op(w.dzh, w.dzl, H, 1, H, sl + SL_DZ1);
+      a.b = ps_op(w.xh, w.xl, D, 1, D, sl + SL_X);
+      a.M = H; a.N = D; a.K = Mp; a.epi = PS_STORE; a.C = g + o[0]; a.ldc = D;
+      a.splits = gemm_ps_splits(H, D, Mp);
+      a.part = w.part;
+      if (int rc = launch_gemm_ps(a, s)) return rc;
+    } else if (int rc = gemm(w.dzb, H, 1, mb, stride, 0, g + o[0], D, H, D, M, GEMM_STORE, nullptr, nullptr, 0,
+                             sl + SL_DZ1, sl + SL_X, nullptr, s, w.part)) {
       return rc;
+    }
     if (int rc = launch_colsum(w.dzb, M, H, H, g + o[1], 0, w.part, s)) return rc;
   }
   if (stats) {
