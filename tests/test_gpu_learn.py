@@ -206,7 +206,9 @@ def test_ppo_grad_matches_oracle(rows, A, precision):
 
 
 @pytest.mark.parametrize("rows,D,H,A", [(512, 6, 256, 2), (384, 12, 512, 4), (256, 192, 2048, 64), (300, 24, 96, 8),
-                                        (8192, 24, 512, 8), (4096, 192, 2048, 64)])  # split-K weight gradients
+                                        (8192, 24, 512, 8), (4096, 192, 2048, 64),
+                                        (300, 192, 256, 64), (1000, 64, 512, 16)])  # split-K weight gradients;
+# obs 192 / 64 at ragged rows: Z1 and dW1 on the pre-split GEMM with zero-padded X / dZ1 plane rows
 def test_wide_grad_matches_oracle(rows, D, H, A):
     """generic-width path (wide_mlp.hip: split-fp16 GEMMs with fused epilogues), incl. the c5 shape
     (obs 3 x 64 clusters, 64 actions, hidden 2048) and ragged rows; same 1e-5 bar"""
