@@ -812,7 +812,10 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1
     for (int dt = 0; dt < DT; ++dt) {
       const f4 dw = mk16x3(xth[dt], xtl[dt], zh, zl, f4zero());  // rows d = 16 dt + 4g + i, column k
       const float4 v = {dw[0] * u1, dw[1] * u1, dw[2] * u1, dw[3] * u1};
-      *reinterpret_cast<float4*>(sEp + (kt % KPR) * SLOT + (w * 16 + c) * 16 * DT + 16 * dt + 4 * gq) = v;
+      // row k = c of the wave's slot: 16-byte quad gq at gq ^ ((c >> 1) & 3), so that the 8 lanes of a
+      // ds_write_b128 group (c = 0..7) cover all 32 banks (unswizzled: 4-way conflicts; profiles/r03s
+      // F1b 11% of CU cycles in LDS bank conflicts)
+      *reinterpret_cast<float4*>(sEp + (kt % KPR) * SLOT + (w * 16 + c) * 16 * DT + 16 * dt + 4 * (gq ^ ((c >> 1) & 3))) = v;
     }
     if (kt % KPR == KPR - 1) {  // (k-tile, k, d) elements; ND a compile-time constant (no runtime division)
       __syncthreads();
@@ -821,8 +824,9 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1
         const int jj = e / (16 * ND), e2 = e - jj * 16 * ND, kk = e2 / ND, d = e2 - kk * ND;
         const int k = 16 * (kt0 + jj) + kk;
         float sum = 0.f;
+        const int dq = (d & ~15) + 4 * (((d >> 2) & 3) ^ ((kk >> 1) & 3)) + (d & 3);  // the stores' quad swizzle
 #pragma unroll
-        for (int ww = 0; ww < W; ++ww) sum += sEp[jj * SLOT + (ww * 16 + kk) * 16 * DT + d];
+        for (int ww = 0; ww < W; ++ww) sum += sEp[jj * SLOT + (ww * 16 + kk) * 16 * DT + dq];
         if (d < ND - 1) N.part_w1[((size_t)blk * HID + k) * (ND - 1) + d] = sum;
         else N.part_b1[(size_t)blk * HID + k] = sum;
       }
