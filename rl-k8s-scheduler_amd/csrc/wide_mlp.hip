@@ -109,23 +109,26 @@ __global__ __launch_bounds__(LOSS_ROWS) void k_wide_loss_vf(const float* __restr
   }
 }
 
-// the policy net's loss with one wave per row and one lane per action (A <= 64): the logits and old
+// the policy net's loss with one wave per row and one lane per action (A <= 64; 16 waves per block of
+// LOSS_ROWS rows, so four waves per SIMD): the logits and old
 // logits of a row are one coalesced load each, the softmax sums wave reductions.  (One thread per row,
 // looping over 64 actions with row-strided loads, took 0.29 ms per SGD step at c5: one wave per SIMD
 // and 64 cache lines per load instruction.)  Same per-block stats layout as k_wide_loss_vf.
-__global__ __launch_bounds__(LOSS_ROWS) void k_wide_loss_pi(const float* __restrict__ out, const float* __restrict__ x,
+constexpr int LOSS_PI_WAVES = 16;  // waves per policy-loss block: LOSS_ROWS / 16 rows each (4 waves per SIMD)
+__global__ __launch_bounds__(64 * LOSS_PI_WAVES) void k_wide_loss_pi(const float* __restrict__ out, const float* __restrict__ x,
                                                           int stride, int M, int D, int A, rlks_ppo_coeffs co,
                                                           const float* __restrict__ dyn, float* __restrict__ dout,
                                                           float* __restrict__ part_stat, unsigned* __restrict__ dmax) {
-  __shared__ float red[3][LOSS_ROWS / 64];
+  constexpr int RPW = LOSS_ROWS / LOSS_PI_WAVES;  // rows per wave
+  __shared__ float red[4][LOSS_PI_WAVES];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const bool on = l < A;
   const float inv_count = dyn[RLKS_DYN_INV_COUNT], klc = dyn[RLKS_DYN_KL_COEFF];
   const float adv_mean = dyn[RLKS_DYN_ADV_MEAN], adv_invstd = dyn[RLKS_DYN_ADV_INVSTD];
   const float lo_c = 1.f - co.clip_param, hi_c = 1.f + co.clip_param;
   float st0 = 0.f, st2 = 0.f, st3 = 0.f, mx_d = 0.f;
-  for (int i = 0; i < 64; ++i) {
-    const int m = blockIdx.x * LOSS_ROWS + w * 64 + i;
+  for (int i = 0; i < RPW; ++i) {
+    const int m = blockIdx.x * LOSS_ROWS + w * RPW + i;
     if (m >= M) break;
     const float* rec = x + (size_t)m * stride;
     const float lg = on ? out[(size_t)m * A + l] : -INFINITY, lo = on ? rec[D + l] : -INFINITY;
@@ -159,17 +162,22 @@ __global__ __launch_bounds__(LOSS_ROWS) void k_wide_loss_pi(const float* __restr
   }
   mx_d = wave_max(mx_d);
   if (l == 0) {
-    atomicMax(dmax, __float_as_uint(mx_d));
     red[0][w] = st0;
     red[1][w] = st2;
     red[2][w] = st3;
+    red[3][w] = mx_d;
   }
   __syncthreads();
+  if (threadIdx.x == 64) {  // one atomic per block (single-address atomics serialise at their L2 channel)
+    float m = 0.f;
+    for (int j = 0; j < LOSS_PI_WAVES; ++j) m = fmaxf(m, red[3][j]);
+    atomicMax(dmax, __float_as_uint(m));
+  }
   if (threadIdx.x < 4) {
     const int k = threadIdx.x;
     float s = 0.f;
     if (k != 1)
-      for (int j = 0; j < LOSS_ROWS / 64; ++j) s += red[k == 0 ? 0 : k - 1][j];
+      for (int j = 0; j < LOSS_PI_WAVES; ++j) s += red[k == 0 ? 0 : k - 1][j];
     part_stat[(size_t)blockIdx.x * 4 + k] = s;
   }
 }
@@ -416,7 +424,7 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     RLKS_HIP(hipMemsetAsync(sl, 0, 4 * SL_N, s));
     if (int rc = forward_net(d, P, n, mb, stride, M, net, w.xh, w.xl, s)) return rc;
     if (net == 0)
-      hipLaunchKernelGGL(k_wide_loss_pi, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
+      hipLaunchKernelGGL(k_wide_loss_pi, dim3(w.blocks), dim3(64 * LOSS_PI_WAVES), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
                          n.dout, n.part_stat, sl + SL_DOUT);
     else
       hipLaunchKernelGGL(k_wide_loss_vf, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
