@@ -274,12 +274,13 @@ def _net(torch, flat, off, D, H, A, net):
     return ts
 
 
-def mlp_forward(flat, off, D, H, A, obs):
-    """RLlib FCNet forward (tanh, separate value net) in float64: (logits, value)"""
+def mlp_forward(flat, off, D, H, A, obs, dtype=np.float64):
+    """RLlib FCNet forward (tanh, separate value net) in float64: (logits, value)
+    (dtype=np.float32: torch fp32 on the CPU, the precision baseline of the per-element tests)"""
     import torch
 
-    x = torch.as_tensor(np.asarray(obs, np.float64))
-    f = torch.as_tensor(np.asarray(flat, np.float64))
+    x = torch.as_tensor(np.asarray(obs, dtype))
+    f = torch.as_tensor(np.asarray(flat, dtype))
     out = []
     for net in (0, 1):
         w1, b1, w2, b2, w3, b3 = _net(torch, f, off, D, H, A, net)

@@ -72,6 +72,12 @@ class PPOConfig:
         self.evaluation_interval = None
         self.evaluation_duration = 10
         self.metrics_num_episodes_for_smoothing = 100
+        # rlks.metrics.JsonLinesReporter: append every train() result to this file as one JSON line
+        # (also: $RLKS_METRICS_JSONL)
+        self.metrics_json_lines = None
+        # save() with no directory: this run's logdir under rlks.checkpoints.results_root()
+        # (~/ray_results/PPO_<env>_<time>, RLlib's Algorithm.logdir)
+        self.logdir = None
         # save() includes the lanes' env state: None = yes for table envs (~30 B per lane), no for
         # node-level envs (C x nodes x 8 B per lane: ~1 GB at c3, written on every save())
         self.checkpoint_env_state = None
@@ -142,7 +148,9 @@ class PPOConfig:
             self.evaluation_duration = evaluation_duration
         return self
 
-    def reporting(self, metrics_num_episodes_for_smoothing=None, **kw):
+    def reporting(self, metrics_num_episodes_for_smoothing=None, json_lines=None, **kw):
+        if json_lines is not None:
+            self.metrics_json_lines = str(json_lines)
         if metrics_num_episodes_for_smoothing is not None:
             w = int(metrics_num_episodes_for_smoothing)
             # the window is filled from the device episode log, which keeps RLKS_EPLOG_CAP episodes
@@ -327,6 +335,9 @@ class PPO:
         self.sample_calls = 0   # compute_actions / compute_single_action draws so far (Philox counter)
         self.iteration = 0
         self.timesteps_total = 0
+        from .metrics import JsonLinesReporter
+
+        self.reporter = JsonLinesReporter.from_config(cfg, self.rank)
         self.episodes_total = 0
 
     # ------------------------------------------------------------------ internals
@@ -555,6 +566,8 @@ class PPO:
         if iv and self.iteration % int(iv) == 0:
             result["evaluation"] = self.evaluate()
         result["time_this_iter_s"] = time.time() - t0
+        if self.reporter is not None:
+            self.reporter.report(result, self)
         return result
 
     # Philox counter word 0 of policy-side draws (compute_actions / compute_single_action): no env
@@ -630,7 +643,9 @@ class PPO:
         return self.config.nodes is None if v is None else bool(v)
 
     def save(self, checkpoint_dir=None):
-        """RLlib Algorithm.save(): writes <dir>/checkpoint_<iter:06d>/ and returns its path.
+        """RLlib Algorithm.save(): writes <dir>/checkpoint_<iter:06d>/ and returns its path (no dir:
+        this run's logdir, ~/ray_results/PPO_<env>_<time> or $RLKS_RESULTS_DIR, where
+        rlks.checkpoints.latest_checkpoint finds it as final_evaluation.py:13-25 does).
         Files: state.pt (tensors, weights_only-loadable), algorithm_state.json (config + scalars),
         table.npz (the env table's float64 bits) and, with checkpoint_env_state, env_state.bin
         (raw device snapshot, rlks_env_save_state; rank-suffixed when world > 1).  The snapshot is
@@ -640,7 +655,14 @@ class PPO:
         ranks meet at a barrier."""
         import torch
 
-        base = Path(checkpoint_dir) if checkpoint_dir else Path.home() / "rlks_results" / "PPO"
+        from .checkpoints import default_logdir
+
+        if checkpoint_dir is None and self.config.logdir is None:
+            # one logdir per run (RLlib's Algorithm.logdir), so that successive save() calls land
+            # side by side and rlks.checkpoints.latest_checkpoint() finds the newest
+            env = getattr(self.config.env, "__name__", None) or "K8sMultiCloudEnv"
+            self.config.logdir = str(default_logdir(env))
+        base = Path(checkpoint_dir) if checkpoint_dir else Path(self.config.logdir)
         path = base / f"checkpoint_{self.iteration:06d}"
         path.mkdir(parents=True, exist_ok=True)
         st = self.get_state()
@@ -653,6 +675,7 @@ class PPO:
         if env_state is not None:
             env_state.numpy().tofile(path / f"env_state{sfx}.bin")
             st["env_state_bytes"] = int(env_state.numel())
+        st["env_state_saved"] = env_state is not None
         torch.save(tensors, path / f"state{sfx}.pt")
         if self.rank == 0:
             self.table.save(path / "table.npz")
@@ -696,6 +719,17 @@ class PPO:
             self.buf["obs"][0].copy_(tensors["current_obs"].to(self.device))
             self._carry = False
             self.env.episode_log(clear=True)
+        else:
+            # node-level envs default to checkpoint_env_state off (~1 GB per save at c3): weights,
+            # Adam state and counters resume, the env lanes start fresh, so the run is not a
+            # bit-exact continuation
+            import warnings
+
+            why = ("saved with checkpoint_env_state off" if not meta.get("env_state_saved", True)
+                   else "its env_state file is missing")
+            warnings.warn(f"checkpoint {path}: {why}; the env lanes keep their current state, so the resumed "
+                          "run is not an exact continuation (set PPOConfig.checkpoint_env_state = True)",
+                          RuntimeWarning, stacklevel=2)
 
     @classmethod
     def from_checkpoint(cls, checkpoint_path, config: PPOConfig | None = None, **kw):

@@ -1,0 +1,54 @@
+"""Host-side checkpoint discovery (final_evaluation.py:13-25) and the JSON-lines reporter (SURVEY.md
+§5): no GPU needed."""
+import json
+import sys
+from pathlib import Path
+from types import SimpleNamespace
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "rl-k8s-scheduler_amd"))
+
+
+def test_latest_checkpoint_picks_highest_number(tmp_path, monkeypatch):
+    from rlks.checkpoints import checkpoint_number, find_checkpoints, latest_checkpoint
+
+    exp = tmp_path / "FINAL_PPO_AWS_AZURE"
+    for trial, nums in (("PPO_K8sMultiCloudEnv_00000", (10, 20, 80)), ("PPO_K8sMultiCloudEnv_00001", (9, 100))):
+        for n in nums:
+            (exp / trial / f"checkpoint_{n:06d}").mkdir(parents=True)
+    (exp / "PPO_K8sMultiCloudEnv_00000" / "checkpoint_tmp").mkdir()       # no trailing number: ignored
+    (exp / "PPO_K8sMultiCloudEnv_00000" / "checkpoint_000999.json").write_text("{}")  # a file: ignored
+    got = latest_checkpoint(tmp_path, "FINAL_PPO_AWS_AZURE")
+    assert got == exp / "PPO_K8sMultiCloudEnv_00001" / "checkpoint_000100"
+    assert [checkpoint_number(p) for p in find_checkpoints(exp)] == [9, 10, 20, 80, 100]
+    assert latest_checkpoint(tmp_path / "missing") is None
+    monkeypatch.setenv("RLKS_RESULTS_DIR", str(tmp_path))
+    assert latest_checkpoint(name="FINAL_PPO_AWS_AZURE") == got
+
+
+def test_json_lines_reporter(tmp_path):
+    from rlks.metrics import JsonLinesReporter, flops_per_env_step
+
+    # 269,824 FLOP forward per sample (2 actions), ~8.37 MFLOP per env-step at 10 epochs
+    fwd = flops_per_env_step(6, 256, 2, 0)
+    assert fwd == 2 * (6 * 256 + 256 * 256 + 256 * 2) + 2 * (6 * 256 + 256 * 256 + 256)
+    assert abs(flops_per_env_step(6, 256, 2, 10) / 8.37e6 - 1) < 0.03
+    r = JsonLinesReporter(tmp_path / "m" / "metrics.jsonl")
+    algo = SimpleNamespace(samples=4000, world=1, D=6, H=256, A=2, precision="sf16",
+                           config=SimpleNamespace(num_sgd_iter=10))
+    res = {"training_iteration": 3, "timesteps_total": 12000, "episode_reward_mean": 4765.2,
+           "episode_reward_mean_this_iter": float("nan"), "episodes_this_iter": 40, "episodes_total": 120,
+           "time_this_iter_s": 0.5,
+           "info": {"learner": {"default_policy": {"learner_stats": {"policy_loss": -0.01, "kl": 0.002}}}}}
+    for _ in range(2):
+        r.report(res, algo)
+    lines = (tmp_path / "m" / "metrics.jsonl").read_text().splitlines()
+    assert len(lines) == 2
+    rec = json.loads(lines[0])
+    assert rec["training_iteration"] == 3 and rec["episode_reward_mean"] == 4765.2
+    assert rec["episode_reward_mean_this_iter"] is None      # NaN is not JSON
+    assert rec["env_steps_per_s"] == 8000.0 and rec["learner"]["kl"] == 0.002
+    assert 0 < rec["frac_sf16_mfma_ceiling"] < 1
+    quiet = JsonLinesReporter(tmp_path / "rank1.jsonl", rank=1)
+    quiet.report(res, algo)
+    assert not (tmp_path / "rank1.jsonl").exists()

@@ -20,6 +20,7 @@ import numpy as np
 import pytest
 
 import oracle
+from parity import grad_close_as_fp32
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -264,7 +265,8 @@ def test_checkpoint_resume_is_exact(tmp_path, kind):
 def test_c4_shard_rollout_and_gradient():
     """BASELINE configs[3] per GPU: 131,072 lanes.  A 4-step fused rollout replays bit-exactly in
     the oracle (actions re-drawn from the logits), then one SGD gradient on a gathered 65,536-row
-    minibatch matches the fp64 oracle norm-wise to 1e-5 per tensor"""
+    minibatch matches the fp64 oracle norm-wise to 1e-5 per tensor and, per element, no worse than
+    torch-CPU fp32 by 4x (tests/parity.py)"""
     from rlks import _lib
     from rlks.policy import TENSOR_NAMES
     from rlks.ppo import PPO
@@ -287,10 +289,14 @@ def test_c4_shard_rollout_and_gradient():
     eg, _ = oracle.ppo_loss_grad(algo.params.flat.cpu().numpy(), algo.params.offsets, 6, 256, 2,
                                  algo.mbuf.cpu().numpy(), kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]),
                                  adv_inv_std=float(dyn[1]))
+    eg32, _ = oracle.ppo_loss_grad(algo.params.flat.cpu().numpy(), algo.params.offsets, 6, 256, 2,
+                                   algo.mbuf.cpu().numpy(), kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]),
+                                   adv_inv_std=float(dyn[1]), dtype=np.float32)
     g = algo.grad.cpu().numpy()
     for i, (name, _, _) in enumerate(TENSOR_NAMES):
         o, n_ = algo.params.offsets[i], int(np.prod(algo.params.shapes[i]))
         assert np.linalg.norm(g[o:o + n_] - eg[o:o + n_]) <= 1e-5 * np.linalg.norm(eg[o:o + n_]) + 1e-12, name
+    grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes)
 
 
 # ----------------------------------------------------------------------------- c5 node env
@@ -465,3 +471,54 @@ def test_restore_rejects_another_world_size(tmp_path):
     (path / "algorithm_state.json").write_text(json.dumps(meta))
     with pytest.raises(ValueError, match="rank"):
         a.restore(path)
+
+
+def test_run_experiment_checkpoints_and_latest(tmp_path, monkeypatch):
+    """train_final.py's Tune run shape (stop at N iterations, checkpoint every k, keep the newest
+    few, one at the end) -> final_evaluation.py:13-25's discovery (highest checkpoint number under
+    ~/ray_results/FINAL_PPO_AWS_AZURE) -> PPO.from_checkpoint resumes those weights; save() with
+    no directory lands in the run's logdir under the same root; the JSON-lines reporter writes one
+    line per train()"""
+    from rlks.checkpoints import latest_checkpoint, run_experiment
+    from rlks.metrics import JsonLinesReporter
+    from rlks.ppo import PPO
+
+    d = _dev()
+    monkeypatch.setenv("RLKS_RESULTS_DIR", str(tmp_path / "ray_results"))
+    cfg = _cfg(256, 16, 1024, epochs=1, seed=9)
+    rep = JsonLinesReporter(tmp_path / "metrics.jsonl")
+    out = run_experiment(cfg, name="FINAL_PPO_AWS_AZURE", stop_iterations=5, checkpoint_frequency=2, num_to_keep=2,
+                         checkpoint_at_end=True, reporter=rep, device=d)
+    kept = [Path(p).name for p in out["checkpoints"]]
+    assert kept == ["checkpoint_000004", "checkpoint_000005"], kept
+    assert not (Path(out["trial_dir"]) / "checkpoint_000002").exists()   # num_to_keep removed it
+    best = latest_checkpoint(name="FINAL_PPO_AWS_AZURE")
+    assert best is not None and best.name == "checkpoint_000005"
+    algo = PPO.from_checkpoint(str(best), device=d)
+    assert algo.iteration == 5 and torch.equal(algo.params.flat, out["algo"].params.flat)
+    lines = [json.loads(x) for x in (tmp_path / "metrics.jsonl").read_text().splitlines()]
+    assert [x["training_iteration"] for x in lines] == [1, 2, 3, 4, 5]
+    assert all(x["env_steps_per_s"] > 0 for x in lines)
+    p = Path(algo.save())   # no directory: RLlib-style logdir under the results root
+    assert p.parent.parent == tmp_path / "ray_results" and p.parent.name.startswith("PPO_K8sMultiCloudEnv_")
+    assert latest_checkpoint(tmp_path / "ray_results") is not None
+
+
+def test_restore_warns_without_env_state(tmp_path):
+    """node-level envs save no env state by default (checkpoint_env_state None): restore() says
+    that the resumed run is not an exact continuation"""
+    from rlks.env import NodeSpec
+    from rlks.ppo import PPO
+    from rlks.tables import synthetic_table
+
+    d = _dev()
+    cfg = _cfg(256, 8, 1024, epochs=1, seed=4)
+    cfg.table = synthetic_table(4, 100, seed=3)
+    cfg.nodes = NodeSpec(4, 16, arrival_rate=2.0, depart_prob=0.05)
+    a = PPO(config=cfg, device=d)
+    a.train()
+    path = a.save(tmp_path)
+    meta = json.loads((Path(path) / "algorithm_state.json").read_text())
+    assert meta["state"]["env_state_saved"] is False
+    with pytest.warns(RuntimeWarning, match="exact continuation"):
+        PPO.from_checkpoint(path, device=d)

@@ -5,7 +5,11 @@ Tolerances (north star: "rewards, advantages and gradients within 1e-5 relative"
   - elementwise outputs (GAE, forward logits/values, Adam): |x - ref| <= 1e-5 * |ref| + atol with
     atol = 1e-5 * max|ref| (fp32 accumulation over K = 256 or T = 128 terms);
   - gradients (sums over the minibatch rows): per tensor, ||g - ref||_2 <= 1e-5 * ||ref||_2 and
-    elementwise |g - ref| <= 1e-5 * max|ref| + 1e-5 * |ref|.
+    elementwise |g - ref| <= 1e-5 * max|ref| + 1e-5 * |ref|;
+  - and, for every fp32 output above, per element (tests/parity.py): over the elements with
+    |ref| > 1e-6 max|ref|, the relative error against fp64 no worse than a float32 reference of the
+    same computation (torch-CPU fp32 / the serial fp32 recurrence) by 4x at p50, p99, p99.9 and the
+    maximum, so a near-zero element cannot hide behind max|ref|.
 """
 import ctypes as C
 
@@ -13,6 +17,7 @@ import numpy as np
 import pytest
 
 import oracle
+from parity import close_as_fp32, gae_fp32_serial, grad_close_as_fp32, logp_of
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -31,35 +36,6 @@ def close(x, ref, rtol=1e-5):
     err = np.abs(x - ref)
     ok = err <= rtol * np.abs(ref) + atol
     assert ok.all(), f"max err {err.max():.3e} vs max|ref| {np.abs(ref).max():.3e}"
-
-
-def gae_fp32_serial(r, v, dn, gamma, lam):
-    """the plain float32 backward recurrence (RLlib's discount_cumsum evaluated in the rollout's
-    float32): delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t, A_t = delta_t + gamma lam (1 - d_t) A_{t+1}"""
-    T = r.shape[0]
-    f = np.float32
-    adv = np.zeros(r.shape, f)
-    a = np.zeros(r.shape[1:], f)
-    g, gl = f(gamma), f(gamma * lam)
-    for t in range(T - 1, -1, -1):
-        nd = (1 - dn[t]).astype(f)
-        delta = (r[t] + g * v[t + 1] * nd - v[t]).astype(f)
-        a = (delta + gl * nd * a).astype(f)
-        adv[t] = a
-    return adv, (adv + v[:T]).astype(f)
-
-
-def close_as_fp32(x, ref64, ref32, factor=4.0, floor=1e-6):
-    """element-wise relative error of x against the float64 reference, over the elements with
-    |ref| > floor max|ref|, no worse than the float32 reference's by `factor` at the 50th, 99th and
-    99.9th percentiles and at the maximum (a near-zero element cannot hide behind max|ref|)"""
-    x, ref64, ref32 = (np.asarray(a, np.float64).ravel() for a in (x, ref64, ref32))
-    keep = np.abs(ref64) > floor * np.abs(ref64).max()
-    e = np.abs(x - ref64)[keep] / np.abs(ref64[keep])
-    e32 = np.abs(ref32 - ref64)[keep] / np.abs(ref64[keep])
-    for q in (50, 99, 99.9, 100):
-        a, b = np.percentile(e, q), np.percentile(e32, q)
-        assert a <= factor * b + 1e-9, f"p{q}: {a:.3e} vs fp32 {b:.3e}"
 
 
 # ----------------------------------------------------------------------------- GAE
@@ -139,8 +115,11 @@ def test_policy_forward_matches_oracle(n):
     lg, v = p.forward(torch.from_numpy(obs).to(d))
     flat = p.flat.cpu().numpy()
     el, ev = oracle.mlp_forward(flat, p.offsets, 6, 256, 2, obs)
+    fl, fv = oracle.mlp_forward(flat, p.offsets, 6, 256, 2, obs, dtype=np.float32)
     close(lg.cpu().numpy(), el)
     close(v.cpu().numpy(), ev)
+    close_as_fp32(lg.cpu().numpy(), el, fl, what="logits")
+    close_as_fp32(v.cpu().numpy(), ev, fv, what="values")
 
 
 def _minibatch(rows, rng, D=6, A=2, p=None, d=None):
@@ -191,6 +170,9 @@ def test_ppo_grad_matches_oracle(rows, A, precision):
     g = grad.cpu().numpy()
     eg, est = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, 256, A, mb, entropy_coeff=0.01,
                                    kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd)
+    eg32, _ = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, 256, A, mb, entropy_coeff=0.01,
+                                   kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd, dtype=np.float32)
+    grad_close_as_fp32(g, eg, eg32, p.offsets, p.shapes)
     from rlks.policy import TENSOR_NAMES
 
     for i, (name, _, _) in enumerate(TENSOR_NAMES):
@@ -235,6 +217,9 @@ def test_wide_grad_matches_oracle(rows, D, H, A):
     g = grad.cpu().numpy()
     eg, est = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, H, A, mb, entropy_coeff=0.01,
                                    kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd)
+    eg32, _ = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, H, A, mb, entropy_coeff=0.01,
+                                   kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd, dtype=np.float32)
+    grad_close_as_fp32(g, eg, eg32, p.offsets, p.shapes)
     from rlks.policy import TENSOR_NAMES
 
     for i, (name, _, _) in enumerate(TENSOR_NAMES):
@@ -257,8 +242,11 @@ def test_wide_forward_matches_oracle(n, D, H, A):
     obs = rng.random((n, D)).astype(np.float32)
     lg, v = p.forward(torch.from_numpy(obs).to(d))
     el, ev = oracle.mlp_forward(p.flat.cpu().numpy(), p.offsets, D, H, A, obs)
+    fl, fv = oracle.mlp_forward(p.flat.cpu().numpy(), p.offsets, D, H, A, obs, dtype=np.float32)
     close(lg.cpu().numpy(), el)
     close(v.cpu().numpy(), ev)
+    close_as_fp32(lg.cpu().numpy(), el, fl, what="logits")
+    close_as_fp32(v.cpu().numpy(), ev, fv, what="values")
 
 
 def test_adam_matches_torch():
@@ -532,21 +520,22 @@ def test_ppo_iteration_parity_and_surface(tmp_path):
         np.testing.assert_array_equal(o.view(np.uint32), b["obs"][t + 1].view(np.uint32))
         np.testing.assert_array_equal(r.astype(np.float32).view(np.uint32), b["rewards"][t].view(np.uint32))
         np.testing.assert_array_equal(term, b["dones"][t])
-    # logp consistent with the stored logits
-    lo = b["logits"].astype(np.float64)
-    lsm = lo - np.log(np.exp(lo - lo.max(-1, keepdims=True)).sum(-1, keepdims=True)) - lo.max(-1, keepdims=True)
-    close(np.take_along_axis(lsm, b["actions"][..., None].astype(int), -1)[..., 0], b["logp"], 1e-5)
-    # logits and values of visited observations recomputed by the oracle
+    # logp consistent with the stored logits (per element, against fp64 and fp32 log-softmax)
+    close_as_fp32(b["logp"], logp_of(b["logits"], b["actions"]), logp_of(b["logits"], b["actions"], np.float32),
+                  what="logp")
+    # logits and values of visited observations recomputed by the oracle (fp64, and torch fp32)
     flat = algo.params.flat.cpu().numpy()
     for t in (0, 57, T):
         el, ev = oracle.mlp_forward(flat, algo.params.offsets, 6, 256, 2, b["obs"][t])
-        close(b["values"][t], ev)
+        fl, fv = oracle.mlp_forward(flat, algo.params.offsets, 6, 256, 2, b["obs"][t], dtype=np.float32)
+        close_as_fp32(b["values"][t], ev, fv, what=f"values[{t}]")
         if t < T:
-            close(b["logits"][t], el)
+            close_as_fp32(b["logits"][t], el, fl, what=f"logits[{t}]")
     algo.advantages()
     ea, evt = oracle.gae(b["rewards"], b["values"], b["dones"], 0.99, 1.0)
-    close(algo.buf["adv"].cpu().numpy(), ea)
-    close(algo.buf["vtarg"].cpu().numpy(), evt)
+    fa, fvt = gae_fp32_serial(b["rewards"], b["values"], b["dones"], 0.99, 1.0)
+    close_as_fp32(algo.buf["adv"].cpu().numpy(), ea, fa, what="adv")
+    close_as_fp32(algo.buf["vtarg"].cpu().numpy(), evt, fvt, what="vtarg")
     # one SGD step: gradient vs oracle on the gathered minibatch
     _lib.call("rlks_ppo_gather", C.byref(algo.params.desc), C.byref(algo.bufs), 5, 0, 0, algo.mb,
               algo.dyn.data_ptr(), algo.mbuf.data_ptr(), None)
@@ -556,10 +545,12 @@ def test_ppo_iteration_parity_and_surface(tmp_path):
     _lib.call("rlks_ppo_grad", C.byref(algo.params.desc), C.byref(algo.coeffs), algo.params.flat.data_ptr(),
               algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, wsb.data_ptr(),
               wsb.numel(), None)
-    eg, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 6, 256, 2, mb, kl_coeff=float(dyn[2]),
-                                 adv_mean=float(dyn[0]), adv_inv_std=float(dyn[1]))
+    kw = dict(kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]), adv_inv_std=float(dyn[1]))
+    eg, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 6, 256, 2, mb, **kw)
+    eg32, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 6, 256, 2, mb, dtype=np.float32, **kw)
     g = algo.grad.cpu().numpy()
     assert np.linalg.norm(g - eg) <= 1e-5 * np.linalg.norm(eg)
+    grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes)
     # full iterations through the RLlib-named surface
     r1 = algo.train()
     r2 = algo.train()

@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
+from parity import close_as_fp32, gae_fp32_serial, grad_close_as_fp32, logp_of
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -108,13 +109,6 @@ def test_nodes_full_c3_size():
 
 
 # ----------------------------------------------------------------------------- PPO on node envs
-def _close(x, ref, rtol=1e-5):
-    x = np.asarray(x, np.float64)
-    ref = np.asarray(ref, np.float64)
-    err = np.abs(x - ref)
-    assert (err <= rtol * np.abs(ref) + rtol * max(1e-30, float(np.abs(ref).max()))).all(), f"max err {err.max():.3e}"
-
-
 @pytest.mark.parametrize("C,nodes,H,N,T,mb,precision", [
     (8, 64, 256, 2048, 24, 8192, "auto"),    # c3 shape (obs 24, 8 actions), split-fp16 rollout forward
     (8, 64, 256, 1024, 16, 4096, "fp32"),    # same env, fp32-MFMA rollout forward
@@ -152,20 +146,20 @@ def test_ppo_on_node_envs(C, nodes, H, N, T, mb, precision):
         np.testing.assert_array_equal(o.view(np.uint32), b["obs"][t + 1].view(np.uint32))
         np.testing.assert_array_equal(r.astype(np.float32).view(np.uint32), b["rewards"][t].view(np.uint32))
         np.testing.assert_array_equal(term, b["dones"][t])
-    lo = b["logits"].astype(np.float64)
-    mx = lo.max(-1, keepdims=True)
-    lsm = lo - mx - np.log(np.exp(lo - mx).sum(-1, keepdims=True))
-    _close(np.take_along_axis(lsm, b["actions"][..., None].astype(int), -1)[..., 0], b["logp"])
+    close_as_fp32(b["logp"], logp_of(b["logits"], b["actions"]), logp_of(b["logits"], b["actions"], np.float32),
+                  what="logp")
     flat = algo.params.flat.cpu().numpy()
     for t in (0, T // 2, T):
         el, ev = oracle.mlp_forward(flat, algo.params.offsets, 3 * C, H, C, b["obs"][t])
-        _close(b["values"][t], ev)
+        fl, fv = oracle.mlp_forward(flat, algo.params.offsets, 3 * C, H, C, b["obs"][t], dtype=np.float32)
+        close_as_fp32(b["values"][t], ev, fv, what=f"values[{t}]")
         if t < T:
-            _close(b["logits"][t], el)
+            close_as_fp32(b["logits"][t], el, fl, what=f"logits[{t}]")
     algo.advantages()
     ea, evt = oracle.gae(b["rewards"], b["values"], b["dones"], 0.99, 1.0)
-    _close(algo.buf["adv"].cpu().numpy(), ea)
-    _close(algo.buf["vtarg"].cpu().numpy(), evt)
+    fa, fvt = gae_fp32_serial(b["rewards"], b["values"], b["dones"], 0.99, 1.0)
+    close_as_fp32(algo.buf["adv"].cpu().numpy(), ea, fa, what="adv")
+    close_as_fp32(algo.buf["vtarg"].cpu().numpy(), evt, fvt, what="vtarg")
     _lib.call("rlks_ppo_gather", C_.byref(algo.params.desc), C_.byref(algo.bufs), 3, 0, 0, algo.mb,
               algo.dyn.data_ptr(), algo.mbuf.data_ptr(), None)
     mbh = algo.mbuf.cpu().numpy()
@@ -173,11 +167,69 @@ def test_ppo_on_node_envs(C, nodes, H, N, T, mb, precision):
     _lib.call("rlks_ppo_grad", C_.byref(algo.params.desc), C_.byref(algo.coeffs), algo.params.flat.data_ptr(),
               algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, algo.ws.data_ptr(),
               algo.ws.numel(), None)
-    eg, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 3 * C, H, C, mbh, kl_coeff=float(dyn[2]),
-                                 adv_mean=float(dyn[0]), adv_inv_std=float(dyn[1]))
+    kw = dict(kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]), adv_inv_std=float(dyn[1]))
+    eg, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 3 * C, H, C, mbh, **kw)
+    eg32, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 3 * C, H, C, mbh, dtype=np.float32, **kw)
     g = algo.grad.cpu().numpy()
     assert np.linalg.norm(g - eg) <= 1e-5 * np.linalg.norm(eg)
+    grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes)
     for _ in range(2):
         r = algo.train()
         assert np.isfinite(r["info"]["learner"]["default_policy"]["learner_stats"]["policy_loss"])
     assert bool(torch.isfinite(algo.params.flat).all())
+
+
+def test_node_rollout_full_c3_size():
+    """BASELINE configs[2] through the agent: PPO.rollout over 65,536 envs x 8 clusters x 256 nodes
+    (bench.py's c3 env: Poisson(1) arrivals, stationary departures), T = 4 steps of node_rollout
+    (forward of both nets -> Categorical sample -> node step).  Every transition replays bit-exactly
+    in the C oracle fed the rollout's actions (obs, f32 rewards, dones, and every node's free cpu /
+    mem at the end); every sampled action equals the Philox inverse-CDF draw recomputed on the CPU
+    from the stored logits (up to draws within 4 float32 ulp of a CDF boundary, bounded at 1e-4);
+    logits / values / logp per element against fp64 and fp32 references (tests/parity.py)"""
+    from bench import env_setup
+    from rlks.ppo import PPO, PPOConfig
+
+    d = _dev()
+    N, T, seed = 65536, 4, 42
+    tab, spec = env_setup("c3")
+    cfg = (PPOConfig().framework("torch")
+           .training(train_batch_size=N * T, sgd_minibatch_size=65536, num_sgd_iter=1, lr=3e-4, gamma=0.99)
+           .debugging(seed=seed))
+    cfg.num_envs, cfg.table, cfg.nodes = N, tab, spec
+    cfg.rollout_fragment_length = T
+    algo = PPO(config=cfg, device=d)
+    assert algo.T == T and algo.D == 24 and algo.A == 8 and algo.precision == "sf16"
+    algo.rollout(explore=True)
+    b = {k: v.cpu().numpy() for k, v in algo.buf.items()}
+    ora = oracle.OracleEnv(oracle.make_cfg(N, tab.n_rows, 8, noise_mode=0, seed=seed, autoreset=1, nodes=256,
+                                           arrival_rate=spec.arrival_rate, depart_prob=spec.depart_prob,
+                                           init_occupancy=spec.init_occupancy, reject_penalty=spec.reject_penalty),
+                           tab.cost, tab.latency, spec.node_cpu_m, spec.node_mem_mi, None)
+    np.testing.assert_array_equal(ora.reset().view(np.uint32), b["obs"][0].view(np.uint32))
+    gids = np.arange(N)
+    amb = 0
+    for t in range(T):
+        st, ep = ora.lane_counters()
+        act, margin = oracle.sample_actions(b["logits"][t], gids, ep, st, seed)
+        near = margin < 4.0
+        amb += int(near.sum())
+        bad = (act != b["actions"][t]) & ~near
+        assert not bad.any(), f"t={t}: {int(bad.sum())} sampled actions differ from the Philox inverse CDF"
+        o, r, term, _, _, _ = ora.step(b["actions"][t])
+        np.testing.assert_array_equal(o.view(np.uint32), b["obs"][t + 1].view(np.uint32))
+        np.testing.assert_array_equal(r.astype(np.float32).view(np.uint32), b["rewards"][t].view(np.uint32))
+        np.testing.assert_array_equal(term, b["dones"][t])
+    assert amb <= 1e-4 * N * T, amb
+    assert len(np.unique(b["actions"])) == 8
+    _compare_state(algo.env, ora)
+    close_as_fp32(b["logp"], logp_of(b["logits"], b["actions"]), logp_of(b["logits"], b["actions"], np.float32),
+                  what="logp")
+    flat = algo.params.flat.cpu().numpy()
+    rows = slice(0, 16384)   # a quarter of the lanes: the fp64 / fp32 CPU forwards stay in seconds
+    for t in (0, T):
+        el, ev = oracle.mlp_forward(flat, algo.params.offsets, 24, 256, 8, b["obs"][t][rows])
+        fl, fv = oracle.mlp_forward(flat, algo.params.offsets, 24, 256, 8, b["obs"][t][rows], dtype=np.float32)
+        close_as_fp32(b["values"][t][rows], ev, fv, what=f"values[{t}]")
+        if t < T:
+            close_as_fp32(b["logits"][t][rows], el, fl, what=f"logits[{t}]")
