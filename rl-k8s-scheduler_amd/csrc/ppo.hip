@@ -454,12 +454,14 @@ struct SfWs {
   float* pmax_roll[2];  // the rollout's weight-max slots (the SGD steps' pmax keeps its parity state)
   int64_t bytes, weight_bytes;
   int blocks, splits, tiles_per_split;
+  int fa_parts;  // F1a's dW3 / db3 / stats partials per net (sf_f1a_parts <= blocks)
 };
 
 static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   SfWs w{};
   const int KD = sf_kd(D), tiles = M / 32;  // F2's 32-row tiles
   w.blocks = M / (16 * SF_F1_W);  // F1 workgroups of SF_F1_W x 16 rows
+  w.fa_parts = sf_f1a_parts(M, A);
   w.splits = 1;
   constexpr int F2_MAX_SPLITS = 128;  // F2 row splits per net (one 512-thread workgroup each)
   while (w.splits * 2 <= F2_MAX_SPLITS && tiles % (w.splits * 2) == 0) w.splits *= 2;
@@ -809,11 +811,11 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     R.add(n.part_b1, grad + o[1], nullptr, H, w.blocks, H, 2 * net + 1);
     R.add(n.part_w2, grad + o[2], nullptr, SF_W2_PSTRIDE, w.splits, H * H, 2 * net);
     R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
-    R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, w.blocks, An * H);
-    R.add(n.part_b3, grad + o[5], nullptr, An, w.blocks, An);
+    R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, w.fa_parts, An * H);
+    R.add(n.part_b3, grad + o[5], nullptr, An, w.fa_parts, An);
   }
   if (stats) {  // per-block columns [policy loss, vf loss, kl, entropy] -> RLKS_STAT_* directly
-    const int tiles = w.blocks;
+    const int tiles = w.fa_parts;
     R.add(w.n[0].part_stat + 0, nullptr, stats + RLKS_STAT_POLICY_LOSS, 4, tiles, 1);
     R.add(w.n[1].part_stat + 1, nullptr, stats + RLKS_STAT_VF_LOSS, 4, tiles, 1);
     R.add(w.n[0].part_stat + 2, nullptr, stats + RLKS_STAT_KL, 4, tiles, 1);

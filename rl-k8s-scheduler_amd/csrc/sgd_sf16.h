@@ -43,7 +43,7 @@ struct SfNet {
   int* tile_edz;  // [M/16]: each 16-row tile's dZ2 split exponent (F1a -> F1b, F2)
   int* tile_ex;   // [M/16]: each 16-row tile's X split exponent (F1a -> F2)
   float *part_w1, *part_b1;                 // [F1 blocks of 128 rows][...] (F1b)
-  float *part_w3, *part_b3, *part_stat;     // [F1 blocks of 128 rows][...] (F1a)
+  float *part_w3, *part_b3, *part_stat;     // [sf_f1a_parts][...] (F1a)
   float *part_w2, *part_b2;                                   // [splits][...]
 };
 struct SfArgs {
@@ -86,5 +86,7 @@ int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
 // halves: 1 = F1a (k_sf_fwd), 2 = F1b (k_sf_bwd), 3 = both
 int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int halves = 3);  // needs M % 256 == 0
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
+// F1a's partials of dW3 / db3 / stats per net (the warp-specialised F1a writes one per workgroup)
+int sf_f1a_parts(int M, int A);
 
 }  // namespace rlks

@@ -92,7 +92,7 @@ def run_experiment(config, *, name: str = "FINAL_PPO_AWS_AZURE", stop_iterations
     while algo.iteration < stop_iterations:
         result = algo.train()
         if reporter is not None:
-            reporter.report(result)
+            reporter.report(result, algo)
         if checkpoint_frequency and algo.iteration % checkpoint_frequency == 0:
             save()
     if checkpoint_at_end and (not kept or checkpoint_number(kept[-1]) != algo.iteration):

@@ -232,6 +232,19 @@ class DeviceEnv:
             raise ValueError(f"env state snapshot has {buf.numel()} bytes, this env needs {self.state_bytes()}")
         _lib.call("rlks_env_load_state", self.handle, _lib.ptr(buf), self.stream)
 
+    def node_state(self):
+        """(free_cpu [N, C, nodes], free_mem [N, C, nodes], used_cpu [N, C]) int32 device tensors of a
+        node-level env (rlks_env_node_state)"""
+        torch = self.torch
+        if self.nodes is None:
+            raise ValueError("node_state: this env has no node-level state")
+        n, C_, k = self.n, self.cfg.n_clouds, self.nodes.nodes_per_cluster
+        fc = torch.empty(n, C_, k, dtype=torch.int32, device=self.device)
+        fm = torch.empty(n, C_, k, dtype=torch.int32, device=self.device)
+        used = torch.empty(n, C_, dtype=torch.int32, device=self.device)
+        _lib.call("rlks_env_node_state", self.handle, _lib.ptr(fc), _lib.ptr(fm), _lib.ptr(used), self.stream)
+        return fc, fm, used
+
     def episode_log(self, clear=True):
         """(returns f64 [k], keys i64 [k], total count) of the episodes completed since the last
         clear, k = min(total, RLKS_EPLOG_CAP), in completion order (sorted by episode, lane)"""
@@ -472,13 +485,7 @@ class VecK8sMultiCloudEnv:
 
     def node_state(self):
         """(free_cpu [N, C, nodes], free_mem [N, C, nodes], used_cpu [N, C]) int32 device tensors"""
-        torch = _torch()
-        n, C_, k = self.num_envs, self.n_clouds, self.nodes.nodes_per_cluster
-        fc = torch.empty(n, C_, k, dtype=torch.int32, device=self.device)
-        fm = torch.empty(n, C_, k, dtype=torch.int32, device=self.device)
-        used = torch.empty(n, C_, dtype=torch.int32, device=self.device)
-        _lib.call("rlks_env_node_state", self.handle, _lib.ptr(fc), _lib.ptr(fm), _lib.ptr(used), self.dev.stream)
-        return fc, fm, used
+        return self.dev.node_state()
 
     def counters(self, enable=-1):
         """[node checks, pods placed, pods rejected, pods departed, node write-backs, node reads] since

@@ -11,6 +11,9 @@ a near-zero element cannot hide behind max|ref|.
 import numpy as np
 
 QS = (50, 99, 99.9, 100)
+# an fp32 result is not asked to beat ~2 ulp of relative error per element (a tiny sample's fp32
+# reference can be exact by chance)
+ULP2 = 2.0 ** -22
 
 
 def rel_errors(x, ref64, ref32, floor=1e-6):
@@ -27,7 +30,7 @@ def assert_pcts(e, e32, factor=4.0, what=""):
         return
     for q in QS:
         a, b = np.percentile(e, q), np.percentile(e32, q)
-        assert a <= factor * b + 1e-9, f"{what} p{q}: {a:.3e} vs fp32 {b:.3e}"
+        assert a <= factor * b + ULP2, f"{what} p{q}: {a:.3e} vs fp32 {b:.3e}"
 
 
 def close_as_fp32(x, ref64, ref32, factor=4.0, floor=1e-6, what=""):
@@ -37,17 +40,22 @@ def close_as_fp32(x, ref64, ref32, factor=4.0, floor=1e-6, what=""):
     assert_pcts(e, e32, factor, what)
 
 
-def grad_close_as_fp32(g, g64, g32, offsets, shapes, factor=4.0, floor=1e-6):
-    """close_as_fp32 per parameter tensor (the floor is relative to each tensor's own max), plus
-    the pooled percentiles over all tensors"""
+def grad_close_as_fp32(g, g64, g32, offsets, shapes, factor=4.0, floor=1e-6, tensor_max_factor=10.0):
+    """the gradient form of test_sf16_gradient_per_element: over all parameter tensors pooled (the
+    floor relative to each tensor's own max), the relative error no worse than the fp32 reference's
+    by `factor` at p50 / p99 / p99.9 and the maximum; per tensor, p99 within `factor` (tensors of at
+    least 100 elements) and the maximum within `tensor_max_factor` (one worst element of a small
+    tensor is a noisy statistic for both precisions)"""
     es, e32s = [], []
     for i, shp in enumerate(shapes):
         o, n = offsets[i], int(np.prod(shp))
         e, e32 = rel_errors(g[o:o + n], g64[o:o + n], g32[o:o + n], floor)
-        # per tensor: the maximum and the 99th percentile (small tensors have no meaningful 99.9th)
         if e.size:
-            assert e.max() <= factor * e32.max() + 1e-9, f"tensor {i} max: {e.max():.3e} vs fp32 {e32.max():.3e}"
-            assert np.percentile(e, 99) <= factor * np.percentile(e32, 99) + 1e-9, f"tensor {i} p99"
+            assert e.max() <= tensor_max_factor * e32.max() + ULP2, \
+                f"tensor {i} max: {e.max():.3e} vs fp32 {e32.max():.3e}"
+            if e.size >= 100:
+                assert np.percentile(e, 99) <= factor * np.percentile(e32, 99) + ULP2, \
+                    f"tensor {i} p99: {np.percentile(e, 99):.3e} vs fp32 {np.percentile(e32, 99):.3e}"
         es.append(e)
         e32s.append(e32)
     assert_pcts(np.concatenate(es), np.concatenate(e32s), factor, "pooled")
