@@ -337,7 +337,8 @@ def node_env_timing(algo, torch, timed, n=65536, C=8, nodes=256, depart_prob="st
            "departed_per_step": departed, "nodes_written_per_step": written, "chunks_read_per_step": chunks,
            "bytes_per_step": algo_bytes, "GBps": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
            "survey_bytes_per_step": survey_bytes,
-           "frac_hbm_survey_bytes": survey_bytes * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+           "survey_bytes_note": "SURVEY §8(d)'s 2,169 B/env-step assumed a sweep of the chosen cluster's nodes; the "
+                                "chunk-indexed step does not move those bytes, so no fraction is quoted on them"}
     pmc = pmc_traffic()
     if pmc and "k_node_step" in pmc and (n, C, nodes) == (65536, 8, 256) and depart_prob == "stationary":
         res["traffic"] = pmc["k_node_step"]["hbm_bytes_per_launch"]
@@ -357,27 +358,30 @@ def cpu_threads() -> int:
 
 
 def mfma_calibration(torch, sf16_tflops):
-    """what this chip's f16 MFMA pipes deliver on a large plain GEMM through the vendor library
-    (torch.matmul -> hipBLASLt, f16 65536 x 2048 x 2048, random data), measured live after the timed
-    region, against the dominant kernel's f16 MFMA rate (3 f16 products per fp32-accurate FLOP).  The
-    2.5 PF spec is not held under dense MFMA load (MI355X_MICROARCH.md, DVFS give-back)."""
+    """what this chip's f16 MFMA pipes sustain on random operands, measured live in this process after
+    the timed region (librlks_calib.so: one wave per SIMD on every CU, eight independent accumulators,
+    back-to-back issue), for the two shapes the SGD kernels use, against the dominant kernel's f16
+    MFMA rate (3 f16 products per fp32-accurate FLOP).  The 2.5 PF spec is not held under dense MFMA
+    load on random data (MI355X_MICROARCH.md, DVFS give-back)."""
+    lib = C.CDLL(str(ROOT / "rl-k8s-scheduler_amd" / "rlks" / "librlks_calib.so"))
+    lib.rlks_calib_mfma_f16.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.POINTER(C.c_double)]
     dev = torch.device("cuda", torch.cuda.current_device())
-    a = torch.randn(65536, 2048, device=dev, dtype=torch.float16)
-    b = torch.randn(2048, 2048, device=dev, dtype=torch.float16)
-    for _ in range(3):
-        c = a @ b
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        c = a @ b
-    e1.record()
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / 10
-    lib = 2 * 65536 * 2048 * 2048 / (ms * 1e-3) / 1e12
-    del a, b, c
-    return {"hipblaslt_f16_tflops": lib, "shape": "f16 65536x2048x2048 (torch.matmul)",
-            "kernel_f16_mfma_tflops": 3 * sf16_tflops, "frac_of_hipblaslt": 3 * sf16_tflops / lib}
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    g = torch.Generator(device=dev).manual_seed(11)
+    rnd = (torch.rand(1 << 20, generator=g, device=dev) * 2 - 1).to(torch.float16)
+    out = torch.empty(cus * 256, device=dev)
+    s = torch.cuda.current_stream()
+    res = {"cus": cus, "operands": "random fp16 in [-1, 1]"}
+    for shape, name in ((0, "mfma_f32_16x16x32_f16"), (1, "mfma_f32_32x32x16_f16")):
+        tf = C.c_double()
+        rc = lib.rlks_calib_mfma_f16(shape, cus, 10000, 5, rnd.data_ptr(), out.data_ptr(), s.cuda_stream, C.byref(tf))
+        res[name + "_tflops"] = tf.value if rc == 0 else None
+    sustained = res["mfma_f32_16x16x32_f16_tflops"]
+    res["kernel_f16_mfma_tflops"] = 3 * sf16_tflops
+    res["frac_of_sustained_16x16x32"] = 3 * sf16_tflops / sustained if sustained else None
+    res["sf16_ceiling_sustained_tflops"] = sustained / 3 if sustained else None
+    return res
 
 
 def pmc_traffic():
@@ -488,6 +492,17 @@ def main():
                 roofline["traffic_source"] = pmc["source"]
                 if ab:
                     roofline["traffic_over_algorithmic"] = roofline["traffic"] / ab
+            if pmc and args.config in ("c2", "c4") and algo.precision == "sf16":
+                # the whole SGD step against its compulsory bytes: the minibatch records read once, the
+                # parameters read by the weight split, and Adam (p, m, v read + written, the gradient
+                # written and read): everything else is a hand-off between the step's own kernels
+                step = [k for k in ("k_sf_split", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce") if k in pmc]
+                moved = sum(pmc[k]["hbm_bytes_per_launch"] for k in step)
+                P = algo.params.padded
+                comp = algo.mb * algo.stride * 4 + P * 4 + (6 + 2) * P * 4
+                roofline["sgd_step"] = {"traffic": moved, "kernels": step, "compulsory_bytes": comp,
+                                        "traffic_over_compulsory": moved / comp,
+                                        "floor_us_at_6p3TBps": moved / 6.3e12 * 1e6}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             sys.path.insert(0, str(ROOT / "oracle"))

@@ -313,6 +313,17 @@ int rlks_ppo_grad_step_next(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* co
                             const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
                             int step, int prev_fused, const rlks_gather_next* next, void* workspace,
                             int64_t ws_bytes, void* stream);
+/* rlks_ppo_grad_step_next in two parts, so that the caller's all-reduce of part 1's gradient buckets
+ * runs under part 2's kernels: part 1 = the weight split, the forward / loss kernel (F1a), dW2 / db2
+ * (F2) and the reduce of W2, b2, W3, b3 (both nets) and the stats; part 2 = the dH1 / dW1 kernel
+ * (F1b) and the reduce of W1, b1 (+ the next gather, `next` is read by part 2 only).  The gradient
+ * equals rlks_ppo_grad_step's bit for bit.  Buckets (offsets of rlks_mlp_layout): part 1 =
+ * [off[2], off[6]) and [off[8], padded), part 2 = [off[0], off[2]) and [off[6], off[8]).  Other
+ * precisions: the whole gradient in part 1, part 2 only gathers. */
+int rlks_ppo_grad_step_part(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
+                            const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
+                            int step, int prev_fused, int part, const rlks_gather_next* next, void* workspace,
+                            int64_t ws_bytes, void* stream);
 int rlks_ppo_adam_apply(const rlks_mlp_desc* desc, float* params_dev, const float* grad_dev, float* adam_m_dev,
                         float* adam_v_dev, int64_t n_params, float lr, float beta1, float beta2, float eps, int step,
                         void* workspace, int64_t ws_bytes, int rows, void* stream);

@@ -17,9 +17,20 @@ int fail(int code, const std::string& msg) {
 }
 
 #ifdef RLKS_DEBUG
-int dcheck_read_env(unsigned long long*);
-int dcheck_read_ppo(unsigned long long*);
-int dcheck_read_sgd(unsigned long long*);
+// the counters' readers of every translation unit (registered by their static initialisers; a
+// function-local registry, so that the units' initialisation order does not matter)
+struct DcheckReaders {
+  int (*f[64])(unsigned long long*);
+  int n = 0;
+};
+static DcheckReaders& dcheck_readers() {
+  static DcheckReaders r;
+  return r;
+}
+void dcheck_register(int (*reader)(unsigned long long*)) {
+  DcheckReaders& r = dcheck_readers();
+  if (r.n < 64) r.f[r.n++] = reader;
+}
 #endif
 
 }  // namespace rlks
@@ -28,11 +39,12 @@ int rlks_debug_checks(unsigned long long* out) {
 #ifdef RLKS_DEBUG
   RLKS_REQUIRE(out, RLKS_ERR_ARG, "rlks_debug_checks: null argument");
   RLKS_HIP(hipDeviceSynchronize());
-  int (*readers[])(unsigned long long*) = {rlks::dcheck_read_env, rlks::dcheck_read_ppo, rlks::dcheck_read_sgd};
+  const rlks::DcheckReaders& R = rlks::dcheck_readers();
+  RLKS_REQUIRE(R.n >= 11, RLKS_ERR_HIP, "rlks_debug_checks: a translation unit did not register its counters");
   out[0] = out[1] = out[2] = 0;
-  for (auto rd : readers) {
+  for (int i = 0; i < R.n; ++i) {
     unsigned long long v[3];
-    RLKS_REQUIRE(rd(v) == 0, RLKS_ERR_HIP, "rlks_debug_checks: counter read failed");
+    RLKS_REQUIRE(R.f[i](v) == 0, RLKS_ERR_HIP, "rlks_debug_checks: counter read failed");
     if (v[0] && !out[0]) { out[1] = v[1]; out[2] = v[2]; }
     out[0] += v[0];
   }

@@ -20,7 +20,6 @@
 
 namespace rlks {
 
-RLKS_DCHECK_READER(env)
 
 // ----------------------------------------------------------------------------- kernels
 // Skip n_draws[lane] calls of random() (2 words each) on every masked lane: positions lane e of a

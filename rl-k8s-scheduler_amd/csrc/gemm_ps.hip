@@ -55,10 +55,14 @@ __device__ __forceinline__ void dma_plane(const _Float16* plane, int ld, int row
   const _Float16* src;
   if (!KM) {
     const int r = sig >> 2, q = (sig & 3) ^ ((r >> 2) & 3);
-    src = plane + (size_t)min(r0 + r, rows - 1) * ld + k0 + 8 * q;
+    int kk = k0 + 8 * q;
+    if (!dcheck(kk + 8 <= ld, DC_GEMM_K, kk)) kk = ld - 8;
+    src = plane + (size_t)min(r0 + r, rows - 1) * ld + kk;
   } else {
     const int k = sig >> 5, p = (sig & 31) ^ (4 * (k & 3));
-    src = plane + (size_t)(k0 + k) * ld + min(r0 + 8 * p, rows - 8);
+    int c = min(r0 + 8 * p, rows - 8);
+    if (!dcheck(c >= 0 && c + 8 <= ld, DC_GEMM_K, c)) c = 0;
+    src = plane + (size_t)(k0 + k) * ld + c;
   }
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + w * 512), 16, 0, 0);
 }

@@ -12,7 +12,6 @@
 
 namespace rlks {
 
-RLKS_DCHECK_READER(ppo)
 
 // ----------------------------------------------------------------------------- reduce
 // out[i] = sum_p part[p * pstride + i] (i < len, p < P) in a fixed order with f64 accumulation.
@@ -243,13 +242,16 @@ struct GatherArgs {
 };
 
 // source index t * N + n of minibatch row i: rows [k rows_g, (k+1) rows_g) come from lane group
-// k, whose permutation p -> (t = p / Ng, lane k Ng + p mod Ng)
-__device__ __forceinline__ int64_t gather_src(const Perm* perm, int64_t row0g, int rows_g, int Ng, int N, uint32_t i) {
+// k, whose permutation p -> (t = p / Ng, lane k Ng + p mod Ng).  groups: the entries of `perm`
+// (debug checks: the group index against it, and the permutation's input against its domain --
+// its output is in [0, S) by construction)
+__device__ __forceinline__ int64_t gather_src(const Perm* perm, int64_t row0g, int rows_g, int Ng, int N, uint32_t i,
+                                              int groups) {
   uint32_t k = i / (uint32_t)rows_g;
-  const uint32_t ii = i - k * (uint32_t)rows_g;
-  if (!dcheck(k < (uint32_t)MAX_GROUPS, DC_GATHER_GROUP, k)) k = 0;
-  uint64_t p = perm_apply(perm[k], (uint64_t)(row0g + ii));
-  if (!dcheck(p < perm[k].S, DC_GATHER_SRC, (long long)p)) p = 0;
+  uint64_t ii = i - k * (uint32_t)rows_g;
+  if (!dcheck(k < (uint32_t)groups, DC_GATHER_GROUP, k)) k = 0;
+  if (!dcheck((uint64_t)row0g + ii < perm[k].S, DC_GATHER_SRC, (long long)(row0g + ii))) ii = 0;
+  const uint64_t p = perm_apply(perm[k], (uint64_t)(row0g + ii));
   uint64_t t, nl;
   if (p >> 32) {
     t = p / (uint64_t)Ng;
@@ -262,7 +264,7 @@ __device__ __forceinline__ int64_t gather_src(const Perm* perm, int64_t row0g, i
   return (int64_t)(t * (uint64_t)N + (uint64_t)k * Ng + nl);
 }
 __device__ __forceinline__ int64_t gather_src(const GatherArgs& g, uint32_t i) {
-  return gather_src(g.perm, g.row0g, g.rows_g, g.Ng, g.b.N, i);
+  return gather_src(g.perm, g.row0g, g.rows_g, g.Ng, g.b.N, i, (g.rows + g.rows_g - 1) / g.rows_g);
 }
 
 // narrow records (stride 12 / 20 / 36: 2, 4 or 8 clouds): one thread per row computes the row's permuted source
@@ -349,7 +351,7 @@ __device__ __forceinline__ void gather_packed_elem(const Perm* perm, int64_t row
   constexpr int TPR = PS / 4;
   const uint32_t i = e / TPR, q = e % TPR;
   if (i >= (uint32_t)rows) return;
-  const int64_t tn = gather_src(perm, row0g, rows_g, Ng, N, i);
+  const int64_t tn = gather_src(perm, row0g, rows_g, Ng, N, i, (rows + rows_g - 1) / rows_g);
   const float4 v = reinterpret_cast<const float4*>(packed + tn * PS)[q];
   if (4 * q < (uint32_t)S) reinterpret_cast<float4*>(mb + (size_t)i * S)[q] = v;
 }
@@ -770,16 +772,20 @@ struct FusedAdam {
                       // all-reduce follows; rlks_ppo_adam_apply then applies Adam)
 };
 
+// part: 0 = the whole gradient; 1 = the weight split, F1a, F2 and the reduce of W2 / b2 / W3 / b3 and
+// the stats; 2 = F1b and the reduce of W1 / b1 (rlks_ppo_grad_step_part: the caller all-reduces part
+// 1's buckets while part 2 runs)
 static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
                    const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes, int phases,
-                   hipStream_t s, const FusedAdam* fa = nullptr, const NextGather* nx = nullptr) {
+                   hipStream_t s, const FusedAdam* fa = nullptr, const NextGather* nx = nullptr, int part = 0) {
   RLKS_REQUIRE(M > 0 && M % 256 == 0, RLKS_ERR_ARG, "rlks_ppo_grad: split-fp16 rows must be a positive multiple of 256");
   const int D = d->obs_dim, A = d->n_actions, H = HID;
   const SfWs w = sf_ws_layout(D, A, M, (char*)workspace);
   RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_ppo_grad: workspace too small");
   const Layout L = make_layout(D, H, A);
   const bool f_pi = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_PI), f_vf = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_VF);
-  if (phases & (RLKS_PHASE_FWD | RLKS_PHASE_PREP)) {
+  if (part == 2) phases &= ~(RLKS_PHASE_PREP | RLKS_PHASE_DW2);
+  if ((phases & (RLKS_PHASE_FWD | RLKS_PHASE_PREP)) && part != 2) {
     const int parity = fa ? ((fa->step - 1) & 1) : 0;
     if (int rc = sf_prep(d, w, params, s, false, parity, fa && fa->prev_fused, fa ? (unsigned)fa->step : 0u))
       return rc;
@@ -794,7 +800,7 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
   }
   // F1 (forward, loss, dZ2, dH1 -> dW1 / db1, dW3 / db3) per net; F2 (dW2, db2) for both
   if (f_pi || f_vf)
-    if (int rc = launch_sf_f1(a, f_pi ? 0 : 1, (f_pi && f_vf) ? 2 : 1, A, s)) return rc;
+    if (int rc = launch_sf_f1(a, f_pi ? 0 : 1, (f_pi && f_vf) ? 2 : 1, A, s, part == 0 ? 3 : part)) return rc;
   // split F1 halves alone, both nets (profiling: each reads what a full F1 left in the workspace)
   if (!(f_pi || f_vf) && (phases & (RLKS_PHASE_F1A | RLKS_PHASE_F1B)))
     if (int rc = launch_sf_f1(a, 0, 2, A, s, (phases & RLKS_PHASE_F1A ? 1 : 0) | (phases & RLKS_PHASE_F1B ? 2 : 0)))
@@ -807,14 +813,18 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     const int An = net == 0 ? A : 1;
     const int64_t* o = L.off + 6 * net;
     const SfNet& n = w.n[net];
-    R.add(n.part_w1, grad + o[0], nullptr, (int64_t)H * D, w.blocks, H * D, 2 * net + 1);
-    R.add(n.part_b1, grad + o[1], nullptr, H, w.blocks, H, 2 * net + 1);
-    R.add(n.part_w2, grad + o[2], nullptr, SF_W2_PSTRIDE, w.splits, H * H, 2 * net);
-    R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
-    R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, w.fa_parts, An * H);
-    R.add(n.part_b3, grad + o[5], nullptr, An, w.fa_parts, An);
+    if (part != 1) {
+      R.add(n.part_w1, grad + o[0], nullptr, (int64_t)H * D, w.blocks, H * D, 2 * net + 1);
+      R.add(n.part_b1, grad + o[1], nullptr, H, w.blocks, H, 2 * net + 1);
+    }
+    if (part != 2) {
+      R.add(n.part_w2, grad + o[2], nullptr, SF_W2_PSTRIDE, w.splits, H * H, 2 * net);
+      R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
+      R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, w.fa_parts, An * H);
+      R.add(n.part_b3, grad + o[5], nullptr, An, w.fa_parts, An);
+    }
   }
-  if (stats) {  // per-block columns [policy loss, vf loss, kl, entropy] -> RLKS_STAT_* directly
+  if (stats && part != 2) {  // per-block columns [policy loss, vf loss, kl, entropy] -> RLKS_STAT_* directly
     const int tiles = w.fa_parts;
     R.add(w.n[0].part_stat + 0, nullptr, stats + RLKS_STAT_POLICY_LOSS, 4, tiles, 1);
     R.add(w.n[1].part_stat + 1, nullptr, stats + RLKS_STAT_VF_LOSS, 4, tiles, 1);
@@ -824,6 +834,7 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     R.a.rows = (double)M;
   }
   if (fa && fa->apply) {  // Adam on every parameter as its gradient is summed; W2 / W1a maxima -> the next prep
+    RLKS_REQUIRE(part == 0, RLKS_ERR_ARG, "sf_grad: fused Adam needs the whole gradient");
     for (int k = 0; k < 4; ++k)
       RLKS_REQUIRE(R.mnext[k] <= SF_PMAX, RLKS_ERR_UNSUPPORTED, "rlks_ppo_sgd_step: too many reduce blocks per weight");
     R.a.p = fa->p; R.a.m = fa->m; R.a.v = fa->v; R.a.grad = grad; R.a.co = fa->co;
@@ -1057,6 +1068,28 @@ int rlks_ppo_grad_step_next(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, c
   FusedAdam fa{nullptr, nullptr, nullptr, AdamCo{}, step, prev_fused ? 1 : 0, false};
   return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
                  &fa, &n);
+}
+
+int rlks_ppo_grad_step_part(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
+                            const float* mb, int M, float* grad, double* stats, int step, int prev_fused, int part,
+                            const rlks_gather_next* x, void* workspace, int64_t ws_bytes, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(part == 1 || part == 2, RLKS_ERR_ARG, "rlks_ppo_grad_step_part: part must be 1 or 2");
+  RLKS_REQUIRE(co && params && dyn && mb && grad && workspace && step >= 1, RLKS_ERR_ARG,
+               "rlks_ppo_grad_step_part: bad argument");
+  if (d->precision != RLKS_PRECISION_SF16 || is_wide(d)) {  // no split form: everything in part 1
+    if (part == 2) return x ? gather_after(d, x, stream) : RLKS_OK;
+    return rlks_ppo_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, stream);
+  }
+  FusedAdam fa{nullptr, nullptr, nullptr, AdamCo{}, step, prev_fused ? 1 : 0, false};
+  NextGather n;
+  bool fused = false;
+  if (x && part == 2)
+    if (int rc = next_gather(d, x, n, fused)) return rc;
+  if (int rc = sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
+                       &fa, fused ? &n : nullptr, part))
+    return rc;
+  return (x && part == 2 && !fused) ? gather_after(d, x, stream) : RLKS_OK;
 }
 
 int rlks_ppo_adam_apply(const rlks_mlp_desc* d, float* params, const float* grad, float* adam_m, float* adam_v,

@@ -38,8 +38,8 @@ inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 // minibatch gather's source rows, the SGD step's tiles).  A failed check does not fault the GPU: it
 // counts the violation, records the first site and value in this translation unit's g_dcheck, and
 // the caller clamps the index so that the access stays in bounds.  rlks_debug_checks() reads and
-// clears the counters of every translation unit; in the product build dcheck() is `true` and
-// compiles away.
+// clears the counters of every translation unit (each registers its reader at load); in the
+// product build dcheck() is `true` and compiles away.
 enum DcheckSite {
   DC_NODE_GROUP = 1,   // 8-chunk group of a departure scan within the cluster's chunks
   DC_NODE_CHUNK = 2,   // chunk of a departing pod
@@ -48,8 +48,12 @@ enum DcheckSite {
   DC_GATHER_SRC = 5,   // minibatch gather source sample < T N
   DC_GATHER_GROUP = 6, // lane group < groups
   DC_SGD_TILE = 7,     // F1 / F2 tile < M / 16
+  DC_GEMM_K = 8,       // pre-split GEMM: a DMA piece's 8 halves within the plane's row (ld)
+  DC_WIDE_COL = 9,     // wide dZ2 kernel: the thread's 8 columns within H
 };
 #ifdef RLKS_DEBUG
+// every translation unit that includes this header gets its own counters and registers their
+// reader when the library loads (common.hip's registry), so no unit's checks go unread
 static __device__ unsigned long long g_dcheck[3];  // violations, first site, first value
 __device__ __forceinline__ bool dcheck(bool ok, int site, long long val) {
   if (!ok && atomicAdd(&g_dcheck[0], 1ull) == 0ull) {
@@ -58,16 +62,16 @@ __device__ __forceinline__ bool dcheck(bool ok, int site, long long val) {
   }
   return ok;
 }
+void dcheck_register(int (*reader)(unsigned long long*));
 // host reader of this translation unit's counters (cleared after reading)
-#define RLKS_DCHECK_READER(tu)                                                                   \
-  int dcheck_read_##tu(unsigned long long* h) {                                                  \
-    const unsigned long long z[3] = {0ull, 0ull, 0ull};                                          \
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dcheck), sizeof(g_dcheck)) != hipSuccess) return 1;  \
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_dcheck), z, sizeof(z)) == hipSuccess ? 0 : 1;          \
-  }
+static int dcheck_read_tu(unsigned long long* h) {
+  const unsigned long long z[3] = {0ull, 0ull, 0ull};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dcheck), sizeof(g_dcheck)) != hipSuccess) return 1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dcheck), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+static const int g_dcheck_registered = (dcheck_register(&dcheck_read_tu), 0);
 #else
 __device__ __forceinline__ bool dcheck(bool, int, long long) { return true; }
-#define RLKS_DCHECK_READER(tu)
 #endif
 
 // ----------------------------------------------------------------------------- Philox4x32-10

@@ -35,7 +35,6 @@
 
 namespace rlks {
 
-RLKS_DCHECK_READER(sgd)
 
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
@@ -899,12 +898,19 @@ __device__ __forceinline__ void f1a_ws_body(const SfArgs& g, const int wg, const
       // of the block loop into 32 live 64-bit registers
       const _Float16 *w2h = N.w2ph, *w2l = N.w2pl;
       asm volatile("" : "+s"(w2h), "+s"(w2l));
-#pragma unroll
+      // step 0: H1 of the block's tile (k-tile by k-tile, each followed by its n-tile 0 MFMAs); steps
+      // 1-15: one n-tile each, a runtime loop (one copy of the step's code: the consumer's 16 steps
+      // are unrolled, and the two roles' code shares the instruction cache)
+#pragma unroll 1
       for (int k = 0; k < 16; ++k) {
+#ifdef FW_XP_NODMA
+        const bool dma = false;
+#else
         const bool dma = live && (k < 14 || more);  // the slab of step k + 2 (the next block's after k = 13)
+#endif
         if (live) {
-          if (dma) fw_dma(w2h, w2l, (k + 2) & 15, sRing + ((k + 2) % FW_RING) * FW_SLAB, p, l);
-          const _Float16* slab = sRing + (k % FW_RING) * FW_SLAB;
+          if (dma) fw_dma(w2h, w2l, (k + 2) & 15, sRing + ((k + 2) & (FW_RING - 1)) * FW_SLAB, p, l);
+          const _Float16* slab = sRing + (k & (FW_RING - 1)) * FW_SLAB;
           const int lo_ = opaque(l), cc = lo_ & 15, gg = lo_ >> 4;
           const int fo = cc * 32 + 8 * (gg ^ sw16(cc));
           float* mb = sMb + p * 512 + 4 * lo_;

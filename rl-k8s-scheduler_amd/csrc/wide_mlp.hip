@@ -239,7 +239,9 @@ __global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout
   __shared__ __attribute__((aligned(16))) float sA[DZ_K][DZ_ROWS + 4];  // dout^T chunk (padded: the transposing stores)
   __shared__ __attribute__((aligned(16))) float sB[DZ_K][DZ_COLS];      // W3 chunk; at the end the db2 sums
   const int tid = threadIdx.x, cg = tid & 31, rg = tid >> 5;
-  const int n0 = blockIdx.x * DZ_COLS, n = n0 + 8 * cg;  // this thread's 8 columns (H % 8 == 0: host check)
+  const int n0 = blockIdx.x * DZ_COLS;
+  int n = n0 + 8 * cg;  // this thread's 8 columns (H % 8 == 0: host check)
+  if (!dcheck(n + 8 <= H || n0 + DZ_COLS > H, DC_WIDE_COL, n)) n = H - 8;
   float mx = 0.f, cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // max |dZ2|, db2: this thread's column sums
   for (int rt = 0; rt < DZ_RT; ++rt) {
     const int m0 = (blockIdx.y * DZ_RT + rt) * DZ_ROWS;

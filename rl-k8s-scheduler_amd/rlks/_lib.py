@@ -134,6 +134,8 @@ SIGNATURES = {
     "rlks_ppo_grad_step": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _I, _I, _P, _I64, _P],
     "rlks_ppo_grad_step_next": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _I, _I,
                                 C.POINTER(GatherNext), _P, _I64, _P],
+    "rlks_ppo_grad_step_part": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _I, _I, _I,
+                                C.POINTER(GatherNext), _P, _I64, _P],
     "rlks_ppo_adam_apply": [C.POINTER(MlpDesc), _P, _P, _P, _P, _I64, _F, _F, _F, _F, _I, _P, _I64, _I, _P],
     "rlks_kl_update": [_P, _P, _F, _P],
 }

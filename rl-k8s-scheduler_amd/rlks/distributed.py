@@ -4,7 +4,9 @@ The env lanes shard with no data-path collective: rank r owns g
 [r*N, (r+1)*N) — the Philox counters are keyed by the global lane id, so a lane's trajectory does
 not depend on the world size.  The only exchanges are
   * one all-reduce (sum) of the flat fp32 gradient per SGD step; every rank scales its loss by
-    1 / (rows_per_rank * world), so the sum is the gradient of the global-minibatch mean;
+    1 / (rows_per_rank * world), so the sum is the gradient of the global-minibatch mean.  With the
+    split-fp16 step it is issued as two buckets (rlks_ppo_grad_step_part): W2 / b2 / W3 / b3 as soon
+    as they are reduced, under the dH1 / dW1 kernel, then W1 / b1;
   * per iteration: the advantage moments [sum A, sum A^2, count], the SGD-step loss stats and the
     episode-return sums, so that standardisation, the KL-coefficient update and the reported
     episode_reward_mean equal the single-process values.
@@ -42,3 +44,14 @@ def allreduce_sum_(t):
     if d is not None and d.get_world_size() > 1:
         d.all_reduce(t)
     return t
+
+
+def allreduce_sum_async(tensors):
+    """start in-place sums over ranks of each tensor (contiguous views of one buffer are fine) and
+    return their work handles; wait() on each orders the caller's stream after the collective
+    (RCCL: the collective runs on its own stream, so it overlaps whatever the caller's stream does
+    until then).  Single process: no-op, []."""
+    d = group()
+    if d is None or d.get_world_size() == 1:
+        return []
+    return [d.all_reduce(t, async_op=True) for t in tensors]

@@ -84,6 +84,9 @@ class PPOConfig:
         # minibatches are drawn per block of lanes (rlks_ppo_gather_grouped): None = one block per
         # rank.  A single-rank run with num_lane_groups = W trains exactly like W ranks.
         self.num_lane_groups = None
+        # more than one rank, split-fp16 step: all-reduce the W2 / W3 gradient bucket while the dW1
+        # kernel runs (rlks_ppo_grad_step_part), instead of the whole gradient after it
+        self.overlap_allreduce = True
         # rlks-specific knobs
         self.num_envs = None          # lanes per GPU (default: workers x envs per worker)
         self.noise = "philox"         # env utilisation noise: "philox" or "mt19937"
@@ -331,7 +334,13 @@ class PPO:
         # the previous SGD step was a fused one on the current parameters (rlks_ppo_sgd_step)
         self._fused_prev = False
         self._ep_history = collections.deque(maxlen=max(1, int(cfg.metrics_num_episodes_for_smoothing)))
-        self._ar_events = None  # profile_allreduce(): (start, end) events of each gradient all-reduce
+        self._ar_events = None  # profile_allreduce(): (start, compute end, done) events per SGD step
+        # gradient buckets of the overlapped all-reduce (include/rlks.h rlks_ppo_grad_step_part): views of
+        # the flat gradient, W2 / b2 / W3 / b3 of each net (+ alignment padding), then W1 / b1
+        off = list(self.params.offsets) + [self.params.padded]
+        g = self.grad
+        self._buckets = ([g[off[2]:off[6]], g[off[8]:off[12]]], [g[off[0]:off[2]], g[off[6]:off[8]]])
+        self._overlap = bool(cfg.overlap_allreduce) and self.world > 1 and self.precision == "sf16"
         self.sample_calls = 0   # compute_actions / compute_single_action draws so far (Philox counter)
         self.iteration = 0
         self.timesteps_total = 0
@@ -407,17 +416,38 @@ class PPO:
             return
         # ranks: gradient -> all-reduce -> Adam, the Adam pass also leaving the next split's weight
         # maxima (rlks_ppo_grad_step / rlks_ppo_adam_apply: no weight-max pass per SGD step)
-        _lib.call("rlks_ppo_grad_step_next", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat),
-                  _lib.ptr(self.dyn), _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row),
-                  self.adam_step, int(self._fused_prev), nxt, _lib.ptr(self.ws), self.ws.numel(), s)
-        if self._ar_events is not None:  # profile_allreduce(): events on the launch stream around it
-            e0 = self.torch.cuda.Event(enable_timing=True)
-            e0.record(self.torch.cuda.current_stream(self.device))
-        self._allreduce(self.grad)
-        if self._ar_events is not None:
-            e1 = self.torch.cuda.Event(enable_timing=True)
-            e1.record(self.torch.cuda.current_stream(self.device))
-            self._ar_events.append((e0, e1))
+        ev = self._ar_events is not None  # profile_allreduce(): events on the launch stream
+        cur = self.torch.cuda.current_stream(self.device)
+
+        def event():
+            e = self.torch.cuda.Event(enable_timing=True)
+            e.record(cur)
+            return e
+
+        if self._overlap:
+            # part 1 (F1a, F2, the W2 / W3 reduce) -> its bucket's all-reduce on the collective's stream,
+            # under part 2 (F1b, the W1 reduce, the next gather) -> the W1 bucket's; Adam after both
+            args = (desc, C.byref(self.coeffs), _lib.ptr(self.params.flat), _lib.ptr(self.dyn), _lib.ptr(self.mbuf),
+                    self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row), self.adam_step, int(self._fused_prev))
+            _lib.call("rlks_ppo_grad_step_part", *args, 1, None, _lib.ptr(self.ws), self.ws.numel(), s)
+            e0 = event() if ev else None
+            h = ddp.allreduce_sum_async(self._buckets[0])
+            _lib.call("rlks_ppo_grad_step_part", *args, 2, nxt, _lib.ptr(self.ws), self.ws.numel(), s)
+            h += ddp.allreduce_sum_async(self._buckets[1])
+            e1 = event() if ev else None
+            for w in h:
+                w.wait()
+            if ev:  # (part 1 end, part 2 end, all-reduces done): exposed = the last interval
+                self._ar_events.append((e0, e1, event()))
+        else:
+            _lib.call("rlks_ppo_grad_step_next", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat),
+                      _lib.ptr(self.dyn), _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row),
+                      self.adam_step, int(self._fused_prev), nxt, _lib.ptr(self.ws), self.ws.numel(), s)
+            e0 = event() if ev else None
+            self._allreduce(self.grad)
+            if ev:
+                e1 = event()
+                self._ar_events.append((e0, e0, e1))
         _lib.call("rlks_ppo_adam_apply", desc, _lib.ptr(self.params.flat), _lib.ptr(self.grad), _lib.ptr(self.adam_m),
                   _lib.ptr(self.adam_v), self.params.padded, float(self.config.lr), float(beta1), float(beta2),
                   float(self.config.adam_eps), self.adam_step, _lib.ptr(self.ws), self.ws.numel(), self.mb, s)
@@ -450,8 +480,10 @@ class PPO:
     def profile_allreduce(self):
         """one PPO iteration with HIP events on the launch stream around every per-SGD-step gradient
         all-reduce (multi-rank only): where the data-parallel time goes.  Returns None
-        on one rank, else the all-reduce's mean / max duration per SGD step, its total and its share
-        of the iteration, the maximum over ranks of each."""
+        on one rank, else the all-reduce's exposed time per SGD step (compute launches done -> all
+        buckets reduced, what the step's Adam waits for; with overlap_allreduce the first bucket has
+        run under the dW1 kernel), its mean / max, total and share of the iteration, and the span
+        from the first bucket's start; the maximum over ranks of each."""
         if self.world == 1:
             return None
         torch = self.torch
@@ -462,14 +494,19 @@ class PPO:
         self.train_step_no_sync()
         t1.record(st)
         t1.synchronize()
-        ar = [a.elapsed_time(b) for a, b in self._ar_events]
+        # exposed: from the end of the step's compute launches to the all-reduces' completion on the
+        # launch stream (what the next step waits for); span: from the first bucket's start
+        ex = [b.elapsed_time(c) for a, b, c in self._ar_events]
+        sp = [a.elapsed_time(c) for a, b, c in self._ar_events]
         self._ar_events = None
         it_ms = t0.elapsed_time(t1)
-        v = torch.tensor([sum(ar) / len(ar), max(ar), sum(ar), it_ms], dtype=torch.float64, device=self.device)
+        v = torch.tensor([sum(ex) / len(ex), max(ex), sum(ex), sum(sp) / len(sp), it_ms], dtype=torch.float64,
+                         device=self.device)
         d = ddp.group()
         d.all_reduce(v, op=d.ReduceOp.MAX)
-        mean_ms, max_ms, total_ms, it_ms = (float(x) for x in v.cpu())
-        return {"allreduce_ms_per_sgd_step": mean_ms, "allreduce_ms_max": max_ms, "sgd_steps": len(ar),
+        mean_ms, max_ms, total_ms, span_ms, it_ms = (float(x) for x in v.cpu())
+        return {"allreduce_ms_per_sgd_step": mean_ms, "allreduce_ms_max": max_ms, "sgd_steps": len(ex),
+                "allreduce_span_ms_per_sgd_step": span_ms, "overlapped": self._overlap,
                 "allreduce_ms_per_iteration": total_ms, "iteration_ms": it_ms,
                 "allreduce_share_of_iteration": total_ms / it_ms if it_ms > 0 else None,
                 "bytes_per_allreduce": int(self.grad.numel() * 4), "backend": d.get_backend()}

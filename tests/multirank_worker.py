@@ -13,6 +13,7 @@ sys.path[:0] = [str(ROOT / "rl-k8s-scheduler_amd")]
 def main():
     out = Path(sys.argv[1])
     N, T, mb, epochs, iters = (int(x) for x in sys.argv[2:7])
+    overlap = int(sys.argv[7]) if len(sys.argv) > 7 else 1  # PPOConfig.overlap_allreduce
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -29,14 +30,18 @@ def main():
                .debugging(seed=13))
         cfg.num_envs = N
         cfg.rollout_fragment_length = T
+        cfg.overlap_allreduce = bool(overlap)
         algo = PPO(config=cfg, device=torch.device("cuda", 0))
         assert (algo.rank, algo.world, algo.groups, algo.group0) == (rank, world, 1, rank)
         results = [algo.train() for _ in range(iters)]
+        assert algo._overlap == bool(overlap)
+        prof = algo.profile_allreduce()
         keep = ("episode_reward_mean", "episodes_this_iter", "timesteps_total")
         res = [{k: r[k] for k in keep} | {"kl": r["info"]["learner"]["default_policy"]["learner_stats"]["kl"]}
                for r in results]
         np.savez(out / f"rank{rank}.npz", params=algo.params.flat.cpu().numpy(),
-                 kl_coeff=np.float32(algo.dyn[2].item()), results=np.array(json.dumps(res)))
+                 kl_coeff=np.float32(algo.dyn[2].item()), results=np.array(json.dumps(res)),
+                 allreduce=np.array(json.dumps(prof)))
     finally:
         dist.destroy_process_group()
 

@@ -4,7 +4,8 @@ What is checked, with the CPU oracle standing in for the per-rank GPU kernels (t
   1. lane sharding: rank r's lanes (env_offset = r*N) replay exactly the lanes [rN, (r+1)N) of a
      single-process run with 2N lanes (Philox counters keyed by the global lane id);
   2. the gradient protocol: per-rank gradients with loss scale 1/(rows*world), summed by
-     all_reduce, equal the single-process gradient of the global-minibatch mean;
+     all_reduce, equal the single-process gradient of the global-minibatch mean; the two-bucket
+     async form of the overlapped SGD step gives the one-buffer all-reduce's bits;
   3. advantage-moment all-reduce gives the global mean / std used for standardisation.
 """
 import os
@@ -84,6 +85,17 @@ def _worker(rank, world, port, q):
         mine = mb[rank * rows:(rank + 1) * rows]
         g, _ = oracle.ppo_loss_grad(flat, off, D, H, A, mine, count=1.0 / ddp.loss_scale(rows, world))
         gt = torch.from_numpy(g.copy())
+        # the overlapped form (PPO.sgd_step, rlks_ppo_grad_step_part): the W2 / W3 bucket of each net,
+        # then the W1 bucket, as async in-place all-reduces on views of one flat fp32 buffer
+        g32 = torch.from_numpy(g.astype(np.float32))
+        b32 = g32.clone()
+        o = off + [g32.numel()]
+        h = ddp.allreduce_sum_async([b32[o[2]:o[6]], b32[o[8]:o[12]]])
+        h += ddp.allreduce_sum_async([b32[o[0]:o[2]], b32[o[6]:o[8]]])
+        for w in h:
+            w.wait()
+        ddp.allreduce_sum_(g32)
+        assert torch.equal(b32.view(torch.int32), g32.view(torch.int32))
         ddp.allreduce_sum_(gt)
         # advantage moments
         adv = rng.standard_normal(1000 * world)[rank * 1000:(rank + 1) * 1000]

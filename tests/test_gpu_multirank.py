@@ -30,19 +30,15 @@ def _free_port():
     return p
 
 
-def test_two_ranks_equal_one_rank_with_two_lane_groups(tmp_path):
-    if not torch.cuda.is_available():
-        pytest.skip("no HIP device")
-    from rlks.ppo import PPO, PPOConfig
-
-    N, T, mb, epochs, iters, world = 512, 128, 4096, 2, 2, 2
+def _run_ranks(out, N, T, mb, epochs, iters, world, overlap=1):
+    out.mkdir(parents=True, exist_ok=True)
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, str(HERE / "multirank_worker.py"), str(tmp_path), str(N),
-                                       str(T), str(mb), str(epochs), str(iters)], env=env))
+        procs.append(subprocess.Popen([sys.executable, str(HERE / "multirank_worker.py"), str(out), str(N),
+                                       str(T), str(mb), str(epochs), str(iters), str(overlap)], env=env))
     try:
         for p in procs:
             assert p.wait(timeout=100) == 0
@@ -50,7 +46,16 @@ def test_two_ranks_equal_one_rank_with_two_lane_groups(tmp_path):
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    ranks = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    return [np.load(out / f"rank{r}.npz") for r in range(world)]
+
+
+def test_two_ranks_equal_one_rank_with_two_lane_groups(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from rlks.ppo import PPO, PPOConfig
+
+    N, T, mb, epochs, iters, world = 512, 128, 4096, 2, 2, 2
+    ranks = _run_ranks(tmp_path, N, T, mb, epochs, iters, world)
     assert np.array_equal(ranks[0]["params"], ranks[1]["params"])
     res = [json.loads(str(z["results"])) for z in ranks]
     assert res[0] == res[1]
@@ -77,3 +82,22 @@ def test_two_ranks_equal_one_rank_with_two_lane_groups(tmp_path):
         assert a["episodes_this_iter"] == b["episodes_this_iter"] and a["timesteps_total"] == b["timesteps_total"]
         assert a["episode_reward_mean"] == pytest.approx(b["episode_reward_mean"], rel=1e-12)
         assert a["kl"] == pytest.approx(b["info"]["learner"]["default_policy"]["learner_stats"]["kl"], rel=1e-3)
+
+
+def test_overlapped_allreduce_is_bit_identical(tmp_path):
+    """PPOConfig.overlap_allreduce (rlks_ppo_grad_step_part: the W2 / W3 bucket all-reduced while the
+    dW1 kernel runs, then the W1 bucket) leaves the parameters, KL coefficient and results of the
+    one-bucket path bit for bit, on both ranks; the profile reports both forms' exposed time"""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    N, T, mb, epochs, iters, world = 512, 64, 4096, 2, 2, 2
+    on = _run_ranks(tmp_path / "on", N, T, mb, epochs, iters, world, overlap=1)
+    off = _run_ranks(tmp_path / "off", N, T, mb, epochs, iters, world, overlap=0)
+    for r in range(world):
+        assert np.array_equal(on[r]["params"].view(np.int32), off[r]["params"].view(np.int32)), r
+        assert float(on[r]["kl_coeff"]) == float(off[r]["kl_coeff"])
+        assert json.loads(str(on[r]["results"])) == json.loads(str(off[r]["results"]))
+    p_on, p_off = json.loads(str(on[0]["allreduce"])), json.loads(str(off[0]["allreduce"]))
+    assert p_on["overlapped"] and not p_off["overlapped"]
+    print(f"exposed all-reduce per SGD step: overlapped {p_on['allreduce_ms_per_sgd_step']:.3f} ms, "
+          f"one bucket {p_off['allreduce_ms_per_sgd_step']:.3f} ms ({p_on['backend']})")
