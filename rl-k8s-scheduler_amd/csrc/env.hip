@@ -308,6 +308,7 @@ __device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t*
   int2 f[8];
   int dep[8];
   u32x4 x{0u, 0u, 0u, 0u};
+  const float lg1p = log1pf(-(float)v.depart_prob) * 1.4426950408889634f;  // log2(1 - p) < 0
   const float inv_lg1p = 0.6931471805599453f / log1pf(-(float)v.depart_prob);  // 1 / log2(1 - p) = ln 2 / ln(1 - p) < 0
   while (pos < P) {
     if ((n & 3) == 0)
@@ -317,7 +318,11 @@ __device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t*
     const uint32_t u = (n & 3) == 0 ? x.x : (n & 3) == 1 ? x.y : (n & 3) == 2 ? x.z : x.w;
     ++n;
     const int R = P - pos;
-    if (u < (R < v.n_skip ? S[R] : 0u)) break;  // none of the remaining R pods leaves
+    // none of the remaining R pods leaves iff u < S[R].  S[R] ~ (1 - p)^R 2^32 to ~1e-6 relative in
+    // fp32 (< 2^13 absolute): u more than 2^16 below that decides without the table read (the common
+    // case: one dependent L2 load fewer per lane), otherwise the table decides, bit-exactly as before
+    if ((float)u < exp2f((float)R * lg1p) * 0x1p32f - 0x1p16f) break;
+    if (u < (R < v.n_skip ? S[R] : 0u)) break;
     // surviving pods before the departure: the largest s in [0, min(R, L)) with S[s] > u (0 if
     // none), as the oracle's binary search finds it.  S[s] ~ (1 - p)^s 2^32, so s ~ log2(u 2^-32) /
     // log2(1 - p): start there and step to the exact answer against the table (one or two

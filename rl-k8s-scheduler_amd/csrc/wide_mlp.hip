@@ -353,26 +353,30 @@ PsOperand ps_op(const _Float16* hi, const _Float16* lo, int ld, int kmajor, int 
 }
 constexpr int H1_EXP = 14;  // H1 planes hold tanh x 2^14
 
-// forward of net `net` over M rows of x (row stride ldx): H1 (planes), H2 and out in the workspace
+// forward of net `net` over M rows of x (row stride ldx): H1 (planes), H2 and out in the workspace.
+// xslot: X's max |x| slot; x_done: the other net's forward already filled it and (when X goes in
+// planes) split X into xh / xl, identical for both nets (one absmax + split, not two)
 int forward_net(const rlks_mlp_desc* d, const Net& P, const WideNet& n, const float* x, int ldx, int M, int net,
-                _Float16* xh, _Float16* xl, hipStream_t s) {
+                _Float16* xh, _Float16* xl, unsigned* xslot, bool x_done, hipStream_t s) {
   const int D = d->obs_dim, H = d->hidden, An = net == 0 ? d->n_actions : 1;
   unsigned* sl = n.slots;
-  if (int rc = launch_absmax(x, M, D, ldx, sl + SL_X, s)) return rc;
+  if (!x_done)
+    if (int rc = launch_absmax(x, M, D, ldx, xslot, s)) return rc;
   if (int rc = launch_absmax(P.w1, H, D, D, sl + SL_W1, s)) return rc;
   if (int rc = launch_absmax(P.w2, H, H, H, sl + SL_W2, s)) return rc;
   if (int rc = launch_absmax(P.w3, An, H, H, sl + SL_W3, s)) return rc;
   if (int rc = launch_split_planes(P.w2, H, H, H, sl + SL_W2, 0, n.w2h, n.w2l, H, s)) return rc;
   if (D % 32 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0) {
     // H1 = tanh(X W1^T + b1) on the pre-split GEMM (K = obs_dim, 192 at c5), written as planes
-    if (int rc = launch_split_planes(x, M, D, ldx, sl + SL_X, 0, xh, xl, D, s)) return rc;
+    if (!x_done)
+      if (int rc = launch_split_planes(x, M, D, ldx, xslot, 0, xh, xl, D, s)) return rc;
     if (int rc = launch_split_planes(P.w1, H, D, D, sl + SL_W1, 0, n.w1h, n.w1l, D, s)) return rc;
     PsArgs a{};
-    a.a = ps_op(xh, xl, D, 0, M, sl + SL_X);
+    a.a = ps_op(xh, xl, D, 0, M, xslot);
     a.b = ps_op(n.w1h, n.w1l, D, 0, H, sl + SL_W1);
     a.M = M; a.N = H; a.K = D; a.epi = PS_TANH_BIAS_PLANES; a.c_hi = n.h1h; a.c_lo = n.h1l; a.ldc = H; a.bias = P.b1;
     if (int rc = launch_gemm_ps(a, s)) return rc;
-  } else if (int rc = gemm(x, ldx, 0, P.w1, D, 1, nullptr, H, M, H, D, GEMM_TANH_BIAS_PLANES, P.b1, nullptr, 0, sl + SL_X,
+  } else if (int rc = gemm(x, ldx, 0, P.w1, D, 1, nullptr, H, M, H, D, GEMM_TANH_BIAS_PLANES, P.b1, nullptr, 0, xslot,
                            sl + SL_W1, nullptr, s, nullptr, n.h1h, n.h1l)) {
     return rc;
   }
@@ -392,12 +396,15 @@ int forward_net(const rlks_mlp_desc* d, const Net& P, const WideNet& n, const fl
 int wide_forward(const rlks_mlp_desc* d, const float* params, const float* x, int ldx, int M, const WideWs& w,
                  float* logits, float* values, hipStream_t s) {
   const Layout L = make_layout(d->obs_dim, d->hidden, d->n_actions);
+  RLKS_HIP(hipMemsetAsync(w.n[0].slots, 0, 4 * SL_N, s));  // net 0's X slot serves both nets
   for (int net = 0; net < 2; ++net) {
     float* dst = net == 0 ? logits : values;
     if (!dst) continue;
     const WideNet& n = w.n[net];
-    RLKS_HIP(hipMemsetAsync(n.slots, 0, 4 * SL_N, s));
-    if (int rc = forward_net(d, net_of(params, L, net), n, x, ldx, M, net, w.xh, w.xl, s)) return rc;
+    if (net == 1) RLKS_HIP(hipMemsetAsync(n.slots, 0, 4 * SL_N, s));
+    const bool x_done = net == 1 && logits;  // the policy net's forward split X already
+    if (int rc = forward_net(d, net_of(params, L, net), n, x, ldx, M, net, w.xh, w.xl, w.n[0].slots + SL_X, x_done, s))
+      return rc;
     const int An = net == 0 ? d->n_actions : 1;
     RLKS_HIP(hipMemcpyAsync(dst, n.out, sizeof(float) * M * An, hipMemcpyDeviceToDevice, s));
   }
@@ -423,8 +430,10 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     float* g = grad;
     const int64_t* o = L.off + 6 * net;
     unsigned* sl = n.slots;
-    RLKS_HIP(hipMemsetAsync(sl, 0, 4 * SL_N, s));
-    if (int rc = forward_net(d, P, n, mb, stride, M, net, w.xh, w.xl, s)) return rc;
+    unsigned* xsl = w.n[0].slots + SL_X;  // X's scale: one slot for both nets
+    if (net == 0) RLKS_HIP(hipMemsetAsync(sl, 0, 4 * SL_N, s));
+    else RLKS_HIP(hipMemsetAsync(sl + SL_W1, 0, 4 * (SL_N - SL_W1), s));  // keep net 0's X slot (SL_X = 0)
+    if (int rc = forward_net(d, P, n, mb, stride, M, net, w.xh, w.xl, xsl, net == 1, s)) return rc;
     if (net == 0)
       hipLaunchKernelGGL(k_wide_loss_pi, dim3(w.blocks), dim3(64 * LOSS_PI_WAVES), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
                          n.dout, n.part_stat, sl + SL_DOUT);
@@ -469,13 +478,13 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
       if (int rc = launch_split_planes(w.dzb, M, H, H, sl + SL_DZ1, 0, w.dzh, w.dzl, H, s)) return rc;
       PsArgs a{};
       a.a = ps_op(w.dzh, w.dzl, H, 1, H, sl + SL_DZ1);
-      a.b = ps_op(w.xh, w.xl, D, 1, D, sl + SL_X);
+      a.b = ps_op(w.xh, w.xl, D, 1, D, w.n[0].slots + SL_X);
       a.M = H; a.N = D; a.K = Mp; a.epi = PS_STORE; a.C = g + o[0]; a.ldc = D;
       a.splits = gemm_ps_splits(H, D, Mp);
       a.part = w.part;
       if (int rc = launch_gemm_ps(a, s)) return rc;
     } else if (int rc = gemm(w.dzb, H, 1, mb, stride, 0, g + o[0], D, H, D, M, GEMM_STORE, nullptr, nullptr, 0,
-                             sl + SL_DZ1, sl + SL_X, nullptr, s, w.part)) {
+                             sl + SL_DZ1, w.n[0].slots + SL_X, nullptr, s, w.part)) {
       return rc;
     }
     if (int rc = launch_colsum(w.dzb, M, H, H, g + o[1], 0, w.part, s)) return rc;
