@@ -563,22 +563,23 @@ static int node_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* para
                         int explore, const SfWs* w, hipStream_t s) {
   const int N = b->N, D = d->obs_dim, A = d->n_actions;
   const Layout L = make_layout(D, HID, A);
-  SfRollArgs r{};
+  SfFwdArgs r{};
   if (w) {
     if (int rc = sf_prep(d, *w, params, s, true)) return rc;
     for (int net = 0; net < 2; ++net) {
       const NetPtrs P = net_ptrs_host(params, L, net);
-      r.n[net] = SfRollNet{w->w[net].w1h, w->w[net].w1l, w->w[net].w2rh, w->w[net].w2rl, P.b2, P.w3, P.b3, w->w[net].sc};
+      r.n[net] = w->n[net];
+      r.n[net].b2 = P.b2; r.n[net].w3 = P.w3; r.n[net].b3 = P.b3;
     }
-    r.M = N; r.D = D; r.A = A; r.T = 0;
+    r.M = N; r.D = D;
   }
   auto forward = [&](const float* x, float* logits, float* values) -> int {
-    if (w) {
-      SfRollArgs a = r;
-      a.x = const_cast<float*>(x);
-      a.logits = logits;
-      a.values = values;
-      return launch_sf_roll(a, FWD_ONLY, s);
+    if (w) {  // 16-row tiles of both nets (sgd_sf16.hip k_sf_fwd16)
+      SfFwdArgs a = r;
+      a.x = x;
+      a.out[0] = logits;
+      a.out[1] = values;
+      return launch_sf_fwd16(a, A, s);
     }
     for (int net = 0; net < 2; ++net) {
       float* out = net == 0 ? logits : values;

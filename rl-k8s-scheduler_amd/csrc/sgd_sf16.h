@@ -81,6 +81,16 @@ struct SfRollArgs {
 };
 int launch_sf_roll(const SfRollArgs& a, int mode, hipStream_t s);
 
+// forward of both nets on 16-row tiles (sgd_sf16.hip k_sf_fwd16): out[0] = logits [M][A] (or null:
+// the value net alone), out[1] = values [M] (or null)
+struct SfFwdArgs {
+  SfNet n[2];  // weights: w1h/w1l, w2ph/w2pl, sc, b2, w3, b3
+  const float* x;  // [M][D] observations
+  int M, D, net0;
+  float* out[2];
+};
+int launch_sf_fwd16(const SfFwdArgs& a, int A, hipStream_t s);
+
 int sf_kd(int D);
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
 // halves: 1 = F1a (k_sf_fwd), 2 = F1b (k_sf_bwd), 3 = both

@@ -305,17 +305,26 @@ __device__ __forceinline__ void load_tail(const SfArgs& g, int row, RecTail<A_>&
   }
 }
 
+// the device-resident loss scalars of the step (advantage moments, KL coefficient, 1 / rows): read
+// once per kernel, not at every loss evaluation
+struct LossDyn {
+  float inv_count, adv_mean, adv_invstd, klc;
+};
+__device__ __forceinline__ LossDyn load_dyn(const SfArgs& g) {
+  return {g.dyn[RLKS_DYN_INV_COUNT], g.dyn[RLKS_DYN_ADV_MEAN], g.dyn[RLKS_DYN_ADV_INVSTD], g.dyn[RLKS_DYN_KL_COEFF]};
+}
+
 // PPO loss of one row (RLlib ppo_torch_policy semantics): d loss / d logits (pi) or
 // d loss / d value (vf), scaled by 1 / global rows, and the row's [policy loss, vf loss, kl,
 // entropy] terms
 template <int A_, int NET>
-__device__ __forceinline__ void sf_loss_t(const SfArgs& g, const float (&out)[A_], const RecTail<A_>& r,
-                                          float (&dl)[A_], float (&st)[4]) {
-  const float inv_count = g.dyn[RLKS_DYN_INV_COUNT];
+__device__ __forceinline__ void sf_loss_t(const SfArgs& g, const LossDyn& dy, const float (&out)[A_],
+                                          const RecTail<A_>& r, float (&dl)[A_], float (&st)[4]) {
+  const float inv_count = dy.inv_count;
   st[0] = st[1] = st[2] = st[3] = 0.f;
   if (NET == 0) {
     const float* lo = r.lo;
-    const float adv = (r.adv - g.dyn[RLKS_DYN_ADV_MEAN]) * g.dyn[RLKS_DYN_ADV_INVSTD];
+    const float adv = (r.adv - dy.adv_mean) * dy.adv_invstd;
     const float logp_old = r.lpo;
     const int act = (int)r.act;
     float mx = out[0], mo = lo[0];
@@ -345,7 +354,7 @@ __device__ __forceinline__ void sf_loss_t(const SfArgs& g, const float (&out)[A_
     const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
     const float inr = (ratio >= lo_c && ratio <= hi_c) ? 1.f : 0.f;
     const float dr = -adv * (w1 + (1.f - w1) * inr) * ratio;
-    const float klc = g.dyn[RLKS_DYN_KL_COEFF];
+    const float klc = dy.klc;
 #pragma unroll
     for (int a = 0; a < A_; ++a) {
       float d = dr * ((a == act ? 1.f : 0.f) - p[a]);
@@ -368,7 +377,7 @@ __device__ __forceinline__ void sf_loss(const SfArgs& g, const float (&out)[A_],
                                         float (&st)[4]) {
   RecTail<A_> r;
   load_tail<A_, NET>(g, row, r);
-  sf_loss_t<A_, NET>(g, out, r, dl, st);
+  sf_loss_t<A_, NET>(g, load_dyn(g), out, r, dl, st);
 }
 
 
@@ -836,6 +845,12 @@ __device__ __forceinline__ int x_split(const XRaw& r, int gq, int D, int S, h8& 
 // are outstanding (the ring slab of the next step has landed: only the DMA issued this step, and
 // at steps 10 / 11 the next block's X loads, may still be in flight); no wait for the consumers'
 // dZ2 stores
+// a store through the global address space: a generic (flat) store counts on lgkmcnt too
+template <class T>
+__device__ __forceinline__ void gstore(T* p, const T& v) {
+  *(__attribute__((address_space(1))) T*)(p) = v;
+}
+
 template <int VM>
 __device__ __forceinline__ void fw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -978,6 +993,10 @@ __device__ __forceinline__ void f1a_ws_body(const SfArgs& g, const int wg, const
 #pragma unroll
       for (int i = 0; i < 4; ++i) h2[nt][i] = 0.f;
     RecTail<A_> tail{};
+    const LossDyn dy = load_dyn(g);
+    float b3v[A_];
+#pragma unroll
+    for (int a = 0; a < A_; ++a) b3v[a] = N.b3[a];
     float sdz = 1.f;
     int tile_old = 0;
     // (lane offsets laundered per step: opaque())
@@ -1012,9 +1031,9 @@ __device__ __forceinline__ void f1a_ws_body(const SfArgs& g, const int wg, const
         if (false) {
 #endif
 #pragma unroll
-          for (int a = 0; a < A_; ++a) out[a] = sum_rows4(out[a]) + N.b3[a];
+          for (int a = 0; a < A_; ++a) out[a] = sum_rows4(out[a]) + b3v[a];
           float st[4];
-          sf_loss_t<A_, NET>(g, out, tail, dl, st);
+          sf_loss_t<A_, NET>(g, dy, out, tail, dl, st);
           float sv[A_ + 4];
 #pragma unroll
           for (int a = 0; a < A_; ++a) sv[a] = dl[a];
@@ -1075,8 +1094,8 @@ __device__ __forceinline__ void f1a_ws_body(const SfArgs& g, const int wg, const
               lo[j] = y;
             }
             _Float16* dst = dz_old + 8 * lx + (k >> 1) * 1024;
-            *reinterpret_cast<h8*>(dst) = hi;
-            *reinterpret_cast<h8*>(dst + 512) = lo;
+            gstore(reinterpret_cast<h8*>(dst), hi);  // global, not flat: the barrier's lgkmcnt(0) would wait for it
+            gstore(reinterpret_cast<h8*>(dst + 512), lo);
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i) stash[i] = d[i];
@@ -1586,6 +1605,132 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
 #endif
 }
 
+
+// ----------------------------------------------------------------------------- forward only
+// Rollout forward of both nets on 16-row tiles (the F1a schedule above without the loss and the
+// backward epilogue): logits [M][A] of the policy net and values [M] of the value net for M
+// observation rows of stride D.  The node-level rollout (ppo.hip node_rollout) runs it once per step
+// and for the bootstrap; k_sf_roll's 32-row tiles needed 256 registers per wave (2 waves per SIMD),
+// here a wave holds one 16 x 256 accumulator block and four waves share a SIMD.
+// Rows past M (the last tile of a ragged M) are computed on row M - 1 and not stored.
+__device__ __forceinline__ int x_frag_rows(const float* __restrict__ x, int row, int D, int g, h8& xh, h8& xl) {
+  const float* xr = x + (size_t)row * D;
+  float xv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) xv[j] = xa_elem(xr, 8 * g + j, D);
+  float xm = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) xm = fmaxf(xm, fabsf(xv[j]));
+  const int ex = sf_exp(wave_max(xm));
+  split8(xv, 0, pow2(ex), xh, xl);
+  return ex;
+}
+
+template <int A_, int KD, int W>
+constexpr int fwd16_lds_bytes() {
+  return 4 * H16 * 2 + 2 * HID * KD * 2 + (HID + A_ * HID) * 4;
+}
+
+template <int A_, int NET, int KD, int W>
+__device__ __forceinline__ void fwd16_body(const SfFwdArgs& g) {
+  constexpr int NTHR = 64 * W;
+  const SfNet& N = g.n[NET];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  _Float16* sCh = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][128][32]
+  _Float16* sW1 = sCh + 4 * H16;                      // [2 hi/lo][HID][KD]
+  float* sB2 = lds + (4 * H16 * 2 + 2 * HID * KD * 2) / 4;
+  float* sW3 = sB2 + HID;
+
+  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
+  const int row0 = (blockIdx.x * W + w) * 16;
+  const int row = min(row0 + c, g.M - 1);
+
+  hc_dma<W>(N.w2ph, N.w2pl, 0, 0, sCh, w, l);
+  for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i] * SF_2LOG2E;
+  for (int i = tid; i < A_ * HID; i += NTHR) sW3[i] = N.w3[i];
+  w1_stage<KD, NTHR>(N, sW1, tid);
+  h8 xh, xl;
+  const int ex = x_frag_rows(g.x, row, g.D, gq, xh, xl);
+  const float k_z1 = N.sc[1] * pow2(-ex) * SF_2LOG2E;
+  vm_drain();
+  __syncthreads();
+
+  f4 acc[16];
+#pragma unroll
+  for (int nt = 0; nt < 16; ++nt) acc[nt] = f4zero();
+  h8 bh, bl;
+  for (int t = 0; t < 8; ++t) {
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      const int st = 2 * t + ph;
+      if (st < 15) hc_dma<W>(N.w2ph, N.w2pl, 128 * (ph ^ 1), 32 * (t + ph), sCh + (ph ^ 1) * 2 * H16, w, l);
+      if (ph == 0) {
+        f4 z[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          h8 wh, wl;
+          w1_frag<KD>(sW1, 2 * t + b, c, gq, wh, wl);
+          z[b] = mm16x3(wh, wl, xh, xl, f4zero());
+        }
+        float hv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[j] = fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
+        split8(hv, 0, 1.f, bh, bl);
+      }
+      const _Float16* buf = sCh + ph * 2 * H16;
+      h8 ch, cl;
+      hc_frag(buf, 0, c, gq, ch, cl);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        h8 nh, nl;
+        if (j < 7) hc_frag(buf, j + 1, c, gq, nh, nl);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[8 * ph + j] = mm16x3(ch, cl, bh, bl, acc[8 * ph + j]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (j < 7) { ch = nh; cl = nl; }
+      }
+      vm_drain();
+      __syncthreads();
+    }
+  }
+
+  const float k_z2 = N.sc[3] / SF_H1_SCALE * SF_2LOG2E;
+  float out[A_];
+#pragma unroll
+  for (int a = 0; a < A_; ++a) out[a] = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < 16; ++nt) {
+    const int n0 = 16 * nt + 4 * gq;
+    const float4 bb = *reinterpret_cast<const float4*>(sB2 + n0);
+    const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+    float hv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hv[i] = fmaf(-2.f, tanh_r(fmaf(acc[nt][i], k_z2, bv[i])), 1.f);
+#pragma unroll
+    for (int a = 0; a < A_; ++a) {
+      const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
+      out[a] = fmaf(hv[0], t.x, out[a]);
+      out[a] = fmaf(hv[1], t.y, out[a]);
+      out[a] = fmaf(hv[2], t.z, out[a]);
+      out[a] = fmaf(hv[3], t.w, out[a]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < A_; ++a) out[a] = sum_rows4(out[a]) + N.b3[a];
+  // every row group holds the row's outputs: group gq stores actions gq, gq + 4, ...
+  float* dst = g.out[NET];
+  if (dst && row0 + c < g.M)
+#pragma unroll
+    for (int a = 0; a < A_; ++a)
+      if ((a & 3) == gq) dst[(size_t)(row0 + c) * A_ + a] = out[a];
+}
+
+template <int A_, int KD, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_fwd16(SfFwdArgs g) {
+  if (blockIdx.y + g.net0 == 0) fwd16_body<A_, 0, KD, W>(g);
+  else fwd16_body<1, 1, KD, W>(g);
+}
+
 // ----------------------------------------------------------------------------- launchers
 #ifdef RLKS_STAMPS
 extern "C" int rlks_dbg_fa_stamps(unsigned long long* host) {
@@ -1653,6 +1798,32 @@ int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {
   else hipLaunchKernelGGL(k_sf_dw2<32>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
   RLKS_LAUNCHED();
   return RLKS_OK;
+}
+
+
+template <int A_, int KD>
+static int launch_fwd16_t(const SfFwdArgs& a, int net0, int nets, hipStream_t s) {
+  constexpr int W = SF_F1_W;
+  SfFwdArgs b = a;
+  b.net0 = net0;
+  hipLaunchKernelGGL((k_sf_fwd16<A_, KD, W>), dim3((a.M + 16 * W - 1) / (16 * W), nets), dim3(64 * W),
+                     (fwd16_lds_bytes<A_, KD, W>()), s, b);
+  RLKS_LAUNCHED();
+  return RLKS_OK;
+}
+
+int launch_sf_fwd16(const SfFwdArgs& a, int A, hipStream_t s) {
+  RLKS_REQUIRE(a.M > 0 && a.D > 0 && a.D + 1 <= 32, RLKS_ERR_UNSUPPORTED, "split-fp16 forward: obs_dim in [1, 31]");
+  const int net0 = a.out[0] ? 0 : 1, nets = (a.out[0] ? 1 : 0) + (a.out[1] ? 1 : 0);
+  if (nets == 0) return RLKS_OK;
+  if (nets == 1 && net0 == 0) return fail(RLKS_ERR_ARG, "split-fp16 forward: the policy net alone is not a launch shape");
+  const bool k16 = sf_kd(a.D) == 16;
+  switch (A) {
+    case 2: return k16 ? launch_fwd16_t<2, 16>(a, net0, nets, s) : launch_fwd16_t<2, 32>(a, net0, nets, s);
+    case 4: return k16 ? launch_fwd16_t<4, 16>(a, net0, nets, s) : launch_fwd16_t<4, 32>(a, net0, nets, s);
+    case 8: return k16 ? launch_fwd16_t<8, 16>(a, net0, nets, s) : launch_fwd16_t<8, 32>(a, net0, nets, s);
+    default: return fail(RLKS_ERR_UNSUPPORTED, "split-fp16 forward is built for 2, 4 or 8 actions");
+  }
 }
 
 }  // namespace rlks

@@ -179,6 +179,43 @@ def test_ppo_on_node_envs(C, nodes, H, N, T, mb, precision):
     assert bool(torch.isfinite(algo.params.flat).all())
 
 
+@pytest.mark.parametrize("C,N,T", [(4, 1000, 32), (2, 77, 256), (8, 2056, 32)])  # N T % 256 == 0 (sf16)
+def test_node_rollout_ragged_lanes(C, N, T):
+    """node_rollout's split-fp16 forward (k_sf_fwd16, 16-row tiles of 128-row workgroups) with a
+    lane count that is not a multiple of 16 / 128: logits and values of every lane, the last
+    partial tile included, per element against fp64 / fp32 references; transitions bit-exact"""
+    from rlks.env import NodeSpec
+    from rlks.ppo import PPO, PPOConfig
+    from rlks.tables import synthetic_table
+
+    d = _dev()
+    tab = synthetic_table(C, 100, seed=3)
+    spec = NodeSpec(C, 16, arrival_rate=1.0, depart_prob=0.05, init_occupancy=0.5)
+    cfg = (PPOConfig().framework("torch")
+           .training(train_batch_size=N * T, sgd_minibatch_size=N * T, num_sgd_iter=1, lr=3e-4)
+           .debugging(seed=11))
+    cfg.num_envs, cfg.table, cfg.nodes = N, tab, spec
+    cfg.rollout_fragment_length = T
+    algo = PPO(config=cfg, device=d)
+    assert algo.precision == "sf16" and algo.A == C
+    algo.rollout(explore=True)
+    b = {k: v.cpu().numpy() for k, v in algo.buf.items()}
+    ora = oracle.OracleEnv(oracle.make_cfg(N, 100, C, noise_mode=0, seed=11, autoreset=1, nodes=16, arrival_rate=1.0,
+                                           depart_prob=0.05, init_occupancy=0.5),
+                           tab.cost, tab.latency, spec.node_cpu_m, spec.node_mem_mi, None)
+    np.testing.assert_array_equal(ora.reset().view(np.uint32), b["obs"][0].view(np.uint32))
+    for t in range(T):
+        o, r, term, _, _, _ = ora.step(b["actions"][t])
+        np.testing.assert_array_equal(o.view(np.uint32), b["obs"][t + 1].view(np.uint32))
+    flat = algo.params.flat.cpu().numpy()
+    for t in (0, 1, T):
+        el, ev = oracle.mlp_forward(flat, algo.params.offsets, 3 * C, 256, C, b["obs"][t])
+        fl, fv = oracle.mlp_forward(flat, algo.params.offsets, 3 * C, 256, C, b["obs"][t], dtype=np.float32)
+        close_as_fp32(b["values"][t], ev, fv, what=f"values[{t}]")
+        if t < T:
+            close_as_fp32(b["logits"][t], el, fl, what=f"logits[{t}]")
+
+
 def test_node_rollout_full_c3_size():
     """BASELINE configs[2] through the agent: PPO.rollout over 65,536 envs x 8 clusters x 256 nodes
     (bench.py's c3 env: Poisson(1) arrivals, stationary departures), T = 4 steps of node_rollout
