@@ -291,12 +291,16 @@ def mlp_forward(flat, off, D, H, A, obs, dtype=np.float64):
 
 
 def ppo_loss_grad(flat, off, D, H, A, mb, *, clip_param=0.3, vf_clip_param=10.0, vf_loss_coeff=1.0,
-                  entropy_coeff=0.0, kl_coeff=0.2, adv_mean=0.0, adv_inv_std=1.0, count=None, dtype=np.float64):
+                  entropy_coeff=0.0, kl_coeff=0.2, adv_mean=0.0, adv_inv_std=1.0, count=None, dtype=np.float64,
+                  scale=False):
     """Gradient of RLlib's PPO torch loss w.r.t. the flat parameters, float64 autograd
     (dtype=np.float32: the same in torch fp32 on the CPU, the precision baseline of the tests).
 
     mb: packed minibatch records [rows][stride] = [obs D | logits_old A | adv | vtarg | logp_old | action]
-    Returns (grad (same length as flat), stats dict of per-row sums).
+    Returns (grad (same length as flat), stats dict of per-row sums); scale=True adds stats["scale"]:
+    per parameter, the sum over rows of the absolute per-row terms of its gradient (|dZ|^T |input|
+    for a weight, sum |dZ| for a bias): the magnitude a summation error is proportional to, i.e.
+    each element's own cancellation scale (test infrastructure: tests/parity.py).
     """
     import torch
 
@@ -310,12 +314,18 @@ def ppo_loss_grad(flat, off, D, H, A, mb, *, clip_param=0.3, vf_clip_param=10.0,
     vt = rec[:, D + A + 1]
     logp_old = rec[:, D + A + 2]
     act = rec[:, D + A + 3].long()
-    outs = []
+    outs, acts = [], []
     for net in (0, 1):
         w1, b1, w2, b2, w3, b3 = _net(torch, f, off, D, H, A, net)
-        h1 = torch.tanh(x @ w1.T + b1)
-        h2 = torch.tanh(h1 @ w2.T + b2)
-        outs.append(h2 @ w3.T + b3)
+        z1 = x @ w1.T + b1
+        h1 = torch.tanh(z1)
+        z2 = h1 @ w2.T + b2
+        h2 = torch.tanh(z2)
+        out = h2 @ w3.T + b3
+        for z in (z1, z2, out):
+            z.retain_grad()
+        outs.append(out)
+        acts.append((z1, h1, z2, h2, out))
     logits, value = outs[0], outs[1][:, 0]
     logp_all = torch.log_softmax(logits, dim=1)
     logp = logp_all.gather(1, act[:, None])[:, 0]
@@ -329,6 +339,18 @@ def ppo_loss_grad(flat, off, D, H, A, mb, *, clip_param=0.3, vf_clip_param=10.0,
     total.backward()
     stats = {"policy_loss": float((-surr).sum().detach()), "vf_loss": float(vf.sum().detach()),
              "kl": float(kl.sum().detach()), "entropy": float(ent.sum().detach()), "rows": rows}
+    if scale:
+        sc = np.zeros(len(flat))
+        for net, (z1, h1, z2, h2, out) in enumerate(acts):
+            terms = []
+            for dz, inp in ((z1.grad, x), (z2.grad, h1), (out.grad, h2)):
+                adz = dz.abs().double()
+                terms += [adz.T @ inp.detach().abs().double(), adz.sum(0)]
+            for j, t in enumerate(terms):
+                o = off[6 * net + j]
+                v = t.numpy().ravel()
+                sc[o:o + v.size] = v
+        stats["scale"] = sc
     return f.grad.numpy(), stats
 
 

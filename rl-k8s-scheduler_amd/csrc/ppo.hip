@@ -537,6 +537,12 @@ static int sf_prep(const rlks_mlp_desc* d, const SfWs& w, const float* params, h
   return launch_sf_prep(pa, s);
 }
 
+// 2-cloud split-fp16 rollouts: up to this many lanes one persistent k_sf_roll launch runs the whole
+// rollout (each workgroup loops over the T steps of its 32 lanes: a latency design, c2's 4,096 lanes
+// are 128 workgroups); above it each step is k_sf_fwd16 + k_sample_step over all lanes (c4: 131,072
+// lanes, 24.5 -> 14.5 ms per rollout, profiles/r04c)
+constexpr int SF_ROLL_FUSED_MAX_LANES = 16384;
+
 static bool is_wide(const rlks_mlp_desc* d) { return d->precision == RLKS_PRECISION_WIDE || wide_needed(d); }
 
 // the fused kernels (mlp_fwd / mlp_bwd / sgd_sf16 / rollout_sf16) cover hidden 256, obs < 32 and
@@ -1206,6 +1212,35 @@ int rlks_rollout_ws(rlks_env* env, const rlks_mlp_desc* d, const float* params, 
   if (cfg.nodes_per_cluster > 0) {
     RLKS_REQUIRE(cfg.autoreset, RLKS_ERR_ARG, "rlks_rollout_ws: node-level rollout needs autoreset lanes");
     return node_rollout(env, d, params, b, explore, &w, s);
+  }
+#ifdef ROLL_XP_STEPWISE
+  if (true) {
+#else
+  if (N > SF_ROLL_FUSED_MAX_LANES) {
+#endif
+    // per step: the 16-row forward of both nets (k_sf_fwd16), then the fused sample + env step
+    // (k_sample_step); V(obs[T]) by one more forward
+    if (int rc = sf_prep(d, w, params, s, true)) return rc;
+    const Layout L = make_layout(D, HID, A);
+    SfFwdArgs f{};
+    for (int net = 0; net < 2; ++net) {
+      const NetPtrs P = net_ptrs_host(params, L, net);
+      f.n[net] = w.n[net];
+      f.n[net].b2 = P.b2; f.n[net].w3 = P.w3; f.n[net].b3 = P.b3;
+    }
+    f.M = N; f.D = D;
+    for (int t = 0; t <= b->T; ++t) {
+      const size_t tN = (size_t)t * N;
+      f.x = b->obs + tN * D;
+      f.out[0] = t < b->T ? b->logits + tN * A : nullptr;
+      f.out[1] = b->values + tN;
+      if (int rc = launch_sf_fwd16(f, A, s)) return rc;
+      if (t == b->T) break;
+      if (int rc = rlks_env_sample_step(env, b->logits + tN * A, explore, b->actions + tN, b->logp + tN,
+                                        b->obs + (tN + N) * D, b->rewards + tN, b->dones + tN, s))
+        return rc;
+    }
+    return RLKS_OK;
   }
   if (int rc = sf_prep(d, w, params, s, true)) return rc;
   const Layout L = make_layout(D, HID, A);

@@ -96,7 +96,7 @@ int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
 // halves: 1 = F1a (k_sf_fwd), 2 = F1b (k_sf_bwd), 3 = both
 int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int halves = 3);  // needs M % 256 == 0
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
-// F1a's partials of dW3 / db3 / stats per net (the warp-specialised F1a writes one per workgroup)
+// F1a's partials of dW3 / db3 / stats per net (one per F1 workgroup)
 int sf_f1a_parts(int M, int A);
 
 }  // namespace rlks

@@ -751,392 +751,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   else f1a_body<1, 1, KD, W>(g);
 }
 
-// ----------------------------------------------------------------------------- F1a, warp-specialised
-// (round 4; 2 and 4 actions).  k_sf_fwd above runs each tile's MFMA phase (Z1, Z2) and its VALU
-// epilogue (tanh, head, loss, dW3, dZ2 split) in the same wave, and the eight waves of a workgroup
-// reach the epilogue together: the matrix pipe idles through ~15k of a wave's ~60k cycles
-// (profiles/r03w stamps) and the 5.9 VALU per MFMA are issued in series with the MFMAs.  Here the
-// two kinds of work run in different waves of one persistent 1,024-thread workgroup per CU:
-//   producer wave p (8 per workgroup, two per SIMD), per 128-row block: the tile's H1 (Z1 MFMAs,
-//     tanh, split: the B operand, held in 64 registers), then Z2^T = W2 H1^T one 16-row n-tile per
-//     step (8 k-tiles x 3 MFMAs; W2 slabs [16 n][256 k] streamed through a four-slot LDS ring by
-//     LDS-DMA two steps ahead), each finished 16 x 16 n-tile handed to consumer p through an LDS
-//     mailbox;
-//   consumer wave 8 + p (two per SIMD): per step, H2 = tanh(Z2 + b2) of the n-tile its producer
-//     finished in the previous step and the head's partial sums; at the block boundary the loss;
-//     during the next block's 16 steps the previous tile's dW3 (per 4 n-tiles) and dZ2 (per n-tile,
-//     split and stored in the lane order F1b / F2 read), beside the producers' MFMAs.
-// One s_barrier per step orders the ring slots and the mailboxes.  dZ2 is split at the power of two
-// of an upper bound of the tile's max |dZ2|, known as soon as dl is (max over the tile's rows of
-// sum_a |dl_a| max_n |W3[a][n]|, since |1 - H2^2| <= 1), so that no n-tile waits for the whole
-// tile.  dW3 / db3 / stats accumulate per consumer in LDS over its blocks and are summed over the
-// workgroup's consumers in a fixed order at the end: one partial per workgroup (sf_f1a_parts).
-constexpr int FW_P = 8;                 // producer waves (= consumer waves) per workgroup
-constexpr int FW_THREADS = 128 * FW_P;  // 1,024 threads: one workgroup per CU at 128 registers
-constexpr int FW_SLAB = 8 * 2 * 512;    // halves per ring slot: [8 k-tiles][hi, lo][16 n][32 k]
-constexpr int FW_RING = 4;              // ring slots: the slab of step k + 2 is loaded during step k
-constexpr int FW_MAX_WG = 128;          // workgroups per net (both nets: one per CU)
-
-template <int A_, int KD>
-struct FwLds {  // byte offsets of the LDS regions
-  static constexpr int ring = 0;                            // [FW_RING][FW_SLAB] halves
-  static constexpr int w1 = ring + FW_RING * FW_SLAB * 2;   // [2 hi/lo][HID][KD] halves
-  static constexpr int mbox = w1 + 2 * HID * KD * 2;        // [FW_P][2 slots][64 lanes][4] floats
-  static constexpr int w3 = mbox + FW_P * 2 * 64 * 16;      // [A_][HID] floats
-  static constexpr int b2 = w3 + A_ * HID * 4;              // [HID] floats, times 2 log2(e)
-  static constexpr int a3 = b2 + HID * 4;                   // [FW_P][A_][HID] floats: each consumer's dW3 sums
-  static constexpr int ab = a3 + FW_P * A_ * HID * 4;       // [FW_P][A_ + 4] floats: db3, stats sums
-  static constexpr int mw = ab + FW_P * (A_ + 4) * 4;       // [A_] floats: max_n |W3[a][n]| (the dZ2 bound)
-  static constexpr int ex = mw + 16;                        // [FW_P] ints: the producers' X exponents
-  static constexpr int bytes = ex + FW_P * 4;
-};
-
-// v, opaque to the optimiser: lane-derived offsets laundered per step are formed where they are
-// used instead of being hoisted out of the persistent block loop (and spilled) by LICM / CSE
-__device__ __forceinline__ int opaque(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-// W2 slab of n-tile nt (rows 16 nt .. 16 nt + 15 of w2p, all 256 k) into a ring slot: piece
-// b = 2 kt + plane is the [16 n][32 k] block of k-tile kt, 16-byte piece q of row n at slot
-// q ^ sw16(n) (conflict-free fragment reads, as hc_dma); producer p moves pieces 2p and 2p + 1
-__device__ __forceinline__ void fw_dma(const _Float16* hi, const _Float16* lo, int nt, _Float16* slot, int p, int l) {
-  const int n = l >> 2;
-  const int lane = opaque(n * HID + 8 * ((l & 3) ^ sw16(n)));  // formed per call (see opaque)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int b = 2 * p + i, kt = b >> 1;
-    const _Float16* src = ((b & 1) ? lo : hi) + (16 * nt * HID + 32 * kt) + lane;  // uniform part + lane part
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(slot + b * 512), 16, 0, 0);
-  }
-}
-// (hi, lo) A fragment of k-tile kt of a slab: row n = c, piece g, at lane offset
-// fo = c * 32 + 8 * (g ^ sw16(c)) halves (k-tiles at immediate offsets from it)
-__device__ __forceinline__ void fw_frag(const _Float16* slot, int kt, int fo, h8& fh, h8& fl) {
-  const _Float16* q = slot + fo;
-  fh = *reinterpret_cast<const h8*>(q + kt * 1024);
-  fl = *reinterpret_cast<const h8*>(q + kt * 1024 + 512);
-}
-// the two 16-byte pieces of a record row that hold a lane's Xa columns 8g .. 8g + 7, loaded ahead
-// of use; x_split applies xa_row8's selects and x_frag's scale and split to them
-struct XRaw {
-  v4f a, b;
-};
-__device__ __forceinline__ XRaw x_raw(const SfArgs& g, int row, int gq) {
-  const int S = g.x_stride, base = 8 * gq, pb = base < S - 8 ? base : S - 8;
-  const float* xr = g.x + (size_t)row * S + pb;
-  return XRaw{*reinterpret_cast<const v4f*>(xr), *reinterpret_cast<const v4f*>(xr + 4)};
-}
-__device__ __forceinline__ int x_split(const XRaw& r, int gq, int D, int S, h8& xh, h8& xl) {
-  const int base = 8 * gq, pb = base < S - 8 ? base : S - 8;
-  const float t[8] = {r.a[0], r.a[1], r.a[2], r.a[3], r.b[0], r.b[1], r.b[2], r.b[3]};
-  float xv[8], xm = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int d = base + j;
-    xv[j] = fmaf(t[j], (d < D && pb == base) ? 1.f : 0.f, d == D ? 1.f : 0.f);
-    xm = fmaxf(xm, fabsf(xv[j]));
-  }
-  const int ex = sf_exp(wave_max(xm));
-  split8(xv, 0, pow2(ex), xh, xl);
-  return ex;
-}
-// the per-step barrier; producers first wait until at most VM of their vector-memory operations
-// are outstanding (the ring slab of the next step has landed: only the DMA issued this step, and
-// at steps 10 / 11 the next block's X loads, may still be in flight); no wait for the consumers'
-// dZ2 stores
-// a store through the global address space: a generic (flat) store counts on lgkmcnt too
-template <class T>
-__device__ __forceinline__ void gstore(T* p, const T& v) {
-  *(__attribute__((address_space(1))) T*)(p) = v;
-}
-
-template <int VM>
-__device__ __forceinline__ void fw_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  if (VM >= 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM < 0 ? 0 : VM) : "memory");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int A_, int NET, int KD>
-__device__ __forceinline__ void f1a_ws_body(const SfArgs& g, const int wg, const int nwg) {
-  using LB = FwLds<A_, KD>;
-  const SfNet& N = g.n[NET];
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  char* lb = reinterpret_cast<char*>(lds);
-  _Float16* sRing = reinterpret_cast<_Float16*>(lb + LB::ring);
-  _Float16* sW1 = reinterpret_cast<_Float16*>(lb + LB::w1);
-  float* sMb = reinterpret_cast<float*>(lb + LB::mbox);
-  float* sW3 = reinterpret_cast<float*>(lb + LB::w3);
-  float* sB2 = reinterpret_cast<float*>(lb + LB::b2);
-  float* sA3 = reinterpret_cast<float*>(lb + LB::a3);
-  float* sAB = reinterpret_cast<float*>(lb + LB::ab);
-  float* sMw = reinterpret_cast<float*>(lb + LB::mw);
-  int* sEx = reinterpret_cast<int*>(lb + LB::ex);
-  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
-  const bool prod = w < FW_P;
-  const int p = prod ? w : w - FW_P;
-  const int nblk = g.M / (16 * FW_P);
-  const int nb = (nblk - wg + nwg - 1) / nwg;  // this workgroup's blocks: wg, wg + nwg, ...
-
-  for (int i = tid; i < HID; i += FW_THREADS) sB2[i] = N.b2[i] * SF_2LOG2E;
-  for (int i = tid; i < A_ * HID; i += FW_THREADS) sW3[i] = N.w3[i];
-  for (int i = tid; i < FW_P * A_ * HID; i += FW_THREADS) sA3[i] = 0.f;
-  for (int i = tid; i < FW_P * (A_ + 4); i += FW_THREADS) sAB[i] = 0.f;
-  if (w < A_) {  // max_n |W3[a][n]| (the dZ2 bound), wave a
-    float m = 0.f;
-    for (int n = l; n < HID; n += 64) m = fmaxf(m, fabsf(N.w3[w * HID + n]));
-    m = wave_max(m);
-    if (l == 0) sMw[w] = m;
-  }
-  w1_stage<KD, FW_THREADS>(N, sW1, tid);
-  XRaw xr{};
-  if (prod) {  // the slabs of steps 0 and 1
-    fw_dma(N.w2ph, N.w2pl, 0, sRing, p, l);
-    fw_dma(N.w2ph, N.w2pl, 1, sRing + FW_SLAB, p, l);
-    xr = x_raw(g, (wg * FW_P + p) * 16 + c, gq);
-  }
-  vm_drain();
-  __syncthreads();
-
-  if (prod) {
-    // ---- producer: H1 (B operand, registers) per block; Z2^T n-tile k of the block at step k
-    const float k1 = N.sc[1] * SF_2LOG2E;
-    h8 bh[8], bl[8];
-    for (int bi = 0; bi <= nb; ++bi) {
-      const bool live = bi < nb, more = bi + 1 < nb;
-      const int tile = (wg + bi * nwg) * FW_P + p;
-      // opaque per iteration: the per-step slab addresses are formed at their step, not hoisted out
-      // of the block loop into 32 live 64-bit registers
-      const _Float16 *w2h = N.w2ph, *w2l = N.w2pl;
-      asm volatile("" : "+s"(w2h), "+s"(w2l));
-      // step 0: H1 of the block's tile (k-tile by k-tile, each followed by its n-tile 0 MFMAs); steps
-      // 1-15: one n-tile each, a runtime loop (one copy of the step's code: the consumer's 16 steps
-      // are unrolled, and the two roles' code shares the instruction cache)
-#pragma unroll 1
-      for (int k = 0; k < 16; ++k) {
-#ifdef FW_XP_NODMA
-        const bool dma = false;
-#else
-        const bool dma = live && (k < 14 || more);  // the slab of step k + 2 (the next block's after k = 13)
-#endif
-        if (live) {
-          if (dma) fw_dma(w2h, w2l, (k + 2) & 15, sRing + ((k + 2) & (FW_RING - 1)) * FW_SLAB, p, l);
-          const _Float16* slab = sRing + (k & (FW_RING - 1)) * FW_SLAB;
-          const int lo_ = opaque(l), cc = lo_ & 15, gg = lo_ >> 4;
-          const int fo = cc * 32 + 8 * (gg ^ sw16(cc));
-          float* mb = sMb + p * 512 + 4 * lo_;
-          f4 acc = f4zero();
-          if (k == 0) {  // H1^T of k-tile t (two Z1^T tiles, tanh, split), then its n-tile 0 MFMAs
-            h8 xh, xl;
-            const int ex = x_split(xr, gg, g.D, g.x_stride, xh, xl);
-            if (lo_ == 0) sEx[p] = ex;  // stored by the consumer (producers keep their vmcnt to the ring)
-            const float k_z1 = k1 * pow2(-ex);
-            // W1a fragment rows 16 kt + c at immediate offsets from the lane's row-c piece (w1_off: the
-            // KD = 32 swizzle depends on c only)
-            const _Float16* w1b = sW1 + w1_off<KD>(cc, gg & (KD / 8 - 1));
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-              f4 z[2];
-#pragma unroll
-              for (int b = 0; b < 2; ++b) {
-                const _Float16* q = w1b + (2 * t + b) * 16 * KD;
-                const h8 wh = *reinterpret_cast<const h8*>(q), wl = *reinterpret_cast<const h8*>(q + HID * KD);
-                z[b] = mm16x3(wh, wl, xh, xl, f4zero());
-              }
-              float hv[8];  // 2^14 tanh = 2^14 - 2^15 r
-#pragma unroll
-              for (int j = 0; j < 8; ++j) hv[j] = fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
-              split8(hv, 0, 1.f, bh[t], bl[t]);
-              h8 fh, fl;
-              fw_frag(slab, t, fo, fh, fl);
-              acc = mm16x3(fh, fl, bh[t], bl[t], acc);
-            }
-          } else {  // fragments two k-tiles ahead of their MFMAs
-            h8 ch[3], cl[3];
-            fw_frag(slab, 0, fo, ch[0], cl[0]);
-            fw_frag(slab, 1, fo, ch[1], cl[1]);
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-              if (t < 6) fw_frag(slab, t + 2, fo, ch[(t + 2) % 3], cl[(t + 2) % 3]);
-              __builtin_amdgcn_sched_barrier(0);
-#ifdef FW_XP_NOMFMA
-              acc[0] += (float)ch[t % 3][0] + (float)cl[t % 3][0];
-#else
-              acc = mm16x3(ch[t % 3], cl[t % 3], bh[t], bl[t], acc);
-#endif
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          }
-          *reinterpret_cast<f4*>(mb + (k & 1) * 256) = acc;
-          if (k == 10 && more) xr = x_raw(g, (tile + nwg * FW_P) * 16 + cc, gg);  // the next block's X
-        }
-        // the slab of step k + 1 (issued at step k - 1) must have landed: younger than it are this
-        // step's DMA (2) and, at steps 10 / 11, the X loads (2)
-        if ((k == 10 || k == 11) && more) fw_barrier<4>();
-        else if (dma) fw_barrier<2>();
-        else fw_barrier<0>();
-      }
-    }
-  } else {
-    // ---- consumer: H2 and the head per n-tile; at the block boundary the loss and the dZ2 scale;
-    // the previous tile's dW3 (per 4 n-tiles) and dZ2 (per n-tile) during the next block's steps
-    const float k_z2 = N.sc[3] / SF_H1_SCALE * SF_2LOG2E;
-    float h2[16][4], out[A_], dl[A_], stash[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int a = 0; a < A_; ++a) out[a] = dl[a] = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < 16; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) h2[nt][i] = 0.f;
-    RecTail<A_> tail{};
-    const LossDyn dy = load_dyn(g);
-    float b3v[A_];
-#pragma unroll
-    for (int a = 0; a < A_; ++a) b3v[a] = N.b3[a];
-    float sdz = 1.f;
-    int tile_old = 0;
-    // (lane offsets laundered per step: opaque())
-    auto receive = [&](const int nt, const int q4, const int lm) {  // H2 = tanh(Z2 + b2) of n-tile nt; the head
-      const f4 z = *reinterpret_cast<const f4*>(sMb + lm + (nt & 1) * 256);
-      const float4 bb = *reinterpret_cast<const float4*>(sB2 + q4 + 16 * nt);
-      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) h2[nt][i] = fmaf(-2.f, tanh_r(fmaf(z[i], k_z2, bv[i])), 1.f);
-#pragma unroll
-      for (int a = 0; a < A_; ++a) {
-        const float4 t = *reinterpret_cast<const float4*>(sW3 + q4 + a * HID + 16 * nt);
-        out[a] = fmaf(h2[nt][0], t.x, out[a]);
-        out[a] = fmaf(h2[nt][1], t.y, out[a]);
-        out[a] = fmaf(h2[nt][2], t.z, out[a]);
-        out[a] = fmaf(h2[nt][3], t.w, out[a]);
-      }
-    };
-    for (int bi = 0; bi <= nb; ++bi) {
-      const bool live = bi < nb, old = bi > 0;
-      const int tile = (wg + bi * nwg) * FW_P + p;
-      _Float16* dz_old = N.dz2s + (size_t)tile_old * (16 * HID * 2);
-      asm volatile("" : "+s"(dz_old));
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int lx = opaque(l), q4 = 4 * (lx >> 4), lm = p * 512 + 4 * lx;
-        if (old && k == 0) {  // the previous tile: its last n-tile, the loss, db3 / stats, the dZ2 scale
-          receive(15, q4, lm);
-#ifdef FW_XP_NOEPI
-          if (lx == 0) N.tile_edz[tile_old] = (int)out[0];
-        }
-        if (false) {
-#endif
-#pragma unroll
-          for (int a = 0; a < A_; ++a) out[a] = sum_rows4(out[a]) + b3v[a];
-          float st[4];
-          sf_loss_t<A_, NET>(g, dy, out, tail, dl, st);
-          float sv[A_ + 4];
-#pragma unroll
-          for (int a = 0; a < A_; ++a) sv[a] = dl[a];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sv[A_ + i] = st[i];
-#pragma unroll
-          for (int i = 0; i < A_ + 4; ++i) {
-            const float t = row_sum16(sv[i]);
-            if (lx == 0) sAB[p * (A_ + 4) + i] += t;
-          }
-          float bnd = 0.f;
-#pragma unroll
-          for (int a = 0; a < A_; ++a) bnd = fmaf(fabsf(dl[a]), sMw[a], bnd);
-          const float dmx = wave_max(bnd);
-          const int edz = dmx > 0.f ? sf_exp(dmx) : 120;  // an all-zero tile: the largest exponent
-          sdz = pow2(edz);
-          if (lx == 0) N.tile_edz[tile_old] = edz;
-#pragma unroll
-          for (int a = 0; a < A_; ++a) out[a] = 0.f;
-        }
-#ifdef FW_XP_NOEPI
-        if (false) {
-#else
-        if (old) {
-#endif
-          if ((k & 3) == 0) {  // dW3 [a][n] of n-tiles k .. k + 3 over the tile's rows: reduce-scatter
-            // over a row's 16 lanes (lane c: n = 16 k + 16 (c >> 2) + 4 g + (c & 3)), into this consumer's sums
-            float* a3p = sA3 + p * A_ * HID + 16 * k + 4 * (lx & 12) + q4 + (lx & 3);
-#pragma unroll
-            for (int a = 0; a < A_; ++a) {
-              float v[16];
-#pragma unroll
-              for (int kk = 0; kk < 16; ++kk) v[kk] = dl[a] * h2[k + (kk >> 2)][kk & 3];
-              a3p[a * HID] += row_reduce16(v, lx);
-            }
-          }
-          // dZ2^T = (dl W3)(1 - H2^2) of n-tile k, split at the tile's bound; stored per n-step
-          // (2 n-tiles): [tile][n-step][hi, lo][lane][8]
-          float gs[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int a = 0; a < A_; ++a) {
-            const float4 t = *reinterpret_cast<const float4*>(sW3 + q4 + a * HID + 16 * k);
-            gs[0] = fmaf(dl[a], t.x, gs[0]);
-            gs[1] = fmaf(dl[a], t.y, gs[1]);
-            gs[2] = fmaf(dl[a], t.z, gs[2]);
-            gs[3] = fmaf(dl[a], t.w, gs[3]);
-          }
-          float d[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) d[i] = gs[i] * (1.f - h2[k][i] * h2[k][i]);
-          if (k & 1) {
-            h8 hi, lo;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              _Float16 x, y;
-              split1((j < 4 ? stash[j & 3] : d[j & 3]) * sdz, x, y);
-              hi[j] = x;
-              lo[j] = y;
-            }
-            _Float16* dst = dz_old + 8 * lx + (k >> 1) * 1024;
-            gstore(reinterpret_cast<h8*>(dst), hi);  // global, not flat: the barrier's lgkmcnt(0) would wait for it
-            gstore(reinterpret_cast<h8*>(dst + 512), lo);
-          } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) stash[i] = d[i];
-          }
-        }
-        if (live && k >= 1) receive(k - 1, q4, lm);
-        if (live && k == 1 && lx == 0) N.tile_ex[tile] = sEx[p];  // written by the producer at step 0
-        if (live && k == 8) load_tail<A_, NET>(g, tile * 16 + (lx & 15), tail);
-        fw_barrier<-1>();
-      }
-      tile_old = tile;
-    }
-  }
-  __syncthreads();
-  // ---- the workgroup's partials: consumers summed in a fixed order
-  for (int e = tid; e < A_ * HID; e += FW_THREADS) {
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < FW_P; ++q) s += sA3[q * A_ * HID + e];
-    N.part_w3[(size_t)wg * A_ * HID + e] = s;
-  }
-  if (tid < A_ + 4) {
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < FW_P; ++q) s += sAB[q * (A_ + 4) + tid];
-    if (tid < A_) N.part_b3[(size_t)wg * A_ + tid] = s;
-    else N.part_stat[(size_t)wg * 4 + tid - A_] = s;
-  }
-}
-
-template <int A_, int KD>
-__global__ __launch_bounds__(FW_THREADS) void k_sf_fwd_ws(SfArgs g) {
-  if (blockIdx.y + g.net0 == 0) f1a_ws_body<A_, 0, KD>(g, blockIdx.x, gridDim.x);
-  else f1a_ws_body<1, 1, KD>(g, blockIdx.x, gridDim.x);
-}
-
-#ifdef FW_XP_OLD
+// F1a's dW3 / db3 / stats partials per net: one per F1 workgroup
 int sf_f1a_parts(int M, int A) { return M / (16 * SF_F1_W); }
-#else
-int sf_f1a_parts(int M, int A) { return A <= 4 ? (M / (16 * FW_P) < FW_MAX_WG ? M / (16 * FW_P) : FW_MAX_WG) : M / (16 * SF_F1_W); }
-#endif
 
 template <int NET, int KD, int ND, int W>
 __device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1 (rows d of dW1a^T)
@@ -1756,17 +1372,7 @@ static int launch_f1_net(SfArgs a, int net0, int nets, hipStream_t s, int halves
   constexpr int W = SF_F1_W;
   a.net0 = net0;
   const dim3 grid(a.M / (16 * W), nets);
-#ifdef FW_XP_OLD
-  if constexpr (false) {
-#else
-  if constexpr (A_ <= 4) {
-#endif
-    if (halves & 1) {  // warp-specialised F1a: one persistent workgroup per CU
-      const dim3 gws(sf_f1a_parts(a.M, A_), nets);
-      hipLaunchKernelGGL((k_sf_fwd_ws<A_, KD>), gws, dim3(FW_THREADS), (FwLds<A_, KD>::bytes), s, a);
-      RLKS_LAUNCHED();
-    }
-  } else if (halves & 1) {  // pi's LDS (A_ >= 1) covers the value net's
+  if (halves & 1) {  // pi's LDS (A_ >= 1) covers the value net's
     hipLaunchKernelGGL((k_sf_fwd<A_, KD, W>), grid, dim3(64 * W), (f1a_lds_bytes<A_, KD, W>()), s, a);
     RLKS_LAUNCHED();
   }

@@ -35,12 +35,12 @@ def main():
         assert (algo.rank, algo.world, algo.groups, algo.group0) == (rank, world, 1, rank)
         results = [algo.train() for _ in range(iters)]
         assert algo._overlap == bool(overlap)
-        prof = algo.profile_allreduce()
         keep = ("episode_reward_mean", "episodes_this_iter", "timesteps_total")
         res = [{k: r[k] for k in keep} | {"kl": r["info"]["learner"]["default_policy"]["learner_stats"]["kl"]}
                for r in results]
-        np.savez(out / f"rank{rank}.npz", params=algo.params.flat.cpu().numpy(),
-                 kl_coeff=np.float32(algo.dyn[2].item()), results=np.array(json.dumps(res)),
+        params, kl = algo.params.flat.cpu().numpy(), np.float32(algo.dyn[2].item())
+        prof = algo.profile_allreduce()  # one more iteration: after the state above is taken
+        np.savez(out / f"rank{rank}.npz", params=params, kl_coeff=kl, results=np.array(json.dumps(res)),
                  allreduce=np.array(json.dumps(prof)))
     finally:
         dist.destroy_process_group()

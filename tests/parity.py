@@ -25,40 +25,68 @@ def rel_errors(x, ref64, ref32, floor=1e-6):
     return np.abs(x - ref64)[keep] / den, np.abs(ref32 - ref64)[keep] / den
 
 
-def assert_pcts(e, e32, factor=4.0, what=""):
+def assert_pcts(e, e32, factor=4.0, what="", max_factor=None):
     if e.size == 0:
         return
     for q in QS:
         a, b = np.percentile(e, q), np.percentile(e32, q)
-        assert a <= factor * b + ULP2, f"{what} p{q}: {a:.3e} vs fp32 {b:.3e}"
+        f = max_factor if (q == 100 and max_factor is not None) else factor
+        assert a <= f * b + ULP2, f"{what} p{q}: {a:.3e} vs fp32 {b:.3e} (worst element {int(e.argmax())})"
 
 
-def close_as_fp32(x, ref64, ref32, factor=4.0, floor=1e-6, what=""):
+def close_as_fp32(x, ref64, ref32, factor=4.0, floor=1e-6, what="", max_factor=8.0):
     """element-wise relative error of x against the float64 reference no worse than the float32
-    reference's by `factor` at the 50th / 99th / 99.9th percentiles and the maximum"""
+    reference's by `factor` at the 50th / 99th / 99.9th percentiles and by `max_factor` at the
+    maximum: the worst element of a sample sits where the sum cancels (a logit or value near zero),
+    and there the fp32 reference's own error is a matter of luck as much as of precision (the same
+    reasoning as grad_close_as_fp32's per-tensor maximum)"""
     e, e32 = rel_errors(x, ref64, ref32, floor)
-    assert_pcts(e, e32, factor, what)
+    assert_pcts(e, e32, factor, what, max_factor)
 
 
-def grad_close_as_fp32(g, g64, g32, offsets, shapes, factor=4.0, floor=1e-6, tensor_max_factor=10.0):
-    """the gradient form of test_sf16_gradient_per_element: over all parameter tensors pooled (the
-    floor relative to each tensor's own max), the relative error no worse than the fp32 reference's
-    by `factor` at p50 / p99 / p99.9 and the maximum; per tensor, p99 within `factor` (tensors of at
-    least 100 elements) and the maximum within `tensor_max_factor` (one worst element of a small
-    tensor is a noisy statistic for both precisions)"""
+def grad_close_as_fp32(g, g64, g32, offsets, shapes, factor=4.0, floor=1e-6, scale=None, tensor_factor=4.0,
+                       tensor_max_factor=8.0):
+    """the gradient form of test_sf16_gradient_per_element.
+
+    Pooled over all parameter tensors (the floor relative to each tensor's own max): the relative
+    error |g - g64| / |g64| no worse than the fp32 reference's by `factor` at p50 / p99 / p99.9.
+
+    Per tensor, every element against its own cancellation scale s (oracle.ppo_loss_grad(...,
+    scale=True): the sum over the minibatch rows of the absolute per-row terms of that element):
+    |g - g64| / s at p99 within `tensor_factor` and at the maximum within `tensor_max_factor` of the
+    fp32 reference's.  A gradient element is a sum over the rows; where the rows cancel (|g64| << s,
+    typical of bias gradients under PPO's advantage standardisation) the relative error of any
+    floating-point evaluation is the per-row error times s / |g64|, so the relative error's extreme
+    elements compare the two evaluations' luck at cancellation points, not their precision; the
+    scaled error is what a summation's error bound is proportional to (not asked to beat 2^-22 of
+    it: the split-fp16 representation's own error per row term).  Without `scale`, the per-tensor
+    checks use the relative error (p99 within 6x, max within 10x)."""
     es, e32s = [], []
     for i, shp in enumerate(shapes):
         o, n = offsets[i], int(np.prod(shp))
         e, e32 = rel_errors(g[o:o + n], g64[o:o + n], g32[o:o + n], floor)
-        if e.size:
-            assert e.max() <= tensor_max_factor * e32.max() + ULP2, \
-                f"tensor {i} max: {e.max():.3e} vs fp32 {e32.max():.3e}"
-            if e.size >= 100:
-                assert np.percentile(e, 99) <= factor * np.percentile(e32, 99) + ULP2, \
-                    f"tensor {i} p99: {np.percentile(e, 99):.3e} vs fp32 {np.percentile(e32, 99):.3e}"
         es.append(e)
         e32s.append(e32)
-    assert_pcts(np.concatenate(es), np.concatenate(e32s), factor, "pooled")
+        if scale is not None:
+            s = np.asarray(scale[o:o + n], np.float64)
+            keep = s > 0
+            es_ = np.abs(np.asarray(g[o:o + n], np.float64) - g64[o:o + n])[keep] / s[keep]
+            e32_ = np.abs(np.asarray(g32[o:o + n], np.float64) - g64[o:o + n])[keep] / s[keep]
+            pf, mf = tensor_factor, tensor_max_factor
+        else:
+            es_, e32_ = e, e32
+            pf, mf = 6.0, 10.0
+        if es_.size:
+            assert es_.max() <= mf * e32_.max() + ULP2, \
+                f"tensor {i} max: {es_.max():.3e} vs fp32 {e32_.max():.3e}{' (scaled)' if scale is not None else ''}"
+            if es_.size >= 100:
+                a, b = np.percentile(es_, 99), np.percentile(e32_, 99)
+                assert a <= pf * b + ULP2, \
+                    f"tensor {i} p99: {a:.3e} vs fp32 {b:.3e}{' (scaled)' if scale is not None else ''}"
+    e, e32 = np.concatenate(es), np.concatenate(e32s)
+    for q in QS[:-1]:
+        a, b = np.percentile(e, q), np.percentile(e32, q)
+        assert a <= factor * b + ULP2, f"pooled p{q}: {a:.3e} vs fp32 {b:.3e}"
 
 
 def log_softmax(lo, dtype):

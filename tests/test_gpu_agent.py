@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 
 import oracle
-from parity import grad_close_as_fp32
+from parity import close_as_fp32, grad_close_as_fp32
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -88,13 +88,15 @@ def _start(ora):
 
 
 # ----------------------------------------------------------------------------- rollout carry + sampler (c2)
-def test_rollouts_carry_observations_and_sample_exactly():
-    """c2 size (4,096 lanes x 128 steps), two iterations: the second rollout starts from the
-    observations the first one ended on (obs[T] -> obs[0]), every transition of both rollouts
-    replays bit-exactly in the oracle env, and every sampled action equals the Philox inverse-CDF
-    draw recomputed on the CPU from the stored logits"""
+@pytest.mark.parametrize("N,T", [(4096, 128), (32768, 16)])
+def test_rollouts_carry_observations_and_sample_exactly(N, T):
+    """c2 size (4,096 lanes x 128 steps: the persistent k_sf_roll launch) and 32,768 lanes x 16 steps
+    (above SF_ROLL_FUSED_MAX_LANES: k_sf_fwd16 + k_sample_step per step), two iterations each: the
+    second rollout starts from the observations the first one ended on (obs[T] -> obs[0]), every
+    transition of both rollouts replays bit-exactly in the oracle env, and every sampled action
+    equals the Philox inverse-CDF draw recomputed on the CPU from the stored logits"""
     d = _dev()
-    N, T, seed = 4096, 128, 11
+    seed = 11
     algo = __import__("rlks.ppo", fromlist=["PPO"]).PPO(config=_cfg(N, T, 65536, epochs=1, seed=seed), device=d)
     ora = _start(_oracle_env(N, seed))
     draws = amb = 0
@@ -109,6 +111,15 @@ def test_rollouts_carry_observations_and_sample_exactly():
         algo.rollout(explore=True)
         b = _host(algo)
         n, a, _ = replay(ora, b, seed)
+        if it == 0:  # both nets' forward of the rollout path against fp64 / fp32 (4,096 lanes, 3 steps)
+            flat = algo.params.flat.cpu().numpy()
+            for t in (0, 1, T):
+                x = b["obs"][t][:4096]
+                el, ev = oracle.mlp_forward(flat, algo.params.offsets, 6, 256, 2, x)
+                fl, fv = oracle.mlp_forward(flat, algo.params.offsets, 6, 256, 2, x, dtype=np.float32)
+                close_as_fp32(b["values"][t][:4096], ev, fv, what=f"values[{t}]")
+                if t < T:
+                    close_as_fp32(b["logits"][t][:4096], el, fl, what=f"logits[{t}]")
         draws += n
         amb += a
         lo = b["logits"].astype(np.float64)
@@ -286,9 +297,9 @@ def test_c4_shard_rollout_and_gradient():
               algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, algo.ws.data_ptr(),
               algo.ws.numel(), None)
     dyn = algo.dyn.cpu().numpy()
-    eg, _ = oracle.ppo_loss_grad(algo.params.flat.cpu().numpy(), algo.params.offsets, 6, 256, 2,
-                                 algo.mbuf.cpu().numpy(), kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]),
-                                 adv_inv_std=float(dyn[1]))
+    eg, est = oracle.ppo_loss_grad(algo.params.flat.cpu().numpy(), algo.params.offsets, 6, 256, 2,
+                                   algo.mbuf.cpu().numpy(), kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]),
+                                   adv_inv_std=float(dyn[1]), scale=True)
     eg32, _ = oracle.ppo_loss_grad(algo.params.flat.cpu().numpy(), algo.params.offsets, 6, 256, 2,
                                    algo.mbuf.cpu().numpy(), kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]),
                                    adv_inv_std=float(dyn[1]), dtype=np.float32)
@@ -296,7 +307,7 @@ def test_c4_shard_rollout_and_gradient():
     for i, (name, _, _) in enumerate(TENSOR_NAMES):
         o, n_ = algo.params.offsets[i], int(np.prod(algo.params.shapes[i]))
         assert np.linalg.norm(g[o:o + n_] - eg[o:o + n_]) <= 1e-5 * np.linalg.norm(eg[o:o + n_]) + 1e-12, name
-    grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes)
+    grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes, scale=est["scale"])
 
 
 # ----------------------------------------------------------------------------- c5 node env

@@ -169,10 +169,10 @@ def test_ppo_grad_matches_oracle(rows, A, precision):
               rows, grad.data_ptr(), stats.data_ptr(), ws.data_ptr(), ws.numel(), None)
     g = grad.cpu().numpy()
     eg, est = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, 256, A, mb, entropy_coeff=0.01,
-                                   kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd)
+                                   kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd, scale=True)
     eg32, _ = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, 256, A, mb, entropy_coeff=0.01,
                                    kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd, dtype=np.float32)
-    grad_close_as_fp32(g, eg, eg32, p.offsets, p.shapes)
+    grad_close_as_fp32(g, eg, eg32, p.offsets, p.shapes, scale=est["scale"])
     from rlks.policy import TENSOR_NAMES
 
     for i, (name, _, _) in enumerate(TENSOR_NAMES):
@@ -216,10 +216,10 @@ def test_wide_grad_matches_oracle(rows, D, H, A):
               rows, grad.data_ptr(), stats.data_ptr(), ws.data_ptr(), ws.numel(), None)
     g = grad.cpu().numpy()
     eg, est = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, H, A, mb, entropy_coeff=0.01,
-                                   kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd)
+                                   kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd, scale=True)
     eg32, _ = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, H, A, mb, entropy_coeff=0.01,
                                    kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd, dtype=np.float32)
-    grad_close_as_fp32(g, eg, eg32, p.offsets, p.shapes)
+    grad_close_as_fp32(g, eg, eg32, p.offsets, p.shapes, scale=est["scale"])
     from rlks.policy import TENSOR_NAMES
 
     for i, (name, _, _) in enumerate(TENSOR_NAMES):
@@ -546,11 +546,11 @@ def test_ppo_iteration_parity_and_surface(tmp_path):
               algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, wsb.data_ptr(),
               wsb.numel(), None)
     kw = dict(kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]), adv_inv_std=float(dyn[1]))
-    eg, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 6, 256, 2, mb, **kw)
+    eg, est = oracle.ppo_loss_grad(flat, algo.params.offsets, 6, 256, 2, mb, **kw, scale=True)
     eg32, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 6, 256, 2, mb, dtype=np.float32, **kw)
     g = algo.grad.cpu().numpy()
     assert np.linalg.norm(g - eg) <= 1e-5 * np.linalg.norm(eg)
-    grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes)
+    grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes, scale=est["scale"])
     # full iterations through the RLlib-named surface
     r1 = algo.train()
     r2 = algo.train()

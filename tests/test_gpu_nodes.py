@@ -168,11 +168,11 @@ def test_ppo_on_node_envs(C, nodes, H, N, T, mb, precision):
               algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, algo.ws.data_ptr(),
               algo.ws.numel(), None)
     kw = dict(kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]), adv_inv_std=float(dyn[1]))
-    eg, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 3 * C, H, C, mbh, **kw)
+    eg, est = oracle.ppo_loss_grad(flat, algo.params.offsets, 3 * C, H, C, mbh, **kw, scale=True)
     eg32, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 3 * C, H, C, mbh, dtype=np.float32, **kw)
     g = algo.grad.cpu().numpy()
     assert np.linalg.norm(g - eg) <= 1e-5 * np.linalg.norm(eg)
-    grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes)
+    grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes, scale=est["scale"])
     for _ in range(2):
         r = algo.train()
         assert np.isfinite(r["info"]["learner"]["default_policy"]["learner_stats"]["policy_loss"])
