@@ -17,35 +17,34 @@ using f16v = __attribute__((ext_vector_type(16))) float;
 template <int SHAPE>  // 0: v_mfma_f32_16x16x32_f16 (F1a / F1b), 1: v_mfma_f32_32x32x16_f16 (F2)
 __global__ __launch_bounds__(256) void k_rate(const _Float16* __restrict__ rnd, float* __restrict__ out, int iters) {
   const int t = blockIdx.x * 256 + threadIdx.x;
-  h8 a[2], b[2];
+  h8 a[4], b[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    a[i] = *reinterpret_cast<const h8*>(rnd + ((size_t)t * 32 + 16 * i) % (1 << 20));
-    b[i] = *reinterpret_cast<const h8*>(rnd + ((size_t)t * 32 + 16 * i + 8) % (1 << 20));
-  }
-  f4 c4[8];
-  f16v c16[8];
+  for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const h8*>(rnd + ((size_t)t * 48 + 8 * i) % (1 << 20));
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    c4[i] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < 16; ++q) c16[i][q] = 0.f;
-  }
-  for (int it = 0; it < iters; ++it) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (SHAPE == 0) c4[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i & 1], b[(i >> 1) & 1], c4[i], 0, 0, 0);
-      else c16[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i & 1], b[(i >> 1) & 1], c16[i], 0, 0, 0);
-    }
-  }
+  for (int i = 0; i < 2; ++i) b[i] = *reinterpret_cast<const h8*>(rnd + ((size_t)t * 48 + 32 + 8 * i) % (1 << 20));
   float s = 0.f;
+  // the eight MFMAs of an iteration as one asm block: written in C, the compiler register-renamed
+  // the f32x4 accumulators with ~40 accumulator moves per 8 MFMAs (half the 16x16x32 rate); the
+  // 32x32x16 form compiles clean either way.  Each accumulator is re-read 8 MFMAs after its write.
+#define RATE_BODY(OP)                                                                        \
+  asm volatile(OP " %0, %8, %12, %0\n\t" OP " %1, %9, %12, %1\n\t" OP " %2, %8, %13, %2\n\t"       \
+               OP " %3, %9, %13, %3\n\t" OP " %4, %10, %12, %4\n\t" OP " %5, %11, %12, %5\n\t"     \
+               OP " %6, %10, %13, %6\n\t" OP " %7, %11, %13, %7"                                   \
+               : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5), "+v"(c6), "+v"(c7)     \
+               : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(b[0]), "v"(b[1]))
+  if constexpr (SHAPE == 0) {
+    f4 c0{}, c1{}, c2{}, c3{}, c4{}, c5{}, c6{}, c7{};
+    for (int it = 0; it < iters; ++it) RATE_BODY("v_mfma_f32_16x16x32_f16");
+    const f4 r = c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7;
+    s = r[0] + r[1] + r[2] + r[3];
+  } else {
+    f16v c0{}, c1{}, c2{}, c3{}, c4{}, c5{}, c6{}, c7{};
+    for (int it = 0; it < iters; ++it) RATE_BODY("v_mfma_f32_32x32x16_f16");
+    const f16v r = c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (SHAPE == 0)
-      for (int q = 0; q < 4; ++q) s += c4[i][q];
-    else
-      for (int q = 0; q < 16; ++q) s += c16[i][q];
+    for (int q = 0; q < 16; ++q) s += r[q];
   }
+#undef RATE_BODY
   out[t] = s;
 }
 }  // namespace
