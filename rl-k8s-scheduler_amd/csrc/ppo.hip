@@ -503,9 +503,9 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     n.tile_ex = (int*)take(4LL * (M / 16));
     n.part_w1 = (float*)take(4LL * w.blocks * HID * D);
     n.part_b1 = (float*)take(4LL * w.blocks * HID);
-    n.part_w3 = (float*)take(4LL * w.blocks * An * HID);
-    n.part_b3 = (float*)take(4LL * w.blocks * An);
-    n.part_stat = (float*)take(4LL * w.blocks * 4);
+    n.part_w3 = (float*)take(4LL * w.fa_parts * An * HID);
+    n.part_b3 = (float*)take(4LL * w.fa_parts * An);
+    n.part_stat = (float*)take(4LL * w.fa_parts * 4);
     n.part_w2 = (float*)take(4LL * w.splits * SF_W2_PSTRIDE);
     n.part_b2 = (float*)take(4LL * w.splits * HID);
   }
