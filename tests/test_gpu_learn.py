@@ -141,6 +141,50 @@ def _minibatch(rows, rng, D=6, A=2, p=None, d=None):
     return mb
 
 
+@pytest.mark.parametrize("A", [2, 8])
+def test_sf16_grad_tile_dynamic_range(A):
+    """split-fp16 gradient with every other 16-row tile 'quiet': its rows' dlogits / dvalue 2^-20 of the
+    others' (old logits = the current ones, standardised advantage and value error scaled by 2^-20),
+    so the dZ2 exponents of one F2 row split differ by ~20 (F2 scales a tile's H1 rows
+    by the split's smallest dZ2 exponent, pushing a quiet tile's lo plane toward fp16 subnormals).
+    Per element against fp64 / fp32 (cancellation-scaled, tests/parity.py) and 1e-5 norm-wise."""
+    from rlks import _lib
+
+    d = _dev()
+    D, rows = 3 * A, 4096
+    p = _params(d, seed=77 + A, D=D, A=A)
+    p.desc.precision = 1
+    rng = np.random.default_rng(5)
+    mb = _minibatch(rows, rng, D=D, A=A, p=p, d=d)
+    lg, vv = p.forward(torch.from_numpy(mb[:, :D].copy()).to(d))
+    lg, vv = lg.cpu().numpy(), vv.cpu().numpy()
+    adv_mean, adv_invstd, klc, tiny = 0.3, 0.7, 0.2, 2.0 ** -20
+    quiet = (np.arange(rows) // 16) % 2 == 1
+    mb[:, D + A + 1] = vv + rng.standard_normal(rows).astype(np.float32) * 4
+    mb[quiet, D:D + A] = lg[quiet]                      # ratio 1, KL gradient 0
+    lsm = lg - lg.max(1, keepdims=True)
+    lsm = lsm - np.log(np.exp(lsm).sum(1, keepdims=True))
+    act = mb[:, D + A + 3].astype(np.int64)
+    mb[quiet, D + A + 2] = lsm[quiet, act[quiet]]
+    mb[quiet, D + A] = adv_mean + (mb[quiet, D + A] - adv_mean) * tiny
+    mb[quiet, D + A + 1] = vv[quiet] + rng.standard_normal(int(quiet.sum())).astype(np.float32) * tiny
+    dyn = torch.tensor([adv_mean, adv_invstd, klc, 1.0 / rows, 0, 0, 0, 0], dtype=torch.float32, device=d)
+    co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.0)
+    wsb = C.c_int64()
+    _lib.call("rlks_ppo_workspace_bytes", C.byref(p.desc), rows, C.byref(wsb))
+    ws = torch.empty(wsb.value, dtype=torch.uint8, device=d)
+    grad = torch.zeros(p.padded, device=d)
+    mbt = torch.from_numpy(mb).to(d)
+    _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
+              rows, grad.data_ptr(), None, ws.data_ptr(), ws.numel(), None)
+    g = grad.cpu().numpy()
+    kw = dict(kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd)
+    eg, est = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, 256, A, mb, scale=True, **kw)
+    eg32, _ = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, 256, A, mb, dtype=np.float32, **kw)
+    assert np.linalg.norm(g - eg) <= 1e-5 * np.linalg.norm(eg)
+    grad_close_as_fp32(g, eg, eg32, p.offsets, p.shapes, scale=est["scale"])
+
+
 @pytest.mark.parametrize("rows,A,precision", [(256, 2, 0), (4096, 2, 0), (256, 2, 1), (4096, 2, 1), (65536, 2, 1),
                                               (512, 4, 1), (512, 8, 1), (512, 4, 0), (1024, 8, 0)])
 def test_ppo_grad_matches_oracle(rows, A, precision):
