@@ -461,13 +461,8 @@ __device__ __forceinline__ double node_reward(const EnvView& v, const double* __
 // are adjacent in one wave, whose step/episode loads precede the chosen lane's stores in program
 // order.  Consecutive lanes write consecutive obs floats.  Same results, counters included, as
 // k_node_step's lane per env (the C > 64 path).
-#ifdef RLKS_NODE_EC_WPE  // A/B builds: waves per SIMD the register allocation is held to
-#define NODE_EC_ATTR __attribute__((amdgpu_waves_per_eu(RLKS_NODE_EC_WPE)))
-#else
-#define NODE_EC_ATTR
-#endif
 template <bool LDS_SKIP>
-__global__ void __launch_bounds__(256) NODE_EC_ATTR k_node_step_ec(EnvView v, const double* __restrict__ cost,
+__global__ void __launch_bounds__(256) k_node_step_ec(EnvView v, const double* __restrict__ cost,
                                                       const double* __restrict__ lat,
                                                       const int32_t* __restrict__ actions, float* __restrict__ obs,
                                                       double* __restrict__ rew64, float* __restrict__ rew32,
