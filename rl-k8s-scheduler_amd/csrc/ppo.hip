@@ -1237,13 +1237,9 @@ int rlks_rollout_ws(rlks_env* env, const rlks_mlp_desc* d, const float* params, 
     RLKS_REQUIRE(cfg.autoreset, RLKS_ERR_ARG, "rlks_rollout_ws: node-level rollout needs autoreset lanes");
     return node_rollout(env, d, params, b, explore, &w, s);
   }
-#ifdef ROLL_XP_STEPWISE
-  if (true) {
-#else
-  if (N > SF_ROLL_FUSED_MAX_LANES) {
-#endif
+  if (N > SF_ROLL_FUSED_MAX_LANES && cfg.autoreset) {
     // per step: the 16-row forward of both nets (k_sf_fwd16), then the fused sample + env step
-    // (k_sample_step); V(obs[T]) by one more forward
+    // (k_sample_step, auto-reset lanes); V(obs[T]) by one more forward
     if (int rc = sf_prep(d, w, params, s, true)) return rc;
     const Layout L = make_layout(D, HID, A);
     SfFwdArgs f{};
