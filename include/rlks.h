@@ -166,9 +166,12 @@ int rlks_adv_stats(const double* partials_dev, int n_partials, double count, dou
 int rlks_adv_finalize(const double* sums_dev, float* dyn_dev, void* stream);
 
 /* ============================================================== policy / value MLP (K4) == */
-/* Flat parameter buffer layout (fp32, torch [out][in] weights, each tensor 64-float aligned):
+/* Flat parameter buffer layout (fp32, torch [out][in] weights, each tensor 64-float aligned).
+ * Tensor indices (offsets12[i]):
  *   0 pi.w1 [H][D]  1 pi.b1 [H]  2 pi.w2 [H][H]  3 pi.b2 [H]  4 pi.w3 [A][H]  5 pi.b3 [A]
  *   6 vf.w1 [H][D]  7 vf.b1 [H]  8 vf.w2 [H][H]  9 vf.b2 [H] 10 vf.w3 [1][H] 11 vf.b3 [1]
+ * stored in the order 0 1 6 7 2 3 4 5 8 9 10 11 (both nets' first layers first: the two gradient
+ * buckets of rlks_ppo_grad_step_part are [0, offsets12[2]) and [offsets12[2], padded)).
  * (RLlib FCNet with vf_share_layers=False: _hidden_layers/_logits/_value_branch_separate/
  *  _value_branch.) */
 #define RLKS_N_TENSORS 12
@@ -317,8 +320,8 @@ int rlks_ppo_grad_step_next(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* co
  * runs under part 2's kernels: part 1 = the weight split, the forward / loss kernel (F1a), dW2 / db2
  * (F2) and the reduce of W2, b2, W3, b3 (both nets) and the stats; part 2 = the dH1 / dW1 kernel
  * (F1b) and the reduce of W1, b1 (+ the next gather, `next` is read by part 2 only).  The gradient
- * equals rlks_ppo_grad_step's bit for bit.  Buckets (offsets of rlks_mlp_layout): part 1 =
- * [off[2], off[6]) and [off[8], padded), part 2 = [off[0], off[2]) and [off[6], off[8]).  Other
+ * equals rlks_ppo_grad_step's bit for bit.  Buckets (offsets of rlks_mlp_layout, storage order
+ * above): part 1 = [off[2], padded), part 2 = [off[0], off[2]), one contiguous range each.  Other
  * precisions: the whole gradient in part 1, part 2 only gathers. */
 int rlks_ppo_grad_step_part(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
                             const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,

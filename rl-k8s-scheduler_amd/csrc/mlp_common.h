@@ -100,12 +100,17 @@ struct Layout {
   int64_t padded, real;
 };
 
+// storage order (include/rlks.h): both nets' first layers, then pi's and vf's W2 / b2 / W3 / b3, so
+// that the overlapped all-reduce's two gradient buckets are two contiguous ranges
+// (rlks_ppo_grad_step_part)
+constexpr int LAYOUT_ORDER[RLKS_N_TENSORS] = {0, 1, 6, 7, 2, 3, 4, 5, 8, 9, 10, 11};
 inline Layout make_layout(int D, int H, int A) {
   const int64_t sz[RLKS_N_TENSORS] = {(int64_t)H * D, H, (int64_t)H * H, H, (int64_t)A * H, A,
                                       (int64_t)H * D, H, (int64_t)H * H, H, H, 1};
   Layout L{};
   int64_t o = 0;
-  for (int i = 0; i < RLKS_N_TENSORS; ++i) {
+  for (int j = 0; j < RLKS_N_TENSORS; ++j) {
+    const int i = LAYOUT_ORDER[j];
     L.off[i] = o;
     o += (sz[i] + 63) / 64 * 64;
     L.real += sz[i];

@@ -335,11 +335,12 @@ class PPO:
         self._fused_prev = False
         self._ep_history = collections.deque(maxlen=max(1, int(cfg.metrics_num_episodes_for_smoothing)))
         self._ar_events = None  # profile_allreduce(): (start, compute end, done) events per SGD step
-        # gradient buckets of the overlapped all-reduce (include/rlks.h rlks_ppo_grad_step_part): views of
-        # the flat gradient, W2 / b2 / W3 / b3 of each net (+ alignment padding), then W1 / b1
-        off = list(self.params.offsets) + [self.params.padded]
+        # gradient buckets of the overlapped all-reduce (include/rlks.h rlks_ppo_grad_step_part): two
+        # contiguous views of the flat gradient (storage order: both nets' W1 / b1 first), W2 / b2 /
+        # W3 / b3 of both nets, then W1 / b1 of both
+        off = self.params.offsets
         g = self.grad
-        self._buckets = ([g[off[2]:off[6]], g[off[8]:off[12]]], [g[off[0]:off[2]], g[off[6]:off[8]]])
+        self._buckets = ([g[off[2]:self.params.padded]], [g[off[0]:off[2]]])
         self._overlap = bool(cfg.overlap_allreduce) and self.world > 1 and self.precision == "sf16"
         self.sample_calls = 0   # compute_actions / compute_single_action draws so far (Philox counter)
         self.iteration = 0

@@ -78,10 +78,12 @@ def test_mlp_layout_default_net():
     assert real == 135939  # RLlib FCNet [256, 256], separate value net
     shapes = tensor_shapes(6, 256, 2)
     o = 0
-    for i, s in enumerate(shapes):
+    for i in (0, 1, 6, 7, 2, 3, 4, 5, 8, 9, 10, 11):  # storage order (include/rlks.h)
         assert off[i] == o and off[i] % 64 == 0
-        o += -(-int(np.prod(s)) // 64) * 64
+        o += -(-int(np.prod(shapes[i])) // 64) * 64
     assert padded == o
+    # the overlapped all-reduce's buckets: both nets' W1 / b1, then everything else
+    assert max(off[i] for i in (0, 1, 6, 7)) < off[2] == min(off[i] for i in (2, 3, 4, 5, 8, 9, 10, 11))
 
 
 def test_seed_key_words_match_cpython():
