@@ -229,6 +229,10 @@ constexpr int SKIP_LDS_MAX = 4096;  // survival-table entries staged in LDS (16 
 #define RLKS_NODE_EC_LDS_SKIP_MAX 4096
 #endif
 constexpr int NODE_EC_LDS_SKIP_MAX = RLKS_NODE_EC_LDS_SKIP_MAX;
+#ifndef RLKS_NODE_WL_NP
+#define RLKS_NODE_WL_NP 2
+#endif
+constexpr int NODE_WL_NP = RLKS_NODE_WL_NP;  // (env, cluster) pairs per thread of k_node_step_wl
 #ifndef RLKS_NODE_EC_MAX_C
 #define RLKS_NODE_EC_MAX_C 64  // (A/B builds set 0: every node env on the lane-per-env kernel)
 #endif
@@ -247,9 +251,8 @@ __device__ __forceinline__ void load_chunk(const int2* p, int2 (&f)[8]) {
     f[2 * i + 1] = make_int2(x[2], x[3]);
   }
 }
-// 8 chunk totals (16 bytes); returns their sum
-__device__ __forceinline__ int load_tot8(const uint16_t* p, int (&t)[8]) {
-  const uint4 x = *reinterpret_cast<const uint4*>(p);
+// 8 chunk totals (16 bytes) unpacked; returns their sum
+__device__ __forceinline__ int unpack_tot8(const uint4 x, int (&t)[8]) {
   const uint32_t w[4] = {x.x, x.y, x.z, x.w};
   int s = 0;
 #pragma unroll
@@ -260,9 +263,65 @@ __device__ __forceinline__ int load_tot8(const uint16_t* p, int (&t)[8]) {
   }
   return s;
 }
+__device__ __forceinline__ int load_tot8(const uint16_t* p, int (&t)[8]) {
+  return unpack_tot8(*reinterpret_cast<const uint4*>(p), t);
+}
+// a cluster's chunk totals read on demand, a 16-byte group at a time
+struct TotLoad {
+  const uint16_t* tot;
+  __device__ __forceinline__ int operator()(int g, int (&t)[8]) const { return load_tot8(tot + 8 * g, t); }
+  __device__ __forceinline__ void left(int, int) {}
+};
+// ... or with the first 4 groups (256 nodes) loaded up front, together: one memory round trip
+// where the on-demand walk has one per group it passes
+struct TotPf {
+  uint4 g0, g1, g2, g3;  // (named, not an array: an array here is put in scratch memory)
+  __device__ __forceinline__ TotPf(const uint16_t* p, int nodes) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const int last = (nodes - 1) >> 6;  // the cluster's last group (fewer than 4: reread, never past it)
+    g0 = q[0];
+    g1 = q[min(1, last)];
+    g2 = q[min(2, last)];
+    g3 = q[min(3, last)];
+  }
+  // (clusters of at most 256 nodes only: a load here for the groups past the fourth would be merged
+  // with the selects below into one load through a pointer into scratch memory)
+  // d pods left chunk ch (written back to memory): the same in the registers, so a first fit after
+  // the departures reads the totals it would load
+  __device__ __forceinline__ void left(int ch, int d) {
+    const uint32_t sub = (uint32_t)d << (16 * (ch & 1));
+    const int w = (ch >> 1) & 3, g = ch >> 3;
+    g0.x -= g == 0 && w == 0 ? sub : 0u; g0.y -= g == 0 && w == 1 ? sub : 0u;
+    g0.z -= g == 0 && w == 2 ? sub : 0u; g0.w -= g == 0 && w == 3 ? sub : 0u;
+    g1.x -= g == 1 && w == 0 ? sub : 0u; g1.y -= g == 1 && w == 1 ? sub : 0u;
+    g1.z -= g == 1 && w == 2 ? sub : 0u; g1.w -= g == 1 && w == 3 ? sub : 0u;
+    g2.x -= g == 2 && w == 0 ? sub : 0u; g2.y -= g == 2 && w == 1 ? sub : 0u;
+    g2.z -= g == 2 && w == 2 ? sub : 0u; g2.w -= g == 2 && w == 3 ? sub : 0u;
+    g3.x -= g == 3 && w == 0 ? sub : 0u; g3.y -= g == 3 && w == 1 ? sub : 0u;
+    g3.z -= g == 3 && w == 2 ? sub : 0u; g3.w -= g == 3 && w == 3 ? sub : 0u;
+  }
+  __device__ __forceinline__ static void opaque(uint4& a) {
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w));
+  }
+  __device__ __forceinline__ int operator()(int grp, int (&t)[8]) const {
+    // (the selects act on register values: selects of the members' loads would become one load at
+    // a computed offset, which keeps the object in scratch memory)
+    uint4 a = g0, b = g1, c = g2, d = g3;
+    opaque(a);
+    opaque(b);
+    opaque(c);
+    opaque(d);
+    uint4 x;
+    x.x = grp == 0 ? a.x : grp == 1 ? b.x : grp == 2 ? c.x : d.x;
+    x.y = grp == 0 ? a.y : grp == 1 ? b.y : grp == 2 ? c.y : d.y;
+    x.z = grp == 0 ? a.z : grp == 1 ? b.z : grp == 2 ? c.z : d.z;
+    x.w = grp == 0 ? a.w : grp == 1 ? b.w : grp == 2 ? c.w : d.w;
+    return unpack_tot8(x, t);
+  }
+};
 // write back the chunk's nodes that lost pods and its new total
-__device__ __forceinline__ void flush_chunk(int2* col, uint16_t* tot, int ch, int ctot, const int2 (&f)[8],
-                                            const int (&dep)[8], unsigned long long& n_wr) {
+__device__ __forceinline__ int flush_chunk(int2* col, uint16_t* tot, int ch, int ctot, const int2 (&f)[8],
+                                           const int (&dep)[8], unsigned long long& n_wr) {
   int d = 0;
 #pragma unroll
   for (int q = 0; q < 8; ++q)
@@ -272,6 +331,7 @@ __device__ __forceinline__ void flush_chunk(int2* col, uint16_t* tot, int ch, in
       d += dep[q];
     }
   tot[ch] = (uint16_t)(ctot - d);
+  return d;
 }
 
 // obs row `row` from the lane's used millicores (exact ints, IEEE f32 divide)
@@ -290,13 +350,28 @@ struct NodeCounters {
   unsigned long long checks = 0, placed = 0, rej = 0, dep = 0, wr = 0, rd = 0;
 };
 
+// u < S[x], the survival table's entry x (0 past the table), decided without reading the table
+// wherever the fp32 estimate (1 - p)^x 2^32 = exp2(x lg1p) 2^32 is more than 2^16 from u: the
+// estimate is within ~400 of S[x] for every x and p (tests/test_nodes_host.py checks the bound), so
+// only u within 2^16 of S[x] (~2^-15 of the draws) needs the table, and the answer is the table's.
+__device__ __forceinline__ bool u_below_S(const EnvView& v, const uint32_t* S, int x, uint32_t u, float lg1p) {
+  const float e = exp2f((float)x * lg1p) * 0x1p32f;
+  const float fu = (float)u;
+  if (fu < e - 0x1p16f) return true;
+  if (fu > e + 0x1p16f) return false;
+  return u < (x < v.n_skip ? S[x] : 0u);
+}
+
 // 1. departures of cluster c (nodes `col`, chunk totals `tot`, `used` millicores in/out): the pods
 // are numbered in node order at the start of the step; a geometric skip over the survival table S
 // picks the next departing pod, the chunk holding it is located from the chunk totals (8 totals a
 // 16-byte load) and loaded once, and written back when the walk moves past it.  Philox counter
 // {gid, episode, t | draw << 16, DEPART << 16 | c}.
+// `get` reads the chunk totals (TotLoad or TotPf) and is told what left each chunk written back.
+template <class Tot>
 __device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t* S, uint32_t gid, int ep, int t, int c,
-                                               int2* col, uint16_t* tot, int32_t& used, NodeCounters& k) {
+                                               int2* col, uint16_t* tot, int32_t& used, NodeCounters& k,
+                                               Tot& get) {
   const int N = v.nodes;
   const int32_t pc = v.pod_cpu, pm = v.pod_mem, cc = v.cap[c];
   const int P = used / pc;
@@ -318,25 +393,22 @@ __device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t*
     const uint32_t u = (n & 3) == 0 ? x.x : (n & 3) == 1 ? x.y : (n & 3) == 2 ? x.z : x.w;
     ++n;
     const int R = P - pos;
-    // none of the remaining R pods leaves iff u < S[R].  S[R] ~ (1 - p)^R 2^32 to ~1e-6 relative in
-    // fp32 (< 2^13 absolute): u more than 2^16 below that decides without the table read (the common
-    // case: one dependent L2 load fewer per lane), otherwise the table decides, bit-exactly as before
-    if ((float)u < exp2f((float)R * lg1p) * 0x1p32f - 0x1p16f) break;
-    if (u < (R < v.n_skip ? S[R] : 0u)) break;
+    // none of the remaining R pods leaves iff u < S[R]
+    if (u_below_S(v, S, R, u, lg1p)) break;
     // surviving pods before the departure: the largest s in [0, min(R, L)) with S[s] > u (0 if
     // none), as the oracle's binary search finds it.  S[s] ~ (1 - p)^s 2^32, so s ~ log2(u 2^-32) /
-    // log2(1 - p): start there and step to the exact answer against the table (one or two
-    // independent table reads instead of ~log2 L dependent ones)
+    // log2(1 - p): start there and step to the exact answer (u_below_S: the table is read only
+    // where the estimate cannot tell)
     const int hi = min(R, v.n_skip) - 1;
     int s = (int)fminf(fmaxf(__log2f((float)u * 0x1p-32f) * inv_lg1p, 0.f), (float)hi);
-    while (s > 0 && S[s] <= u) --s;
-    while (s < hi && S[s + 1] > u) ++s;
+    while (s > 0 && !u_below_S(v, S, s, u, lg1p)) --s;
+    while (s < hi && u_below_S(v, S, s + 1, u, lg1p)) ++s;
     const int idx = pos + s;
     pos = idx + 1;
     // pod idx: its group, chunk, node
     for (;;) {
       if (!dcheck(8 * grp < (N >> 3), DC_NODE_GROUP, grp)) grp = ((N >> 3) - 1) >> 3;
-      if (gsum < 0) gsum = load_tot8(tot + 8 * grp, gt);
+      if (gsum < 0) gsum = get(grp, gt);
       if (idx < gcum + gsum) break;
       gcum += gsum;
       ++grp;
@@ -350,7 +422,7 @@ __device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t*
     for (int q = 0; q < 8; ++q) tj = (q == j) ? gt[q] : tj;
     if (!dcheck(8 * grp + j < (N >> 3), DC_NODE_CHUNK, 8 * grp + j)) j = (N >> 3) - 1 - 8 * grp;
     if (8 * grp + j != ch) {
-      if (ch >= 0) flush_chunk(col, tot, ch, ctot, f, dep, k.wr);
+      if (ch >= 0) get.left(ch, flush_chunk(col, tot, ch, ctot, f, dep, k.wr));
       ch = 8 * grp + j;
       ccum = cj;
       ctot = tj;
@@ -376,13 +448,14 @@ __device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t*
     used -= pc;
     ++k.dep;
   }
-  if (ch >= 0) flush_chunk(col, tot, ch, ctot, f, dep, k.wr);  // some pod left this cluster
+  if (ch >= 0) get.left(ch, flush_chunk(col, tot, ch, ctot, f, dep, k.wr));  // some pod left this cluster
 }
 
 // 2. `rem` arriving pods onto cluster a, first fit: chunks whose 8 nodes are all full are skipped
 // by their totals, the others are loaded and filled node by node in order.  rem: pods left over.
+template <class Tot>
 __device__ __forceinline__ void first_fit_cluster(const EnvView& v, int a, int2* col, uint16_t* tot, int& rem,
-                                                  int32_t& used, NodeCounters& k) {
+                                                  int32_t& used, NodeCounters& k, Tot get) {
   const int N = v.nodes, C = v.C;
   const int32_t pc = v.pod_cpu, pm = v.pod_mem;
   const int32_t cc = v.cap[a], cm = v.cap[C + a];
@@ -391,7 +464,7 @@ __device__ __forceinline__ void first_fit_cluster(const EnvView& v, int a, int2*
   int placed = 0, last = -1;
   for (int g = 0; 8 * g < NC && rem > 0; ++g) {
     int gt[8];
-    (void)load_tot8(tot + 8 * g, gt);
+    (void)get(g, gt);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int chn = 8 * g + j;
@@ -428,6 +501,16 @@ __device__ __forceinline__ void first_fit_cluster(const EnvView& v, int a, int2*
   k.rej += (unsigned long long)rem;
 }
 
+__device__ __forceinline__ void depart_cluster(const EnvView& v, const uint32_t* S, uint32_t gid, int ep, int t, int c,
+                                               int2* col, uint16_t* tot, int32_t& used, NodeCounters& k) {
+  TotLoad get{tot};
+  depart_cluster(v, S, gid, ep, t, c, col, tot, used, k, get);
+}
+__device__ __forceinline__ void first_fit_cluster(const EnvView& v, int a, int2* col, uint16_t* tot, int& rem,
+                                                  int32_t& used, NodeCounters& k) {
+  first_fit_cluster(v, a, col, tot, rem, used, k, TotLoad{tot});
+}
+
 __device__ __forceinline__ void node_counters_flush(const EnvView& v, NodeCounters k) {
   if (!v.counters) return;
   k.checks = wave_sum_u64(k.checks);
@@ -446,11 +529,15 @@ __device__ __forceinline__ void node_counters_flush(const EnvView& v, NodeCounte
   }
 }
 
-__device__ __forceinline__ double node_reward(const EnvView& v, const double* __restrict__ cost,
-                                              const double* __restrict__ lat, int t, int a, int rem) {
-  double r = __dmul_rn(v.scale, __dadd_rn(__dmul_rn(v.w_cost, cost[t * v.C + a]), __dmul_rn(v.w_lat, lat[t * v.C + a])));
+// reward of row t's cost and latency of the chosen cluster, `rem` pods rejected
+__device__ __forceinline__ double node_reward_of(const EnvView& v, double cost_ta, double lat_ta, int rem) {
+  double r = __dmul_rn(v.scale, __dadd_rn(__dmul_rn(v.w_cost, cost_ta), __dmul_rn(v.w_lat, lat_ta)));
   if (v.penalty != 0.0) r = __dsub_rn(r, __dmul_rn(v.penalty, (double)rem));
   return r;
+}
+__device__ __forceinline__ double node_reward(const EnvView& v, const double* __restrict__ cost,
+                                              const double* __restrict__ lat, int t, int a, int rem) {
+  return node_reward_of(v, cost[t * v.C + a], lat[t * v.C + a], rem);
 }
 
 // One lane per (env, cluster): lane c of env `lane` walks cluster c's departures; the lane of the
@@ -545,6 +632,241 @@ __global__ void __launch_bounds__(256) k_node_step_ec(EnvView v, const double* _
   node_counters_flush(v, k);
   const unsigned long long m = __ballot(over);
   if (status && (threadIdx.x & 63) == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
+}
+
+// whether cluster c loses a pod this step: the first departure draw of depart_cluster, decided as it
+// decides it (false: its first draw stops the walk, or the cluster has no pods)
+__device__ __forceinline__ bool depart_any(const EnvView& v, const uint32_t* S, uint32_t gid, int ep, int t, int c,
+                                           int32_t used) {
+  const int P = used / v.pod_cpu;
+  if (P == 0) return false;
+  const u32x4 x = philox4x32_10_mad(u32x4{gid, (uint32_t)ep, (uint32_t)t, ((uint32_t)RLKS_PURPOSE_DEPART << 16) | (uint32_t)c},
+                                    v.k0, v.k1);
+  const float lg1p = log1pf(-(float)v.depart_prob) * 1.4426950408889634f;
+  return !u_below_S(v, S, P, x.x, lg1p);
+}
+
+// barrier for LDS traffic only: waits for the workgroup's LDS accesses, not its global stores (a
+// __syncthreads() also waits for every store the wave has in flight)
+__device__ __forceinline__ void lds_barrier() {
+#ifdef WL_XP_FULLBAR
+  __syncthreads(); return;
+#endif
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Work-list form of the lane-per-(env, cluster) step (the same results, counters included), a
+// workgroup of 256 threads over NP * 256 (env, cluster) pairs.  The step is a chain of dependent
+// memory round trips, so the kernel is laid out to keep that chain short: the divergent paths a wave
+// of k_node_step_ec ran for the few lanes that need them (a departing pod's chunk walk in ~1 pair in
+// 8, the chosen cluster's Poisson draw and first fit in 1 in 8) run over one compact list per
+// workgroup, so a workgroup covers NP times the pairs for the same chain:
+//   A (every pair): the step's loads, all issued together (step, episode, action, used millicores,
+//     the obs and reward rows); the first departure draw's decision; a pair whose cluster loses a
+//     pod, and each env's chosen cluster, go on the list;
+//   B (the list, items spread over the 4 waves): depart_cluster, then for the chosen cluster the
+//     arrivals and first fit, in one thread; the chunk totals the walks need come in one load (TotPf);
+//   D (every pair): obs, auto-reset, reward and bookkeeping, from the used millicores B left in LDS.
+// Between B and D only LDS is exchanged (lds_barrier), unless an env of the workgroup auto-resets:
+// its clusters' nodes are then rewritten in D by other threads than B's, after a full barrier.
+// A cluster's nodes are touched by one item of B only, so the order of the list does not matter.
+#ifdef WL_XP_NOWPE
+#define WL_WPE
+#else
+#define WL_WPE __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+#ifdef WL_XP_CLOCK
+__device__ unsigned long long g_wl_clock[65536 * 6];
+#define WL_STAMP(q)                                                                              \
+  if ((threadIdx.x & 63) == 0)                                                                   \
+    g_wl_clock[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 6 + (q)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define WL_STAMP(q)
+#endif
+template <bool LDS_SKIP, int NP>
+__global__ void __launch_bounds__(256) WL_WPE k_node_step_wl(EnvView v, const double* __restrict__ cost,
+                                                      const double* __restrict__ lat,
+                                                      const int32_t* __restrict__ actions, float* __restrict__ obs,
+                                                      double* __restrict__ rew64, float* __restrict__ rew32,
+                                                      uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                      int32_t* __restrict__ step_out, float* __restrict__ final_obs,
+                                                      int32_t* __restrict__ status, int cs) {
+  if (status && status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
+  WL_STAMP(0)
+  constexpr int NT = 256, PB = NP * NT;  // threads, pairs per workgroup
+  constexpr uint16_t ARR = 0x8000, DEP = 0x4000;  // list item flags over the pair index
+  static_assert(PB <= 0x4000, "pair index must fit below the flags");
+  __shared__ uint32_t s_skip[LDS_SKIP ? SKIP_LDS_MAX : 1];
+  __shared__ int32_t s_used[PB];               // per pair: used millicores after B
+  __shared__ int s_t[PB], s_ep[PB], s_rem[PB];  // per env of the workgroup: step, episode, pods arriving
+                                                // (A) / rejected (B)
+  __shared__ uint16_t s_list[PB];              // work list: pair index | ARR | DEP
+  __shared__ double s_oc[PB], s_ol[PB];        // per pair: obs row t + 1 (0 on reset) cost, latency
+  __shared__ double s_rc[PB], s_rl[PB], s_er[PB];  // per env: reward row t cost, latency; running return
+  __shared__ int s_n, s_reset;
+  const int tid = threadIdx.x;
+  const int cm = (1 << cs) - 1;
+  const int env0 = blockIdx.x * (PB >> cs);
+  const int C = v.C, N = v.nodes, D = 3 * C;
+  // ---- A: loads
+  int t[NP], ep[NP], a[NP];
+  int32_t used0[NP];
+  double ocost[NP], olat[NP], rcost[NP], rlat[NP];  // obs row t + 1 (or 0 on reset), reward row t
+  double eret[NP];                                  // the chosen cluster's pair: the running return
+  // (these five wait for D in LDS, not in registers, through B's walks)
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int p = tid + j * NT, c = p & cm, lane = env0 + (p >> cs);
+    t[j] = ep[j] = a[j] = used0[j] = 0;
+    ocost[j] = olat[j] = rcost[j] = rlat[j] = eret[j] = 0.0;
+    if (lane < v.N && c < C) {
+      t[j] = v.step[lane];
+      ep[j] = v.episode[lane];
+      a[j] = actions[lane];
+      used0[j] = v.used_cpu[(size_t)c * v.N + lane];
+      if (t[j] < v.T) {
+        const int t1 = t[j] + 1;
+        const int row = t1 < v.T && !(t1 >= v.max_steps && v.autoreset) ? t1 : 0;
+        ocost[j] = cost[row * C + c];
+        olat[j] = lat[row * C + c];
+        rcost[j] = cost[t[j] * C + c];
+        rlat[j] = lat[t[j] * C + c];
+        if (v.track_returns && c == a[j]) eret[j] = v.ep_ret[lane];
+      }
+    }
+  }
+  if (tid == 0) s_n = s_reset = 0;
+  if (LDS_SKIP)
+    for (int i = tid; i < v.n_skip; i += NT) s_skip[i] = v.skip[i];
+  __syncthreads();
+  WL_STAMP(1)
+  const uint32_t* S = LDS_SKIP ? s_skip : v.skip;
+  // ---- A: the list
+  bool any_reset = false;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int p = tid + j * NT, c = p & cm, el = p >> cs, lane = env0 + el;
+    if (lane < v.N && c < C) {
+      if (!dcheck(a[j] >= 0 && a[j] < C, DC_NODE_ACTION, a[j])) a[j] = 0;
+      if (t[j] < v.T) {
+        if (c == 0) {
+          s_t[el] = t[j];
+          s_ep[el] = ep[j];
+        }
+        s_oc[p] = ocost[j];
+        s_ol[p] = olat[j];
+        if (c == a[j]) {
+          s_rc[el] = rcost[j];
+          s_rl[el] = rlat[j];
+          s_er[el] = eret[j];
+          s_rem[el] = arrivals(v, (uint32_t)(v.env_offset + lane), ep[j], t[j]);  // pods arriving
+        }
+        const int t1 = t[j] + 1;
+        any_reset |= t1 < v.T && t1 >= v.max_steps && v.autoreset;
+        const bool dep =
+            v.depart_prob > 0.0 && depart_any(v, S, (uint32_t)(v.env_offset + lane), ep[j], t[j], c, used0[j]);
+        if (dep || c == a[j]) s_list[atomicAdd(&s_n, 1)] = (uint16_t)(p | (dep ? DEP : 0) | (c == a[j] ? ARR : 0));
+      }
+    }
+    s_used[p] = used0[j];
+  }
+  if (any_reset) s_reset = 1;
+  lds_barrier();
+  WL_STAMP(2)
+  // ---- B: item i of the list goes to wave i % 4, so the items spread over the workgroup's waves
+  NodeCounters k;
+  const int n = s_n;
+  for (int i = ((tid & 63) << 2) | (tid >> 6); i < n; i += NT) {
+    const int it = s_list[i], p = it & (DEP - 1), ci = p & cm, ei = p >> cs, li = env0 + ei;
+    const uint32_t gid = (uint32_t)(v.env_offset + li);
+    int2* col = node_col(v, li) + (size_t)ci * N;
+    uint16_t* tot = chunk_tot(v, li, ci);
+    int32_t used = s_used[p];
+#ifndef WL_XP_NOPF
+    if (N <= 256) {
+      TotPf pf(tot, N);  // (kept equal to memory through the departures)
+      if (it & DEP) depart_cluster(v, S, gid, s_ep[ei], s_t[ei], ci, col, tot, used, k, pf);
+      if (it & ARR) {
+        int rem = s_rem[ei];
+        first_fit_cluster(v, ci, col, tot, rem, used, k, pf);
+        s_rem[ei] = rem;
+      }
+    } else
+#endif
+    {
+      TotLoad tl{tot};
+      if (it & DEP) depart_cluster(v, S, gid, s_ep[ei], s_t[ei], ci, col, tot, used, k, tl);
+      if (it & ARR) {
+        int rem = s_rem[ei];
+        first_fit_cluster(v, ci, col, tot, rem, used, k, tl);
+        s_rem[ei] = rem;
+      }
+    }
+    s_used[p] = used;
+  }
+  if (s_reset) __syncthreads();  // (uniform: written before the last barrier)
+  else lds_barrier();
+  WL_STAMP(3)
+  // ---- D: step (:115-144): row t1 = t + 1, done, auto-reset, obs
+  int n_over = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int p = tid + j * NT, c = p & cm, el = p >> cs, lane = env0 + el;
+    if (!(lane < v.N && c < C)) continue;
+    if (t[j] >= v.T) {  // iloc[t] out of bounds before any change
+      if (c == 0) {
+        ++n_over;
+        if (rew64) rew64[lane] = 0.0;
+        if (rew32) rew32[lane] = 0.f;
+        term[lane] = 0;
+        if (step_out) step_out[lane] = t[j];
+        if (trunc) trunc[lane] = 0;
+      }
+      continue;
+    }
+    const uint32_t gid = (uint32_t)(v.env_offset + lane);
+    int32_t used = s_used[p];
+    const int t1 = t[j] + 1;
+    const bool done = t1 >= v.max_steps;
+    const bool reset = t1 < v.T && done && v.autoreset;
+    if (reset) {
+      if (final_obs) {
+        float* o = final_obs + (size_t)lane * D;
+        o[c] = (float)cost[t1 * C + c];
+        o[C + c] = (float)lat[t1 * C + c];
+        o[2 * C + c] = __fdiv_rn((float)used, (float)(N * v.cap[c]));
+      }
+      used = nodes_reset_cluster(v, node_col(v, lane) + (size_t)c * N, chunk_tot(v, lane, c), c, gid, ep[j] + 1);
+    }
+    if (used != used0[j] || reset) v.used_cpu[(size_t)c * v.N + lane] = used;
+    if (t1 < v.T) {
+      float* o = obs + (size_t)lane * D;
+      o[c] = (float)s_oc[p];
+      o[C + c] = (float)s_ol[p];
+      o[2 * C + c] = __fdiv_rn((float)used, (float)(N * v.cap[c]));
+    }
+    if (c == a[j]) {
+      const int rem = s_rem[el];
+      const double r = node_reward_of(v, s_rc[el], s_rl[el], rem);
+      v.step[lane] = reset ? 0 : t1;
+      if (t1 >= v.T) ++n_over;
+      else if (v.track_returns) track_return_from(v, lane, ep[j], r, done, s_er[el]);
+      if (reset) v.episode[lane] = ep[j] + 1;
+      if (rew64) rew64[lane] = r;
+      if (rew32) rew32[lane] = (float)r;
+      term[lane] = (uint8_t)done;
+      if (step_out) step_out[lane] = t1;
+      if (trunc) trunc[lane] = 0;
+    }
+  }
+  WL_STAMP(4)
+  node_counters_flush(v, k);
+  if (status) {
+    const int m = (int)wave_sum_u64((unsigned long long)n_over);
+    if ((tid & 63) == 0 && m) atomicAdd(&status[1], m);
+  }
 }
 
 // One lane per env, clusters in turn (C > 64: more clusters than a wave has lanes)
@@ -790,6 +1112,11 @@ std::vector<uint32_t> skip32(int pmax, double p) {
 }
 }  // namespace
 
+#ifdef WL_XP_CLOCK
+extern "C" __attribute__((visibility("default"))) int rlks_xp_wl_clock(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(rlks::g_wl_clock), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 extern "C" {
 
 int rlks_env_create(const rlks_env_cfg* cfg, const double* cost, const double* lat, rlks_env** out) {
@@ -980,12 +1307,27 @@ int rlks_env_step(rlks_env* e, const int32_t* actions, float* obs, double* rew64
       int cs = 0;
       while ((1 << cs) < C) ++cs;
       const dim3 grid(cdiv(e->cfg.n_envs, 256 >> cs)), blk(256);
+#ifdef NODE_XP_EC
       if (e->n_skip <= NODE_EC_LDS_SKIP_MAX)
         hipLaunchKernelGGL(k_node_step_ec<true>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64,
                            rew32, term, trunc, step_out, final_obs, status, cs);
       else
         hipLaunchKernelGGL(k_node_step_ec<false>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64,
                            rew32, term, trunc, step_out, final_obs, status, cs);
+#else
+      const dim3 gridw(cdiv(e->cfg.n_envs, (NODE_WL_NP * 256) >> cs));
+      // (the survival table stays in global memory: u_below_S reads it for ~2^-15 of the draws)
+#ifdef WL_XP_LDSSKIP
+      if (e->n_skip <= NODE_EC_LDS_SKIP_MAX)
+#else
+      if (false)
+#endif
+        hipLaunchKernelGGL((k_node_step_wl<true, NODE_WL_NP>), gridw, blk, 0, s, view(e), e->d_cost, e->d_lat, actions,
+                           obs, rew64, rew32, term, trunc, step_out, final_obs, status, cs);
+      else
+        hipLaunchKernelGGL((k_node_step_wl<false, NODE_WL_NP>), gridw, blk, 0, s, view(e), e->d_cost, e->d_lat, actions,
+                           obs, rew64, rew32, term, trunc, step_out, final_obs, status, cs);
+#endif
       RLKS_LAUNCHED();
       return RLKS_OK;
     }

@@ -229,8 +229,10 @@ __device__ __forceinline__ void emit_obs(const EnvView& v, const double* s_tab, 
 }
 
 // episode return bookkeeping (PPO result episode_reward_mean)
-__device__ __forceinline__ void track_return(const EnvView& v, int lane, int ep, double reward, bool done) {
-  double ret = v.ep_ret[lane] + reward;
+// (ep_ret: the lane's running return, v.ep_ret[lane], loaded by the caller)
+__device__ __forceinline__ void track_return_from(const EnvView& v, int lane, int ep, double reward, bool done,
+                                                  double ep_ret) {
+  double ret = ep_ret + reward;
   if (done) {
     v.ret_sum[lane] += ret;
     v.ep_cnt[lane] += 1;
@@ -238,6 +240,9 @@ __device__ __forceinline__ void track_return(const EnvView& v, int lane, int ep,
     ret = 0.0;
   }
   v.ep_ret[lane] = ret;
+}
+__device__ __forceinline__ void track_return(const EnvView& v, int lane, int ep, double reward, bool done) {
+  track_return_from(v, lane, ep, reward, done, v.ep_ret[lane]);
 }
 
 struct StepOut {

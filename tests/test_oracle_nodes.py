@@ -126,6 +126,23 @@ def test_departure_skip_table():
             assert np.round((1.0 - p) ** len(s) * 2.0**32) == 0, p
 
 
+def test_departure_skip_estimate_bound():
+    """the device decides u < S[x] without the table where u is more than 2^16 from the fp32 estimate
+    exp2(x * log2(1 - p)) 2^32 (env.hip:u_below_S): that estimate, computed in fp32 as the device does,
+    stays within 2^12 of the table for every entry (16x inside the margin, for the device exp2's ulps)"""
+    for p in (1e-6, 1e-5, 1.085e-4, 1e-3, 5e-3, 0.02, 0.05, 0.1, 0.3, 0.5, 0.9, 0.99):
+        s = oracle.skip32(20000, p).astype(np.float64)
+        x = np.arange(len(s), dtype=np.float32)
+        lg1p = np.float32(np.log1p(-np.float32(p))) * np.float32(1.4426950408889634)
+        est = np.exp2((x * np.float32(lg1p)).astype(np.float32)).astype(np.float32) * np.float32(2.0**32)
+        assert np.abs(est.astype(np.float64) - s).max() <= 2.0**12, p
+        # a table cut short where it reaches 0 (entries past it read as 0; a full table covers every
+        # pod count the clusters can hold): the estimate there is as close to 0
+        if len(s) < 20001:
+            tail = np.float32(np.exp2(np.float32(len(s)) * lg1p)) * np.float32(2.0**32)
+            assert tail <= 2.0**12, p
+
+
 @pytest.mark.parametrize("p", [0.0, 1e-3, 0.05, 1.0])
 def test_departures_are_geometric_per_pod(p):
     """no arrivals: each step every pod leaves with probability p (mean over many nodes)"""
