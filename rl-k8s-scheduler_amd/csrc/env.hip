@@ -700,8 +700,7 @@ __global__ void __launch_bounds__(256) WL_WPE k_node_step_wl(EnvView v, const do
   static_assert(PB <= 0x4000, "pair index must fit below the flags");
   __shared__ uint32_t s_skip[LDS_SKIP ? SKIP_LDS_MAX : 1];
   __shared__ int32_t s_used[PB];               // per pair: used millicores after B
-  __shared__ int s_t[PB], s_ep[PB], s_rem[PB];  // per env of the workgroup: step, episode, pods arriving
-                                                // (A) / rejected (B)
+  __shared__ int s_t[PB], s_ep[PB], s_rem[PB];  // per env of the workgroup: step, episode, pods rejected
   __shared__ uint16_t s_list[PB];              // work list: pair index | ARR | DEP
   __shared__ double s_oc[PB], s_ol[PB];        // per pair: obs row t + 1 (0 on reset) cost, latency
   __shared__ double s_rc[PB], s_rl[PB], s_er[PB];  // per env: reward row t cost, latency; running return
@@ -761,7 +760,6 @@ __global__ void __launch_bounds__(256) WL_WPE k_node_step_wl(EnvView v, const do
           s_rc[el] = rcost[j];
           s_rl[el] = rlat[j];
           s_er[el] = eret[j];
-          s_rem[el] = arrivals(v, (uint32_t)(v.env_offset + lane), ep[j], t[j]);  // pods arriving
         }
         const int t1 = t[j] + 1;
         any_reset |= t1 < v.T && t1 >= v.max_steps && v.autoreset;
@@ -789,7 +787,7 @@ __global__ void __launch_bounds__(256) WL_WPE k_node_step_wl(EnvView v, const do
       TotPf pf(tot, N);  // (kept equal to memory through the departures)
       if (it & DEP) depart_cluster(v, S, gid, s_ep[ei], s_t[ei], ci, col, tot, used, k, pf);
       if (it & ARR) {
-        int rem = s_rem[ei];
+        int rem = arrivals(v, gid, s_ep[ei], s_t[ei]);
         first_fit_cluster(v, ci, col, tot, rem, used, k, pf);
         s_rem[ei] = rem;
       }
@@ -799,7 +797,7 @@ __global__ void __launch_bounds__(256) WL_WPE k_node_step_wl(EnvView v, const do
       TotLoad tl{tot};
       if (it & DEP) depart_cluster(v, S, gid, s_ep[ei], s_t[ei], ci, col, tot, used, k, tl);
       if (it & ARR) {
-        int rem = s_rem[ei];
+        int rem = arrivals(v, gid, s_ep[ei], s_t[ei]);
         first_fit_cluster(v, ci, col, tot, rem, used, k, tl);
         s_rem[ei] = rem;
       }
