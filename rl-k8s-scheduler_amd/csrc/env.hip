@@ -233,6 +233,10 @@ constexpr int NODE_EC_LDS_SKIP_MAX = RLKS_NODE_EC_LDS_SKIP_MAX;
 #define RLKS_NODE_WL_NP 2
 #endif
 constexpr int NODE_WL_NP = RLKS_NODE_WL_NP;  // (env, cluster) pairs per thread of k_node_step_wl
+#ifndef RLKS_NODE_WL_W
+#define RLKS_NODE_WL_W 1
+#endif
+constexpr int NODE_WL_W = RLKS_NODE_WL_W;  // its waves per workgroup
 #ifndef RLKS_NODE_EC_MAX_C
 #define RLKS_NODE_EC_MAX_C 64  // (A/B builds set 0: every node env on the lane-per-env kernel)
 #endif
@@ -658,7 +662,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // Work-list form of the lane-per-(env, cluster) step (the same results, counters included), a
-// workgroup of 256 threads over NP * 256 (env, cluster) pairs.  The step is a chain of dependent
+// workgroup of W waves over NP * 64 W (env, cluster) pairs.  The step is a chain of dependent
 // memory round trips, so the kernel is laid out to keep that chain short: the divergent paths a wave
 // of k_node_step_ec ran for the few lanes that need them (a departing pod's chunk walk in ~1 pair in
 // 8, the chosen cluster's Poisson draw and first fit in 1 in 8) run over one compact list per
@@ -666,7 +670,7 @@ __device__ __forceinline__ void lds_barrier() {
 //   A (every pair): the step's loads, all issued together (step, episode, action, used millicores,
 //     the obs and reward rows); the first departure draw's decision; a pair whose cluster loses a
 //     pod, and each env's chosen cluster, go on the list;
-//   B (the list, items spread over the 4 waves): depart_cluster, then for the chosen cluster the
+//   B (the list, items spread over the W waves): depart_cluster, then for the chosen cluster the
 //     arrivals and first fit, in one thread; the chunk totals the walks need come in one load (TotPf);
 //   D (every pair): obs, auto-reset, reward and bookkeeping, from the used millicores B left in LDS.
 // Between B and D only LDS is exchanged (lds_barrier), unless an env of the workgroup auto-resets:
@@ -685,8 +689,8 @@ __device__ unsigned long long g_wl_clock[65536 * 6];
 #else
 #define WL_STAMP(q)
 #endif
-template <bool LDS_SKIP, int NP>
-__global__ void __launch_bounds__(256) WL_WPE k_node_step_wl(EnvView v, const double* __restrict__ cost,
+template <bool LDS_SKIP, int NP, int W>
+__global__ void __launch_bounds__(64 * W) WL_WPE k_node_step_wl(EnvView v, const double* __restrict__ cost,
                                                       const double* __restrict__ lat,
                                                       const int32_t* __restrict__ actions, float* __restrict__ obs,
                                                       double* __restrict__ rew64, float* __restrict__ rew32,
@@ -695,7 +699,7 @@ __global__ void __launch_bounds__(256) WL_WPE k_node_step_wl(EnvView v, const do
                                                       int32_t* __restrict__ status, int cs) {
   if (status && status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
   WL_STAMP(0)
-  constexpr int NT = 256, PB = NP * NT;  // threads, pairs per workgroup
+  constexpr int NT = 64 * W, PB = NP * NT;  // threads, pairs per workgroup
   constexpr uint16_t ARR = 0x8000, DEP = 0x4000;  // list item flags over the pair index
   static_assert(PB <= 0x4000, "pair index must fit below the flags");
   __shared__ uint32_t s_skip[LDS_SKIP ? SKIP_LDS_MAX : 1];
@@ -773,10 +777,10 @@ __global__ void __launch_bounds__(256) WL_WPE k_node_step_wl(EnvView v, const do
   if (any_reset) s_reset = 1;
   lds_barrier();
   WL_STAMP(2)
-  // ---- B: item i of the list goes to wave i % 4, so the items spread over the workgroup's waves
+  // ---- B: item i of the list goes to wave i % W, so the items spread over the workgroup's waves
   NodeCounters k;
   const int n = s_n;
-  for (int i = ((tid & 63) << 2) | (tid >> 6); i < n; i += NT) {
+  for (int i = (tid & 63) * W + (tid >> 6); i < n; i += NT) {
     const int it = s_list[i], p = it & (DEP - 1), ci = p & cm, ei = p >> cs, li = env0 + ei;
     const uint32_t gid = (uint32_t)(v.env_offset + li);
     int2* col = node_col(v, li) + (size_t)ci * N;
@@ -1313,17 +1317,17 @@ int rlks_env_step(rlks_env* e, const int32_t* actions, float* obs, double* rew64
         hipLaunchKernelGGL(k_node_step_ec<false>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64,
                            rew32, term, trunc, step_out, final_obs, status, cs);
 #else
-      const dim3 gridw(cdiv(e->cfg.n_envs, (NODE_WL_NP * 256) >> cs));
+      const dim3 gridw(cdiv(e->cfg.n_envs, (NODE_WL_NP * 64 * NODE_WL_W) >> cs)), blkw(64 * NODE_WL_W);
       // (the survival table stays in global memory: u_below_S reads it for ~2^-15 of the draws)
 #ifdef WL_XP_LDSSKIP
       if (e->n_skip <= NODE_EC_LDS_SKIP_MAX)
 #else
       if (false)
 #endif
-        hipLaunchKernelGGL((k_node_step_wl<true, NODE_WL_NP>), gridw, blk, 0, s, view(e), e->d_cost, e->d_lat, actions,
+        hipLaunchKernelGGL((k_node_step_wl<true, NODE_WL_NP, NODE_WL_W>), gridw, blkw, 0, s, view(e), e->d_cost, e->d_lat, actions,
                            obs, rew64, rew32, term, trunc, step_out, final_obs, status, cs);
       else
-        hipLaunchKernelGGL((k_node_step_wl<false, NODE_WL_NP>), gridw, blk, 0, s, view(e), e->d_cost, e->d_lat, actions,
+        hipLaunchKernelGGL((k_node_step_wl<false, NODE_WL_NP, NODE_WL_W>), gridw, blkw, 0, s, view(e), e->d_cost, e->d_lat, actions,
                            obs, rew64, rew32, term, trunc, step_out, final_obs, status, cs);
 #endif
       RLKS_LAUNCHED();
