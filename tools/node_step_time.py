@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Time the c3 node step alone (bench.py's k_node_step leg: 65,536 envs x 8 clusters x 256 nodes,
-graph-replayed), for comparing library builds via RLKS_LIB."""
+graph-replayed), for comparing library builds via RLKS_LIB.  usage: node_step_time.py [stationary|<p> ...]"""
 import json
 import sys
 from pathlib import Path
@@ -28,6 +28,7 @@ if __name__ == "__main__":
         torch.cuda.synchronize()
         return s.elapsed_time(e) / n
 
-    for dp in ("stationary", 0.02):
+    dps = [a if a == "stationary" else float(a) for a in sys.argv[1:]] or ["stationary", 0.02]
+    for dp in dps:
         r = bench.node_env_timing(_A, torch, timed, depart_prob=dp)
         print(json.dumps({k: r[k] for k in ("depart_prob", "ms", "GBps", "frac_hbm")}))
