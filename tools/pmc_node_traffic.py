@@ -22,9 +22,8 @@ def main():
     fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE"), per_kernel(sys.argv[2], "WRITE_SIZE")
     dst = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
     out = json.load(open(dst))
-    # the stationary-churn launch: the survival table read through L2 (k_node_step_ec<false>); the
-    # heavy-churn leg stages it in LDS (<true>)
-    keep = [k for k in fetch if "<false>" in k] or list(fetch)
+    # the stationary-churn launch: the survival table read through L2 (the <false, ...> instance)
+    keep = [k for k in fetch if "<false" in k] or list(fetch)
     for k in keep[:1]:
         f = fetch[k]
         key = "k_node_step"
