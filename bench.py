@@ -12,8 +12,13 @@ env itself generates it); random-init weights; fp32-accurate arithmetic througho
   (--config picks another BASELINE.json workload — c2: 4,096 envs/GPU (configs[1]); c3: 65,536
    node-level envs x 8 clusters x 256 nodes; c5: 64 x 1,024 nodes with the Locust-fitted MMPP
    arrivals and the [2048, 2048] policy on the generic-width path; the default is c4)
-  (N > 1: launched by torch.distributed.run; one rank per GPU over RCCL; weak scaling —
-   every rank owns its own 131,072 lanes, the global minibatch is 65,536 x N rows)
+  (N > 1: one rank per GPU over RCCL.  Either launched by torch.distributed.run (WORLD_SIZE set,
+   and it must equal --gpus), or, with no launcher, this script starts the N ranks itself as child
+   processes (launch_ranks) and exits with the worst rank's status.
+   --scaling weak (default): every rank owns the config's per-GPU lanes and minibatch (c4: 131,072
+   lanes and 65,536 rows; 1,048,576 lanes at 8 GPUs).  --scaling strong: the whole job's work is
+   fixed at 8x the per-GPU figures (c4: 1,048,576 lanes, a 524,288-row global minibatch) and each
+   of the N ranks owns 1/N of it, so one PPO iteration is the same computation at every N.)
 
 Prints ONE JSON line on rank 0.  Also measures, with HIP events on the launch stream, the average
 duration of each kernel of the SGD step (roofline of the dominant one), of the env step kernel and
@@ -133,7 +138,89 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--precision", default="auto", choices=("auto", "sf16", "fp32"), help="SGD-step matrix arithmetic")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak: per-GPU work fixed as N grows; strong: whole-job work fixed (8x the per-GPU config)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous / timing plumbing only: every rank times an empty step on the "
+                         "CPU (gloo) and rank 0 prints the JSON line; no GPU is touched (the launcher's CPU test)")
     return ap.parse_args()
+
+
+STRONG_FACTOR = 8  # --scaling strong: the whole job = 8 x the config's per-GPU lanes and minibatch rows
+
+
+def shard_sizes(args, preset, world):
+    """(lanes, minibatch rows) per rank.  weak: the config's per-GPU figures (or --envs /
+    --minibatch), whatever the world size.  strong: those figures x STRONG_FACTOR for the whole job
+    (or --envs / --minibatch as whole-job totals), split evenly over the ranks."""
+    envs = args.envs or preset["envs"]
+    mb = args.minibatch or preset["minibatch"]
+    if args.scaling == "weak":
+        return envs, mb
+    tot_envs = args.envs or STRONG_FACTOR * preset["envs"]
+    tot_mb = args.minibatch or STRONG_FACTOR * preset["minibatch"]
+    if tot_envs % world or tot_mb % world:
+        raise SystemExit(f"--scaling strong: {tot_envs} lanes / {tot_mb} minibatch rows do not split over {world} ranks")
+    return tot_envs // world, tot_mb // world
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, timeout=None):
+    """`bench.py --gpus N` with no torch.distributed launcher around it: start N fresh child
+    processes of this script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+    MASTER_PORT set (the contract's torch.distributed.run environment), and return the worst exit
+    status.  This process makes no HIP call (a child is started, never exec'd: see the GPU box's
+    rules); it only counts devices, which does not initialise the GPU on this image.  When a rank
+    fails, the others are stopped (they would wait at the next collective forever)."""
+    import subprocess
+
+    backend = os.environ.get("RLKS_DIST_BACKEND", "nccl")
+    if "--dry-run" not in argv and backend == "nccl":
+        import torch
+
+        have = torch.cuda.device_count()
+        if n > have:
+            raise SystemExit(f"bench.py --gpus {n}: only {have} HIP device(s) visible (RCCL needs one GPU per rank; "
+                             "RLKS_DIST_BACKEND=gloo rehearses several ranks on fewer GPUs)")
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL on this pool's host driver (dmabuf IPC)
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
+    t0 = time.monotonic()
+    worst = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            failed = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if failed or (timeout is not None and time.monotonic() - t0 > timeout):
+                worst = failed[0] if failed else 124
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    for p in procs:
+        if p.returncode != 0 and worst == 0:
+            worst = p.returncode
+    return worst if worst >= 0 else 128 - worst
 
 
 def kernel_timing(algo, torch, config="c2", reps=20):
@@ -395,19 +482,68 @@ def pmc_traffic():
     return None
 
 
-def main():
-    args = parse()
+def dry_run(args, world, rank):
+    """--dry-run: the multi-rank contract without a GPU (gloo on the CPU): barrier, an empty timed
+    region, MAX over ranks, one JSON line from rank 0 with the shard sizes the real run would use"""
     import torch
     import torch.distributed as dist
 
+    if world > 1:
+        dist.init_process_group("gloo")
+    preset = CONFIGS[args.config]
+    envs, mb = shard_sizes(args, preset, world)
+    for _ in range(args.warmup):
+        pass
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": elapsed / max(1, args.steps) * 1e3,
+                          "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
+                          "data": "dry-run (launcher plumbing only; no GPU work)",
+                          "config": {"name": args.config, "envs_per_gpu": envs, "minibatch_per_gpu": mb,
+                                     "global_envs": envs * world, "global_minibatch": mb * world,
+                                     "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+METRIC = "env-steps/sec (node), batched rollout+policy update, 1/2/4/8 GPUs; %HBM BW"
+
+
+def main():
+    args = parse()
+    argv = sys.argv[1:]
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE {world} != --gpus {args.gpus}")
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # RCCL ("nccl") over xGMI, one GPU per rank.  RLKS_DIST_BACKEND=gloo is for rehearsing the
         # multi-rank path with several ranks on fewer GPUs (ranks share devices round-robin).
         backend = os.environ.get("RLKS_DIST_BACKEND", "nccl")
+        if backend == "nccl" and local >= torch.cuda.device_count():
+            raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} HIP device(s)")
         device = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
         torch.cuda.set_device(device)
         if backend == "nccl":
@@ -421,8 +557,7 @@ def main():
     from rlks.ppo import PPO, PPOConfig
 
     preset = CONFIGS[args.config]
-    envs = args.envs or preset["envs"]
-    minibatch = args.minibatch or preset["minibatch"]
+    envs, minibatch = shard_sizes(args, preset, world)
     H = preset["hidden"]
     table, nodes = env_setup(args.config)
     cfg = (PPOConfig().environment("K8sMultiCloudEnv").framework("torch")
@@ -514,13 +649,14 @@ def main():
             cpu = {"value": c["value"], "unit": "env-steps/s", "cores": c["cores"], "kind": "port",
                    "sample": c["sample"]}
         result = {
-            "metric": "env-steps/sec (node), batched rollout+policy update, 1/2/4/8 GPUs; %HBM BW",
+            "metric": METRIC,
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": "fp32" if algo.precision == "fp32" else "fp32 (split-fp16 MFMA, fp32-accurate)", "data": "synthetic (env-generated rollouts, random-init FCNet)",
             "config": {"workload": preset["text"], "name": args.config,
                        "envs_per_gpu": envs, "rollout_steps": args.rollout, "minibatch_per_gpu": algo.mb,
-                       "epochs": args.epochs, "global_batch": algo.samples * world, "sgd_precision": algo.precision,
+                       "epochs": args.epochs, "global_batch": algo.samples * world, "global_envs": envs * world,
+                       "global_minibatch": algo.mb * world, "sgd_precision": algo.precision,
                        "parallelism": f"dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "allreduce": allreduce, "kernels": kernels, "finite": finite,
         }

@@ -101,3 +101,26 @@ def test_overlapped_allreduce_is_bit_identical(tmp_path):
     assert p_on["overlapped"] and not p_off["overlapped"]
     print(f"exposed all-reduce per SGD step: overlapped {p_on['allreduce_ms_per_sgd_step']:.3f} ms, "
           f"one bucket {p_off['allreduce_ms_per_sgd_step']:.3f} ms ({p_on['backend']})")
+
+
+def test_bench_launches_two_ranks(tmp_path):
+    """`bench.py --gpus 2` with no torch.distributed launcher: bench.py starts
+    both ranks itself (gloo here: the box has one GPU, both ranks share it; RCCL is the 8-GPU node's),
+    rank 0 prints one JSON line with n_gpus 2 and a finite policy, the whole job's lanes counted"""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    root = HERE.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(RLKS_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--config", "c2", "--envs", "512",
+                        "--rollout", "16", "--minibatch", "4096", "--epochs", "1", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-kernel-timing"], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    j = lines[0]
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["finite"]
+    assert j["config"]["global_batch"] == 2 * 512 * 16
+    assert j["value"] == pytest.approx(2 * 512 * 16 * 2 / (j["ms_per_step"] * 2e-3), rel=1e-6)
+    assert j["allreduce"] is not None
