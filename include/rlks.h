@@ -195,6 +195,9 @@ typedef struct rlks_rollout_bufs {
   float* vtarg;     /* [T][N] */
   int32_t T;
   int32_t N;
+  int32_t global_lanes; /* lanes of the whole data-parallel job (0: N).  The split-fp16 rollout picks
+                           its forward kernel from this count, not from N, so that a lane's rollout
+                           does not depend on how the job's lanes are split over ranks. */
 } rlks_rollout_bufs;
 
 /* T steps of (policy forward -> sample -> env step) into bufs, then the bootstrap values

@@ -40,7 +40,8 @@ int rlks_debug_checks(unsigned long long* out) {
   RLKS_REQUIRE(out, RLKS_ERR_ARG, "rlks_debug_checks: null argument");
   RLKS_HIP(hipDeviceSynchronize());
   const rlks::DcheckReaders& R = rlks::dcheck_readers();
-  RLKS_REQUIRE(R.n >= 11, RLKS_ERR_HIP, "rlks_debug_checks: a translation unit did not register its counters");
+  // RLKS_N_TU: the Makefile's source count (every TU includes rlks_internal.h and registers once)
+  RLKS_REQUIRE(R.n == RLKS_N_TU, RLKS_ERR_HIP, "rlks_debug_checks: registered counter sets != translation units");
   out[0] = out[1] = out[2] = 0;
   for (int i = 0; i < R.n; ++i) {
     unsigned long long v[3];

@@ -223,23 +223,10 @@ __global__ __launch_bounds__(256) void k_env_step2(EnvView v, const double* __re
 // only the clusters where a pod leaves and the first-fit prefix: per env-step about one cluster of
 // nodes at c3's stationary churn instead of all C x N.
 constexpr int SKIP_LDS_MAX = 4096;  // survival-table entries staged in LDS (16 KB)
-// the lane-per-(env, cluster) step stages the table too: at c3's heavy churn (4,096 entries)
-// 0.398 -> 0.314 ms against reading it through L1/L2 (profiles/r03b/node_ab.txt)
-#ifndef RLKS_NODE_EC_LDS_SKIP_MAX
-#define RLKS_NODE_EC_LDS_SKIP_MAX 4096
-#endif
-constexpr int NODE_EC_LDS_SKIP_MAX = RLKS_NODE_EC_LDS_SKIP_MAX;
-#ifndef RLKS_NODE_WL_NP
-#define RLKS_NODE_WL_NP 2
-#endif
-constexpr int NODE_WL_NP = RLKS_NODE_WL_NP;  // (env, cluster) pairs per thread of k_node_step_wl
-#ifndef RLKS_NODE_WL_W
-#define RLKS_NODE_WL_W 1
-#endif
-constexpr int NODE_WL_W = RLKS_NODE_WL_W;  // its waves per workgroup
-#ifndef RLKS_NODE_EC_MAX_C
-#define RLKS_NODE_EC_MAX_C 64  // (A/B builds set 0: every node env on the lane-per-env kernel)
-#endif
+// k_node_step_wl's shape (profiles/r04x, r04y: 1 or 4 pairs a thread and 2-4 waves a workgroup were slower)
+constexpr int NODE_WL_NP = 2;  // (env, cluster) pairs per thread
+constexpr int NODE_WL_W = 1;   // waves per workgroup
+constexpr int NODE_WL_MAX_C = 64;  // clusters per env up to which the work-list kernel runs (2^cs lanes an env)
 
 __device__ __forceinline__ int node_pods(const EnvView& v, int32_t cc, int32_t free_cpu) {
   return (int)(__umul24((uint32_t)(cc - free_cpu), v.pod_mag) >> v.pod_shift);
@@ -544,100 +531,6 @@ __device__ __forceinline__ double node_reward(const EnvView& v, const double* __
   return node_reward_of(v, cost[t * v.C + a], lat[t * v.C + a], rem);
 }
 
-// One lane per (env, cluster): lane c of env `lane` walks cluster c's departures; the lane of the
-// chosen cluster a also draws the arrivals, places them first fit and does the env's bookkeeping
-// (reward, step, episode return); every lane writes its cluster's three obs columns (cost, latency,
-// utilisation) and, on auto-reset, redraws its cluster's occupancy.  A cluster's nodes are touched
-// by its lane only, so the lanes need no synchronisation; an env's CP = 2^cs lanes (C <= CP <= 64)
-// are adjacent in one wave, whose step/episode loads precede the chosen lane's stores in program
-// order.  Consecutive lanes write consecutive obs floats.  Same results, counters included, as
-// k_node_step's lane per env (the C > 64 path).
-template <bool LDS_SKIP>
-__global__ void __launch_bounds__(256) k_node_step_ec(EnvView v, const double* __restrict__ cost,
-                                                      const double* __restrict__ lat,
-                                                      const int32_t* __restrict__ actions, float* __restrict__ obs,
-                                                      double* __restrict__ rew64, float* __restrict__ rew32,
-                                                      uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                      int32_t* __restrict__ step_out, float* __restrict__ final_obs,
-                                                      int32_t* __restrict__ status, int cs) {
-  if (status && status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
-  __shared__ uint32_t s_skip[LDS_SKIP ? SKIP_LDS_MAX : 1];
-  if (LDS_SKIP) {
-    for (int i = threadIdx.x; i < v.n_skip; i += blockDim.x) s_skip[i] = v.skip[i];
-    __syncthreads();
-  }
-  const uint32_t* S = LDS_SKIP ? s_skip : v.skip;
-  const int c = threadIdx.x & ((1 << cs) - 1);
-  const int lane = blockIdx.x * (blockDim.x >> cs) + (threadIdx.x >> cs);
-  const int C = v.C, N = v.nodes, D = 3 * C;
-  bool over = false;
-  NodeCounters k;
-  if (lane < v.N && c < C) {
-    const int t = v.step[lane], ep = v.episode[lane];
-    int a = actions[lane];
-    if (!dcheck(a >= 0 && a < C, DC_NODE_ACTION, a)) a = 0;
-    if (t >= v.T) {  // iloc[t] out of bounds before any change
-      if (c == 0) {
-        over = true;
-        if (rew64) rew64[lane] = 0.0;
-        if (rew32) rew32[lane] = 0.f;
-        term[lane] = 0;
-        if (step_out) step_out[lane] = t;
-        if (trunc) trunc[lane] = 0;
-      }
-    } else {
-      const uint32_t gid = (uint32_t)(v.env_offset + lane);
-      int2* col = node_col(v, lane) + (size_t)c * N;
-      uint16_t* tot = chunk_tot(v, lane, c);
-      int32_t* usedp = v.used_cpu + (size_t)c * v.N + lane;
-      const int32_t used0 = *usedp;
-      int32_t used = used0;
-      if (v.depart_prob > 0.0) depart_cluster(v, S, gid, ep, t, c, col, tot, used, k);
-      int rem = 0;
-      if (c == a) {
-        rem = arrivals(v, gid, ep, t);
-        first_fit_cluster(v, a, col, tot, rem, used, k);
-      }
-      // 3. step (:115-144): row t1 = t + 1, done, auto-reset, obs
-      const int t1 = t + 1;
-      const bool done = t1 >= v.max_steps;
-      const bool reset = t1 < v.T && done && v.autoreset;
-      if (reset) {
-        if (final_obs) {
-          float* o = final_obs + (size_t)lane * D;
-          o[c] = (float)cost[t1 * C + c];
-          o[C + c] = (float)lat[t1 * C + c];
-          o[2 * C + c] = __fdiv_rn((float)used, (float)(N * v.cap[c]));
-        }
-        used = nodes_reset_cluster(v, col, tot, c, gid, ep + 1);
-      }
-      if (used != used0 || reset) *usedp = used;
-      if (t1 < v.T) {
-        const int row = reset ? 0 : t1;
-        float* o = obs + (size_t)lane * D;
-        o[c] = (float)cost[row * C + c];
-        o[C + c] = (float)lat[row * C + c];
-        o[2 * C + c] = __fdiv_rn((float)used, (float)(N * v.cap[c]));
-      }
-      if (c == a) {
-        const double r = node_reward(v, cost, lat, t, a, rem);
-        v.step[lane] = reset ? 0 : t1;
-        if (t1 >= v.T) over = true;
-        else if (v.track_returns) track_return(v, lane, ep, r, done);
-        if (reset) v.episode[lane] = ep + 1;
-        if (rew64) rew64[lane] = r;
-        if (rew32) rew32[lane] = (float)r;
-        term[lane] = (uint8_t)done;
-        if (step_out) step_out[lane] = t1;
-        if (trunc) trunc[lane] = 0;
-      }
-    }
-  }
-  node_counters_flush(v, k);
-  const unsigned long long m = __ballot(over);
-  if (status && (threadIdx.x & 63) == 0 && m) atomicAdd(&status[1], (int)__popcll(m));
-}
-
 // whether cluster c loses a pod this step: the first departure draw of depart_cluster, decided as it
 // decides it (false: its first draw stops the walk, or the cluster has no pods)
 __device__ __forceinline__ bool depart_any(const EnvView& v, const uint32_t* S, uint32_t gid, int ep, int t, int c,
@@ -653,9 +546,6 @@ __device__ __forceinline__ bool depart_any(const EnvView& v, const uint32_t* S, 
 // barrier for LDS traffic only: waits for the workgroup's LDS accesses, not its global stores (a
 // __syncthreads() also waits for every store the wave has in flight)
 __device__ __forceinline__ void lds_barrier() {
-#ifdef WL_XP_FULLBAR
-  __syncthreads(); return;
-#endif
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -664,7 +554,7 @@ __device__ __forceinline__ void lds_barrier() {
 // Work-list form of the lane-per-(env, cluster) step (the same results, counters included), a
 // workgroup of W waves over NP * 64 W (env, cluster) pairs.  The step is a chain of dependent
 // memory round trips, so the kernel is laid out to keep that chain short: the divergent paths a wave
-// of k_node_step_ec ran for the few lanes that need them (a departing pod's chunk walk in ~1 pair in
+// of round 3's k_node_step_ec ran for the few lanes that need them (a departing pod's chunk walk in ~1 pair in
 // 8, the chosen cluster's Poisson draw and first fit in 1 in 8) run over one compact list per
 // workgroup, so a workgroup covers NP times the pairs for the same chain:
 //   A (every pair): the step's loads, all issued together (step, episode, action, used millicores,
@@ -676,21 +566,8 @@ __device__ __forceinline__ void lds_barrier() {
 // Between B and D only LDS is exchanged (lds_barrier), unless an env of the workgroup auto-resets:
 // its clusters' nodes are then rewritten in D by other threads than B's, after a full barrier.
 // A cluster's nodes are touched by one item of B only, so the order of the list does not matter.
-#ifdef WL_XP_NOWPE
-#define WL_WPE
-#else
-#define WL_WPE __attribute__((amdgpu_waves_per_eu(4)))
-#endif
-#ifdef WL_XP_CLOCK
-__device__ unsigned long long g_wl_clock[65536 * 6];
-#define WL_STAMP(q)                                                                              \
-  if ((threadIdx.x & 63) == 0)                                                                   \
-    g_wl_clock[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 6 + (q)] = __builtin_amdgcn_s_memrealtime();
-#else
-#define WL_STAMP(q)
-#endif
-template <bool LDS_SKIP, int NP, int W>
-__global__ void __launch_bounds__(64 * W) WL_WPE k_node_step_wl(EnvView v, const double* __restrict__ cost,
+template <int NP, int W>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) k_node_step_wl(EnvView v, const double* __restrict__ cost,
                                                       const double* __restrict__ lat,
                                                       const int32_t* __restrict__ actions, float* __restrict__ obs,
                                                       double* __restrict__ rew64, float* __restrict__ rew32,
@@ -698,11 +575,9 @@ __global__ void __launch_bounds__(64 * W) WL_WPE k_node_step_wl(EnvView v, const
                                                       int32_t* __restrict__ step_out, float* __restrict__ final_obs,
                                                       int32_t* __restrict__ status, int cs) {
   if (status && status[0] != 0) return;  // some action was invalid: nothing steps (reference assert, :116)
-  WL_STAMP(0)
   constexpr int NT = 64 * W, PB = NP * NT;  // threads, pairs per workgroup
   constexpr uint16_t ARR = 0x8000, DEP = 0x4000;  // list item flags over the pair index
   static_assert(PB <= 0x4000, "pair index must fit below the flags");
-  __shared__ uint32_t s_skip[LDS_SKIP ? SKIP_LDS_MAX : 1];
   __shared__ int32_t s_used[PB];               // per pair: used millicores after B
   __shared__ int s_t[PB], s_ep[PB], s_rem[PB];  // per env of the workgroup: step, episode, pods rejected
   __shared__ uint16_t s_list[PB];              // work list: pair index | ARR | DEP
@@ -741,11 +616,9 @@ __global__ void __launch_bounds__(64 * W) WL_WPE k_node_step_wl(EnvView v, const
     }
   }
   if (tid == 0) s_n = s_reset = 0;
-  if (LDS_SKIP)
-    for (int i = tid; i < v.n_skip; i += NT) s_skip[i] = v.skip[i];
   __syncthreads();
-  WL_STAMP(1)
-  const uint32_t* S = LDS_SKIP ? s_skip : v.skip;
+  // (the survival table stays in global memory, L2-resident: u_below_S reads it for ~2^-15 of the draws)
+  const uint32_t* S = v.skip;
   // ---- A: the list
   bool any_reset = false;
 #pragma unroll
@@ -776,7 +649,6 @@ __global__ void __launch_bounds__(64 * W) WL_WPE k_node_step_wl(EnvView v, const
   }
   if (any_reset) s_reset = 1;
   lds_barrier();
-  WL_STAMP(2)
   // ---- B: item i of the list goes to wave i % W, so the items spread over the workgroup's waves
   NodeCounters k;
   const int n = s_n;
@@ -786,7 +658,6 @@ __global__ void __launch_bounds__(64 * W) WL_WPE k_node_step_wl(EnvView v, const
     int2* col = node_col(v, li) + (size_t)ci * N;
     uint16_t* tot = chunk_tot(v, li, ci);
     int32_t used = s_used[p];
-#ifndef WL_XP_NOPF
     if (N <= 256) {
       TotPf pf(tot, N);  // (kept equal to memory through the departures)
       if (it & DEP) depart_cluster(v, S, gid, s_ep[ei], s_t[ei], ci, col, tot, used, k, pf);
@@ -795,9 +666,7 @@ __global__ void __launch_bounds__(64 * W) WL_WPE k_node_step_wl(EnvView v, const
         first_fit_cluster(v, ci, col, tot, rem, used, k, pf);
         s_rem[ei] = rem;
       }
-    } else
-#endif
-    {
+    } else {
       TotLoad tl{tot};
       if (it & DEP) depart_cluster(v, S, gid, s_ep[ei], s_t[ei], ci, col, tot, used, k, tl);
       if (it & ARR) {
@@ -810,7 +679,6 @@ __global__ void __launch_bounds__(64 * W) WL_WPE k_node_step_wl(EnvView v, const
   }
   if (s_reset) __syncthreads();  // (uniform: written before the last barrier)
   else lds_barrier();
-  WL_STAMP(3)
   // ---- D: step (:115-144): row t1 = t + 1, done, auto-reset, obs
   int n_over = 0;
 #pragma unroll
@@ -863,7 +731,6 @@ __global__ void __launch_bounds__(64 * W) WL_WPE k_node_step_wl(EnvView v, const
       if (trunc) trunc[lane] = 0;
     }
   }
-  WL_STAMP(4)
   node_counters_flush(v, k);
   if (status) {
     const int m = (int)wave_sum_u64((unsigned long long)n_over);
@@ -1114,11 +981,6 @@ std::vector<uint32_t> skip32(int pmax, double p) {
 }
 }  // namespace
 
-#ifdef WL_XP_CLOCK
-extern "C" __attribute__((visibility("default"))) int rlks_xp_wl_clock(void* dst, size_t bytes) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(rlks::g_wl_clock), bytes, 0, hipMemcpyDeviceToHost);
-}
-#endif
 extern "C" {
 
 int rlks_env_create(const rlks_env_cfg* cfg, const double* cost, const double* lat, rlks_env** out) {
@@ -1305,31 +1167,12 @@ int rlks_env_step(rlks_env* e, const int32_t* actions, float* obs, double* rew64
   }
   if (e->cfg.nodes_per_cluster > 0) {
     const int C = e->cfg.n_clouds;
-    if (C <= RLKS_NODE_EC_MAX_C) {  // one lane per (env, cluster): 2^cs >= C lanes per env, 256 / 2^cs envs a block
+    if (C <= NODE_WL_MAX_C) {  // (env, cluster) pairs: 2^cs >= C lanes per env
       int cs = 0;
       while ((1 << cs) < C) ++cs;
-      const dim3 grid(cdiv(e->cfg.n_envs, 256 >> cs)), blk(256);
-#ifdef NODE_XP_EC
-      if (e->n_skip <= NODE_EC_LDS_SKIP_MAX)
-        hipLaunchKernelGGL(k_node_step_ec<true>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64,
-                           rew32, term, trunc, step_out, final_obs, status, cs);
-      else
-        hipLaunchKernelGGL(k_node_step_ec<false>, grid, blk, 0, s, view(e), e->d_cost, e->d_lat, actions, obs, rew64,
-                           rew32, term, trunc, step_out, final_obs, status, cs);
-#else
       const dim3 gridw(cdiv(e->cfg.n_envs, (NODE_WL_NP * 64 * NODE_WL_W) >> cs)), blkw(64 * NODE_WL_W);
-      // (the survival table stays in global memory: u_below_S reads it for ~2^-15 of the draws)
-#ifdef WL_XP_LDSSKIP
-      if (e->n_skip <= NODE_EC_LDS_SKIP_MAX)
-#else
-      if (false)
-#endif
-        hipLaunchKernelGGL((k_node_step_wl<true, NODE_WL_NP, NODE_WL_W>), gridw, blkw, 0, s, view(e), e->d_cost, e->d_lat, actions,
-                           obs, rew64, rew32, term, trunc, step_out, final_obs, status, cs);
-      else
-        hipLaunchKernelGGL((k_node_step_wl<false, NODE_WL_NP, NODE_WL_W>), gridw, blkw, 0, s, view(e), e->d_cost, e->d_lat, actions,
-                           obs, rew64, rew32, term, trunc, step_out, final_obs, status, cs);
-#endif
+      hipLaunchKernelGGL((k_node_step_wl<NODE_WL_NP, NODE_WL_W>), gridw, blkw, 0, s, view(e), e->d_cost, e->d_lat, actions,
+                         obs, rew64, rew32, term, trunc, step_out, final_obs, status, cs);
       RLKS_LAUNCHED();
       return RLKS_OK;
     }

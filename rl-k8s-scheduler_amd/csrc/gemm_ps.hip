@@ -178,7 +178,10 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         if (!nok || m >= g.M) continue;
         float v = acc[i][j][q] * unscale;
         if (EPI == PS_TANH_BIAS || EPI == PS_TANH_BIAS_PLANES)
-          v = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f((v + bias) * 2.885390081777927f) + 1.f), 1.f);
+#ifndef SF_TANH_XP
+#define SF_TANH_XP 0
+#endif
+          v = (SF_TANH_XP & 4) ? tanh_u((v + bias) * 2.885390081777927f) : fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f((v + bias) * 2.885390081777927f) + 1.f), 1.f);
         if (EPI == PS_TANH_BIAS_PLANES) {  // H1 for the pre-split GEMMs: fp16 planes at 2^14
           const float hs = v * 16384.f;
           const _Float16 hh = (_Float16)hs;

@@ -42,7 +42,11 @@ __device__ __forceinline__ int sf_exp(float mx) {
   (void)frexpf(mx, &e);
   return min(max(15 - e, -120), 120);
 }
+#ifndef SF_TANH_XP
+#define SF_TANH_XP 0
+#endif
 __device__ __forceinline__ float tanh_abs(float x) {
+  if (SF_TANH_XP & 4) return tanh_u(x * 2.885390081777927f);
   const float e = __builtin_amdgcn_exp2f(x * 2.885390081777927f);
   return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }

@@ -46,6 +46,32 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return ax < 0.6f ? small : __builtin_copysignf(big, x);
 }
 
+// tanh(x) from u = 2 log2(e) x, the exp2 argument the split-fp16 kernels already form (their scale
+// multiplies fold the constant in): fast_tanh's odd polynomial rewritten in u for |x| < 0.6, else
+// 1 - 2 / (exp2(u) + 1).  Relative error ~2e-7 everywhere, where the exp form alone has ~1e-7
+// *absolute* error (relative error unbounded as x -> 0: the small activations of a layer lost
+// precision, ~7x fp32's at the median of the logits, and the bias gradients summed that error
+// coherently over the rows).  rr: 1 / (exp2(u) + 1), for callers that reuse it.
+constexpr float TANH_U_SMALL = 1.7312340490667564f;  // |x| < 0.6
+__device__ __forceinline__ float tanh_u_poly(float u) {
+  const float v = u * u;
+  float q = -5.289088156800406e-08f;
+  q = fmaf(q, v, 1.5128073202201884e-06f);
+  q = fmaf(q, v, -3.233166373140893e-05f);
+  q = fmaf(q, v, 0.0006666361436294841f);
+  q = fmaf(q, v, -0.013876021376675698f);
+  q = fmaf(q, v, 0.3465735902799726f);
+  return u * q;
+}
+__device__ __forceinline__ float tanh_u(float u, float& rr) {
+  rr = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(u) + 1.f);
+  return fabsf(u) < TANH_U_SMALL ? tanh_u_poly(u) : fmaf(-2.f, rr, 1.f);
+}
+__device__ __forceinline__ float tanh_u(float u) {
+  float rr;
+  return tanh_u(u, rr);
+}
+
 // reduce 16 per-lane values (register r <-> accumulator row) over the 32 lanes of a half-wave;
 // afterwards lane l holds the total of register ((l >> 1) & 15) (lanes l and l^1 agree).
 // Reduce-scatter without LDS: v_permlane16_swap pairs rows 0/1 (and 2/3) of the wave, then

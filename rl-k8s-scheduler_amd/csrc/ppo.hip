@@ -1237,7 +1237,10 @@ int rlks_rollout_ws(rlks_env* env, const rlks_mlp_desc* d, const float* params, 
     RLKS_REQUIRE(cfg.autoreset, RLKS_ERR_ARG, "rlks_rollout_ws: node-level rollout needs autoreset lanes");
     return node_rollout(env, d, params, b, explore, &w, s);
   }
-  if (N > SF_ROLL_FUSED_MAX_LANES && cfg.autoreset) {
+  // by the whole job's lane count: W ranks of N lanes and one rank of W N lanes (num_lane_groups = W)
+  // run the same forward kernel, so their logits, and hence their sampled actions, agree bit for bit
+  const int64_t job_lanes = b->global_lanes > 0 ? b->global_lanes : N;
+  if (job_lanes > SF_ROLL_FUSED_MAX_LANES && cfg.autoreset) {
     // per step: the 16-row forward of both nets (k_sf_fwd16), then the fused sample + env step
     // (k_sample_step, auto-reset lanes); V(obs[T]) by one more forward
     if (int rc = sf_prep(d, w, params, s, true)) return rc;

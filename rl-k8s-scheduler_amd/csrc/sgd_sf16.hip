@@ -108,6 +108,9 @@ __device__ __forceinline__ float tanh_abs(float x) {
 // multiply by): tanh x = 1 - 2 r, 1 - tanh^2 x = 4 r (1 - r).  4 VALU ops instead of 6 with the
 // separate scale multiply.
 __device__ __forceinline__ float tanh_r(float kx) { return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(kx) + 1.f); }
+#ifndef SF_TANH_XP
+#define SF_TANH_XP 0
+#endif
 
 // interleave the scheduling region: NM x (1 MFMA, NV VALU) (cdna_hip_programming.md T19); an
 // MFMA leaves 24 of its 32 issue cycles for independent vector work of the same wave
@@ -591,7 +594,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
         }
         float hv[8];  // 2^14 tanh = 2^14 - 2^15 r (the split's fixed H1 scale folded in)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hv[j] = fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
+        for (int j = 0; j < 8; ++j) hv[j] = (SF_TANH_XP & 1) ? SF_H1_SCALE * tanh_u(z[j >> 2][j & 3] * k_z1) : fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
         split8(hv, 0, 1.f, bh, bl);
       }
       // fragments one n-tile ahead of their MFMAs, fenced so that only two sets are live
@@ -628,7 +631,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
     float hv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      hv[i] = fmaf(-2.f, tanh_r(fmaf(acc[nt][i], k_z2, bv[i])), 1.f);
+      hv[i] = (SF_TANH_XP & 2) ? tanh_u(fmaf(acc[nt][i], k_z2, bv[i])) : fmaf(-2.f, tanh_r(fmaf(acc[nt][i], k_z2, bv[i])), 1.f);
       acc[nt][i] = hv[i];
     }
 #pragma unroll
@@ -1119,7 +1122,7 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         _Float16 a, b;
-        split1(fmaf(-2.f * hs, tanh_r(z[4 * i + j] * k_z1), hs), a, b);
+        split1((SF_TANH_XP & 1) ? hs * tanh_u(z[4 * i + j] * k_z1) : fmaf(-2.f * hs, tanh_r(z[4 * i + j] * k_z1), hs), a, b);
         hh[j] = a;
         hl[j] = b;
       }
@@ -1290,7 +1293,7 @@ __device__ __forceinline__ void fwd16_body(const SfFwdArgs& g) {
         }
         float hv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hv[j] = fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
+        for (int j = 0; j < 8; ++j) hv[j] = (SF_TANH_XP & 8) ? SF_H1_SCALE * tanh_u(z[j >> 2][j & 3] * k_z1) : fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
         split8(hv, 0, 1.f, bh, bl);
       }
       const _Float16* buf = sCh + ph * 2 * H16;
@@ -1321,7 +1324,7 @@ __device__ __forceinline__ void fwd16_body(const SfFwdArgs& g) {
     const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
     float hv[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) hv[i] = fmaf(-2.f, tanh_r(fmaf(acc[nt][i], k_z2, bv[i])), 1.f);
+    for (int i = 0; i < 4; ++i) hv[i] = (SF_TANH_XP & 8) ? tanh_u(fmaf(acc[nt][i], k_z2, bv[i])) : fmaf(-2.f, tanh_r(fmaf(acc[nt][i], k_z2, bv[i])), 1.f);
 #pragma unroll
     for (int a = 0; a < A_; ++a) {
       const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);

@@ -64,7 +64,7 @@ class PpoCoeffs(C.Structure):
 class RolloutBufs(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("logits", C.c_void_p), ("values", C.c_void_p), ("actions", C.c_void_p),
                 ("logp", C.c_void_p), ("rewards", C.c_void_p), ("dones", C.c_void_p), ("adv", C.c_void_p),
-                ("vtarg", C.c_void_p), ("T", C.c_int32), ("N", C.c_int32)]
+                ("vtarg", C.c_void_p), ("T", C.c_int32), ("N", C.c_int32), ("global_lanes", C.c_int32)]
 
 
 class GatherNext(C.Structure):

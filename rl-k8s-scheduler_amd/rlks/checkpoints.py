@@ -69,7 +69,9 @@ def run_experiment(config, *, name: str = "FINAL_PPO_AWS_AZURE", stop_iterations
     """train_final.py's Tune run on one trial: train() until `stop_iterations`, save every
     `checkpoint_frequency` iterations and at the end, keep the `num_to_keep` newest checkpoints.
     Layout: <storage>/<name>/PPO_<env>_00000/checkpoint_<iteration:06d>.  Returns the last result,
-    the trial directory and the kept checkpoints (oldest first)."""
+    the trial directory and the kept checkpoints (oldest first).  `reporter` is installed as the
+    algorithm's own (PPO.train() reports through it), unless the algorithm already has one
+    (PPOConfig.metrics_json_lines / RLKS_METRICS_JSONL): every iteration is reported once."""
     from .ppo import PPO
 
     root = Path(storage_path) if storage_path is not None else results_root()
@@ -77,6 +79,8 @@ def run_experiment(config, *, name: str = "FINAL_PPO_AWS_AZURE", stop_iterations
     trial = root / name / f"PPO_{env}_00000"
     trial.mkdir(parents=True, exist_ok=True)
     algo = algo if algo is not None else PPO(config=config, **ppo_kw)
+    if reporter is not None and getattr(algo, "reporter", None) is None:
+        algo.reporter = reporter
     kept: list[Path] = []
     result = None
 
@@ -91,8 +95,6 @@ def run_experiment(config, *, name: str = "FINAL_PPO_AWS_AZURE", stop_iterations
 
     while algo.iteration < stop_iterations:
         result = algo.train()
-        if reporter is not None:
-            reporter.report(result, algo)
         if checkpoint_frequency and algo.iteration % checkpoint_frequency == 0:
             save()
     if checkpoint_at_end and (not kept or checkpoint_number(kept[-1]) != algo.iteration):

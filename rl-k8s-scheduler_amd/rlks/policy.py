@@ -93,6 +93,24 @@ class PolicyParams:
         for i, (name, _, _) in enumerate(TENSOR_NAMES):
             self.view(i).copy_(sd[name].to(self.flat.device))
 
+    def split(self, buf):
+        """a buffer laid out like `flat` (the Adam moments, a gradient) -> {state_dict name: CPU
+        tensor}: checkpoints keep per-parameter state per tensor, so a change of the flat storage
+        order (mlp_common.h LAYOUT_ORDER) cannot move it onto the wrong tensor"""
+        out = {}
+        for i, (name, _, _) in enumerate(TENSOR_NAMES):
+            n = int(np.prod(self.shapes[i]))
+            out[name] = buf[self.offsets[i]: self.offsets[i] + n].view(self.shapes[i]).detach().cpu().clone()
+        return out
+
+    def join(self, buf, sd):
+        """inverse of split(): copy {name: tensor} into `buf` at this layout's offsets"""
+        for i, (name, _, _) in enumerate(TENSOR_NAMES):
+            if tuple(sd[name].shape) != tuple(self.shapes[i]):
+                raise ValueError(f"tensor {name} has shape {tuple(sd[name].shape)}, this policy {tuple(self.shapes[i])}")
+            n = int(np.prod(self.shapes[i]))
+            buf[self.offsets[i]: self.offsets[i] + n].copy_(sd[name].reshape(-1).to(buf.device))
+
     def forward(self, obs, logits=None, values=None):
         """logits [n, A], values [n] for obs [n, D] (device tensors)"""
         import torch

@@ -82,7 +82,8 @@ class PPOConfig:
         # node-level envs (C x nodes x 8 B per lane: ~1 GB at c3, written on every save())
         self.checkpoint_env_state = None
         # minibatches are drawn per block of lanes (rlks_ppo_gather_grouped): None = one block per
-        # rank.  A single-rank run with num_lane_groups = W trains exactly like W ranks.
+        # rank.  A single-rank run with num_lane_groups = W trains exactly like W ranks (the rollout
+        # picks its forward kernel from the job's lane count, rlks_rollout_bufs.global_lanes).
         self.num_lane_groups = None
         # more than one rank, split-fp16 step: all-reduce the W2 / W3 gradient bucket while the dW1
         # kernel runs (rlks_ppo_grad_step_part), instead of the whole gradient after it
@@ -304,7 +305,8 @@ class PPO:
             b = self.buf
             self.bufs = _lib.RolloutBufs(b["obs"].data_ptr(), b["logits"].data_ptr(), b["values"].data_ptr(),
                                          b["actions"].data_ptr(), b["logp"].data_ptr(), b["rewards"].data_ptr(),
-                                         b["dones"].data_ptr(), b["adv"].data_ptr(), b["vtarg"].data_ptr(), T, N)
+                                         b["dones"].data_ptr(), b["adv"].data_ptr(), b["vtarg"].data_ptr(), T, N,
+                                         N * self.world)
             self.stride = _lib.lib().rlks_minibatch_stride(C.byref(self.params.desc))
             self.mbuf = torch.zeros(self.mb, self.stride, **f32)
             # one aligned record per sample (rlks_ppo_pack after GAE): a minibatch row is then one
@@ -663,7 +665,8 @@ class PPO:
         _lib.call("rlks_env_lane_state", self.env.handle, _lib.ptr(steps), _lib.ptr(eps), self.stream)
         st = {
             "weights": self.params.state_dict(),
-            "adam_m": self.adam_m.cpu(), "adam_v": self.adam_v.cpu(),
+            "adam_m": self.params.split(self.adam_m), "adam_v": self.params.split(self.adam_v),
+            "param_offsets": list(self.params.offsets),
             "adam_step": self.adam_step, "kl_coeff": float(self.dyn[_lib.RLKS_DYN_KL_COEFF].item()),
             "iteration": self.iteration, "timesteps_total": self.timesteps_total,
             "episodes_total": self.episodes_total, "lane_steps": steps.cpu(), "lane_episodes": eps.cpu(),
@@ -706,7 +709,9 @@ class PPO:
         st = self.get_state()
         sfx = f".rank{self.rank}" if self.world > 1 else ""
         tensors = {f"weights/{k}": v for k, v in st.pop("weights").items()}
-        tensors.update({k: st.pop(k) for k in ("adam_m", "adam_v", "lane_steps", "lane_episodes")})
+        for k in ("adam_m", "adam_v"):  # per tensor, like the weights
+            tensors.update({f"{k}/{name}": v for name, v in st.pop(k).items()})
+        tensors.update({k: st.pop(k) for k in ("lane_steps", "lane_episodes")})
         if "current_obs" in st:
             tensors["current_obs"] = st.pop("current_obs")
         env_state = st.pop("env_state", None)
@@ -741,8 +746,17 @@ class PPO:
                 raise ValueError(f"checkpoint tensor {k} has shape {tuple(sd[k].shape)}, this policy {tuple(v.shape)}")
         self.params.load_state_dict(sd)
         self._fused_prev = False
-        self.adam_m.copy_(tensors["adam_m"].to(self.device))
-        self.adam_v.copy_(tensors["adam_v"].to(self.device))
+        for k, buf in (("adam_m", self.adam_m), ("adam_v", self.adam_v)):
+            per = {n[len(k) + 1:]: v for n, v in tensors.items() if n.startswith(k + "/")}
+            if per:
+                self.params.join(buf, per)
+            elif meta.get("param_offsets") == list(self.params.offsets):
+                buf.copy_(tensors[k].to(self.device))  # a flat buffer saved with this very layout
+            else:
+                # an older checkpoint: raw flat moments with no record of the storage order they were
+                # written in; copying them could land one tensor's moments on another silently
+                raise ValueError(f"checkpoint {path}: Adam moments saved as a flat buffer without their parameter "
+                                 "layout; cannot restore them safely")
         self.adam_step = int(meta["adam_step"])
         self.dyn[_lib.RLKS_DYN_KL_COEFF] = float(meta["kl_coeff"])
         self.iteration = int(meta["iteration"])

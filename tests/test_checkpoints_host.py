@@ -52,3 +52,39 @@ def test_json_lines_reporter(tmp_path):
     quiet = JsonLinesReporter(tmp_path / "rank1.jsonl", rank=1)
     quiet.report(res, algo)
     assert not (tmp_path / "rank1.jsonl").exists()
+
+
+def test_per_tensor_state_survives_a_layout_change():
+    """Adam moments are checkpointed per tensor (PolicyParams.split / join): state saved
+    under one flat storage order lands on the same named tensors under another"""
+    import torch
+
+    from rlks.policy import TENSOR_NAMES, PolicyParams
+
+    p = PolicyParams(6, 256, 2, device=torch.device("cpu"))
+    m = torch.arange(p.padded, dtype=torch.float32)
+    sd = p.split(m)
+    assert list(sd) == [n for n, _, _ in TENSOR_NAMES]
+    for i, (name, _, _) in enumerate(TENSOR_NAMES):
+        assert sd[name].shape == torch.Size(p.shapes[i])
+        assert float(sd[name].reshape(-1)[0]) == float(p.offsets[i])
+    # another storage order: the tensors in reverse, packed back to back
+    q = PolicyParams(6, 256, 2, device=torch.device("cpu"))
+    o, offs = 0, [0] * 12
+    for i in reversed(range(12)):
+        offs[i] = o
+        o += int(torch.tensor(q.shapes[i]).prod())
+    q.offsets = offs
+    buf = torch.zeros(o)
+    q.join(buf, sd)
+    back = q.split(buf)
+    for name in sd:
+        assert torch.equal(back[name], sd[name])
+    bad = dict(sd)
+    bad[TENSOR_NAMES[0][0]] = torch.zeros(3)
+    try:
+        q.join(buf, bad)
+    except ValueError:
+        pass
+    else:
+        raise AssertionError("a shape mismatch must refuse")
