@@ -251,6 +251,14 @@ int rlks_ppo_gather_packed(const rlks_mlp_desc* desc, const float* packed_dev, i
  * flat parameters -> grad_dev (padded_count floats).  stats_dev (double[RLKS_STAT_SIZE]) gets
  * the sums for reporting and the KL update.  workspace from rlks_ppo_workspace_bytes. */
 int rlks_ppo_workspace_bytes(const rlks_mlp_desc* desc, int rows, int64_t* bytes);
+/* Diagnostics (tools/f1b_isolate.py): the split-fp16 step's dZ2 hand-off inside `workspace` for `rows`
+ * minibatch rows: out[net] = dZ2 planes ([rows / 16 tiles][8][hi, lo][64][8] fp16, sgd_sf16.hip F1a),
+ * out[2 + net] = the tiles' int32 split exponents. */
+int rlks_debug_sf_handoff(const rlks_mlp_desc* desc, int rows, void* workspace_dev, void** out);
+/* Diagnostics (tools/wide_b2_isolate.py): the generic-width step's per-net forward and loss buffers
+ * inside `workspace` after rlks_ppo_grad: out[3 net] = H2 [rows][hidden], out[3 net + 1] = head
+ * outputs [rows][A or 1], out[3 net + 2] = dL/d outputs [rows][A or 1] (float32). */
+int rlks_debug_wide_bufs(const rlks_mlp_desc* desc, int rows, void* workspace_dev, void** out);
 int rlks_ppo_grad(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
                   const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev,
                   double* stats_dev, void* workspace_dev, int64_t workspace_bytes, void* stream);

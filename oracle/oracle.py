@@ -354,6 +354,65 @@ def ppo_loss_grad(flat, off, D, H, A, mb, *, clip_param=0.3, vf_clip_param=10.0,
     return f.grad.numpy(), stats
 
 
+# ----------------------------------------------------------------------------- fp32 error band
+# A float32 evaluation's error at one element is one draw of its rounding: at an element where a sum
+# cancels, a single evaluation can be exact by luck.  The tests compare against the largest error of a
+# few EQUALLY VALID fp32 evaluations of the same function: the hidden units of each layer relabelled
+# (the same network; every dot product summed in another order) and the minibatch rows reversed (the
+# loss is a mean over rows), each result mapped back to the original labels.  Evaluation 0 is the plain
+# one.  Test infrastructure (tests/parity.py).
+def _hidden_perms(H, n):
+    rng = np.random.default_rng(20251)
+    return [(np.arange(H), np.arange(H))] + [(rng.permutation(H), rng.permutation(H)) for _ in range(n - 1)]
+
+
+def _relabel(flat, off, D, H, A, p1, p2, inverse=False):
+    """flat parameters (or a gradient of them) with hidden units p1 (layer 1) / p2 (layer 2) of both
+    nets relabelled: new unit i = old unit p[i]; inverse=True maps back"""
+    out = np.array(flat, copy=True)
+    for net in (0, 1):
+        An = A if net == 0 else 1
+        shapes = [(H, D), (H,), (H, H), (H,), (An, H), (An,)]
+        t = [np.asarray(flat[off[6 * net + j]: off[6 * net + j] + int(np.prod(shp))]).reshape(shp)
+             for j, shp in enumerate(shapes)]
+        if not inverse:
+            new = [t[0][p1], t[1][p1], t[2][np.ix_(p2, p1)], t[3][p2], t[4][:, p2], t[5]]
+        else:
+            new = [np.empty_like(x) for x in t]
+            new[0][p1] = t[0]
+            new[1][p1] = t[1]
+            new[2][np.ix_(p2, p1)] = t[2]
+            new[3][p2] = t[3]
+            new[4][:, p2] = t[4]
+            new[5] = t[5]
+        for j, x in enumerate(new):
+            out[off[6 * net + j]: off[6 * net + j] + x.size] = x.ravel()
+    return out
+
+
+def ppo_loss_grad_fp32_band(flat, off, D, H, A, mb, n=3, **kw):
+    """n float32 gradients of the same loss (see above): [plain, relabelled, relabelled + rows reversed]"""
+    out = []
+    for i, (p1, p2) in enumerate(_hidden_perms(H, n)):
+        f = _relabel(np.asarray(flat, np.float64), off, D, H, A, p1, p2)
+        rows = np.asarray(mb)[::-1] if i == 2 else mb
+        g, _ = ppo_loss_grad(f.astype(np.float32), off, D, H, A, np.ascontiguousarray(rows), dtype=np.float32, **kw)
+        out.append(_relabel(np.asarray(g, np.float64), off, D, H, A, p1, p2, inverse=True))
+    return out
+
+
+def mlp_forward_fp32_band(flat, off, D, H, A, obs, n=3):
+    """n float32 forwards of the same network, hidden units relabelled (see above):
+    ([logits, ...], [values, ...])"""
+    ls, vs = [], []
+    for p1, p2 in _hidden_perms(H, n):
+        f = _relabel(np.asarray(flat, np.float64), off, D, H, A, p1, p2).astype(np.float32)
+        lg, v = mlp_forward(f, off, D, H, A, obs, dtype=np.float32)
+        ls.append(lg)
+        vs.append(v)
+    return ls, vs
+
+
 def adam(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8):
     """torch.optim.Adam single-tensor step (float32 semantics), returns new (p, m, v)"""
     import torch

@@ -23,6 +23,7 @@ namespace rlks {
 
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
+using v4u = __attribute__((ext_vector_type(4))) unsigned;
 
 namespace {
 
@@ -108,7 +109,13 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   }
   const int n0 = bx * PT, m0 = by * PT;
   const int ea = op_exp(g.a), eb = op_exp(g.b);
-  const float unscale = ldexpf(1.f, -ea - eb);
+  // rounding-bias cancellation (sgd_sf16.hip tile_sign): workgroups alternate the sign of their A
+  // fragments by row block and split layer, and unscale negates the result back, so the slight negative
+  // lean of the MFMA accumulation does not add up coherently over the row blocks / splits that a
+  // gradient (or the next layer's bias gradient) sums
+  const bool neg = ((by + (int)blockIdx.z) & 1) != 0;
+  const unsigned nmask = neg ? 0x80008000u : 0u;
+  const float unscale = (neg ? -1.f : 1.f) * ldexpf(1.f, -ea - eb);
   // this workgroup's K range (split-K: layer z)
   const int kper = g.splits > 1 ? ((g.K + g.splits - 1) / g.splits + PK - 1) / PK * PK : g.K;
   const int kb = blockIdx.z * kper, ke = min(g.K, kb + kper);
@@ -141,7 +148,11 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     for (int s = 0; s < 2; ++s) {
       h8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) frag<AK>(b, wm * 64 + 32 * i, s, l, ah[i], al[i]);
+      for (int i = 0; i < 2; ++i) {
+        frag<AK>(b, wm * 64 + 32 * i, s, l, ah[i], al[i]);
+        ah[i] = __builtin_bit_cast(h8, __builtin_bit_cast(v4u, ah[i]) ^ nmask);
+        al[i] = __builtin_bit_cast(h8, __builtin_bit_cast(v4u, al[i]) ^ nmask);
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j) frag<BK>(b + 2 * PCH, wn * 64 + 32 * j, s, l, bh[j], bl[j]);
 #pragma unroll
@@ -178,10 +189,7 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         if (!nok || m >= g.M) continue;
         float v = acc[i][j][q] * unscale;
         if (EPI == PS_TANH_BIAS || EPI == PS_TANH_BIAS_PLANES)
-#ifndef SF_TANH_XP
-#define SF_TANH_XP 0
-#endif
-          v = (SF_TANH_XP & 4) ? tanh_u((v + bias) * 2.885390081777927f) : fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f((v + bias) * 2.885390081777927f) + 1.f), 1.f);
+          v = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f((v + bias) * 2.885390081777927f) + 1.f), 1.f);
         if (EPI == PS_TANH_BIAS_PLANES) {  // H1 for the pre-split GEMMs: fp16 planes at 2^14
           const float hs = v * 16384.f;
           const _Float16 hh = (_Float16)hs;

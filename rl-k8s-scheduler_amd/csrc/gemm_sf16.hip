@@ -42,11 +42,7 @@ __device__ __forceinline__ int sf_exp(float mx) {
   (void)frexpf(mx, &e);
   return min(max(15 - e, -120), 120);
 }
-#ifndef SF_TANH_XP
-#define SF_TANH_XP 0
-#endif
 __device__ __forceinline__ float tanh_abs(float x) {
-  if (SF_TANH_XP & 4) return tanh_u(x * 2.885390081777927f);
   const float e = __builtin_amdgcn_exp2f(x * 2.885390081777927f);
   return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }
@@ -161,7 +157,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int wm = w >> 1, wn = w & 1;
   const int n0 = blockIdx.x * GT, m0 = blockIdx.y * GT;
   const int ea = sf_exp(__uint_as_float(*g.amax)), eb = sf_exp(__uint_as_float(*g.bmax));
-  const float sa = ldexpf(1.f, ea), sb = ldexpf(1.f, eb), unscale = ldexpf(1.f, -ea - eb);
+  // rounding-bias cancellation (gemm_ps.hip, sgd_sf16.hip tile_sign): A enters negated in odd row
+  // blocks / split layers, and the result is negated back
+  const float sg = ((blockIdx.y + blockIdx.z) & 1) ? -1.f : 1.f;
+  const float sa = sg * ldexpf(1.f, ea), sb = ldexpf(1.f, eb), unscale = sg * ldexpf(1.f, -ea - eb);
 
   // register ring of two chunks per operand: while chunk c is multiplied, chunks c + 1 (parked in
   // LDS at the start of iteration c) and c + 2 / c + 3 are in flight, so a load has two MFMA
@@ -319,7 +318,8 @@ __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int
 }
 
 // column sums of a [rows][cols] matrix over the row range of layer blockIdx.y (rows_per rows):
-// out[y * cols + c] (or, with one layer, out[c] (+)=) = sum_r x[r][c]; one thread per column, f64
+// out[y * cols + c] (or, with one layer, out[c] (+)=) = sum_r x[r][c]; one thread per column, f64.
+// Several layers: each layer's f64 sum as hi (plane y) + lo (plane gridDim.y + y), both reduced
 __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ x, int rows, int cols, int ld, int rows_per,
                                                 float* __restrict__ out, int accumulate) {
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -336,7 +336,11 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ x, int
     for (int j = 0; j < 8; ++j) s += (double)v[j];
   }
   for (; rr < r1; ++rr) s += (double)x[(size_t)rr * ld + c];
-  if (gridDim.y > 1) out[(size_t)blockIdx.y * cols + c] = (float)s;
+  if (gridDim.y > 1) {
+    const float hi = (float)s;
+    out[(size_t)blockIdx.y * cols + c] = hi;
+    out[(size_t)(gridDim.y + blockIdx.y) * cols + c] = (float)(s - (double)hi);
+  }
   else out[c] = accumulate ? out[c] + (float)s : (float)s;
 }
 
@@ -433,7 +437,7 @@ int launch_colsum(const float* x, int rows, int cols, int ld, float* out, int ac
                      sp > 1 ? part : out, accumulate);
   RLKS_LAUNCHED();
   if (sp == 1) return RLKS_OK;
-  return launch_split_reduce(part, sp, 1, cols, out, cols, accumulate, s);
+  return launch_split_reduce(part, 2 * sp, 1, cols, out, cols, accumulate, s);
 }
 
 }  // namespace rlks

@@ -46,32 +46,6 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return ax < 0.6f ? small : __builtin_copysignf(big, x);
 }
 
-// tanh(x) from u = 2 log2(e) x, the exp2 argument the split-fp16 kernels already form (their scale
-// multiplies fold the constant in): fast_tanh's odd polynomial rewritten in u for |x| < 0.6, else
-// 1 - 2 / (exp2(u) + 1).  Relative error ~2e-7 everywhere, where the exp form alone has ~1e-7
-// *absolute* error (relative error unbounded as x -> 0: the small activations of a layer lost
-// precision, ~7x fp32's at the median of the logits, and the bias gradients summed that error
-// coherently over the rows).  rr: 1 / (exp2(u) + 1), for callers that reuse it.
-constexpr float TANH_U_SMALL = 1.7312340490667564f;  // |x| < 0.6
-__device__ __forceinline__ float tanh_u_poly(float u) {
-  const float v = u * u;
-  float q = -5.289088156800406e-08f;
-  q = fmaf(q, v, 1.5128073202201884e-06f);
-  q = fmaf(q, v, -3.233166373140893e-05f);
-  q = fmaf(q, v, 0.0006666361436294841f);
-  q = fmaf(q, v, -0.013876021376675698f);
-  q = fmaf(q, v, 0.3465735902799726f);
-  return u * q;
-}
-__device__ __forceinline__ float tanh_u(float u, float& rr) {
-  rr = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(u) + 1.f);
-  return fabsf(u) < TANH_U_SMALL ? tanh_u_poly(u) : fmaf(-2.f, rr, 1.f);
-}
-__device__ __forceinline__ float tanh_u(float u) {
-  float rr;
-  return tanh_u(u, rr);
-}
-
 // reduce 16 per-lane values (register r <-> accumulator row) over the 32 lanes of a half-wave;
 // afterwards lane l holds the total of register ((l >> 1) & 15) (lanes l and l^1 agree).
 // Reduce-scatter without LDS: v_permlane16_swap pairs rows 0/1 (and 2/3) of the wave, then
@@ -118,6 +92,49 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 __device__ __forceinline__ float wave_sum_f(float v) {
   return wave_reduce(v, [](float a, float b) { return a + b; });
+}
+// row_sum16 over doubles (each 32-bit half moved by the same DPP step)
+template <int CTRL>
+__device__ __forceinline__ double dppd(double x) {
+  const unsigned long long u = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double row_sum16d(double v) {  // over the 16 lanes of a row
+  v += dppd<0x128>(v);
+  v += dppd<0x141>(v);
+  v += dppd<0x4E>(v);
+  return v + dppd<0xB1>(v);
+}
+
+// RLlib's value loss of one row, clamp((v - vt)^2, 0, vf_clip) (as oracle.py:ppo_loss_grad restates it):
+// dl = dL/dv already over the row count, the clamped square (the vf_loss stat), and ex = v - vt
+// exactly (the fp32 difference plus its rounding error, Knuth's TwoSum) where the row is inside the
+// clamp, else 0.  The value head's bias gradient is 2 vf_coeff / count times the sum of ex over the
+// rows: a single sum over the minibatch whose rows cancel to ~1/sqrt(rows) of their magnitudes, so the
+// fp32 rounding of each row's difference (half an ulp of |v - vt|, the same size as the terms' error
+// that a float32 evaluation makes) would dominate its relative error; summed exactly in f64 it is
+// left with the forward's own error of v (profiles/r05_precision).
+struct VfRow {
+  float dl, sq;
+  double ex;
+};
+__device__ __forceinline__ VfRow vf_row(float v, float vt, float vf_clip, float vf_coeff, float inv_count) {
+  const float diff = v - vt;
+  const float bv = diff - v;
+  const float err = (v - (diff - bv)) + (-vt - bv);
+  const float sq = diff * diff;
+  const bool in = sq <= vf_clip;
+  return {in ? vf_coeff * 2.f * diff * inv_count : 0.f, fminf(sq, vf_clip), in ? (double)diff + (double)err : 0.0};
+}
+// the bias gradient's per-block partial from a block's f64 sum of ex, as an exact hi + lo pair of
+// floats (both summed by the f64 reduce)
+__device__ __forceinline__ void vf_b3_part(double sum_ex, float vf_coeff, float inv_count, float* part2) {
+  const double t = sum_ex * (2.0 * (double)vf_coeff * (double)inv_count);
+  const float hi = (float)t;
+  part2[0] = hi;
+  part2[1] = (float)(t - (double)hi);
 }
 
 // ----------------------------------------------------------------------------- layout

@@ -43,6 +43,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
   float* sX = sb1 + H;                   // [BMr][D+1]
   float* sW1 = sX + BMr * ds;            // [H][D+1]
   double* sTab = reinterpret_cast<double*>(sW1 + ((H * ds + 1) & ~1));  // rollout: [2][T][C] tables
+  __shared__ double sVx[2];             // value net: waves 0, 1's f64 sums of v - vt (vf_row)
 
   const NetPtrs& P = g.P;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -162,6 +163,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
 
   // ---- per-row output, loss and dout (one thread per row)
   float st_pl = 0.f, st_vf = 0.f, st_kl = 0.f, st_ent = 0.f;
+  double vex = 0.0;  // value net: the row's exact v - vt (vf_row)
   if (tid < BMr) {
     const int m = row0 + tid;
     float out[A_];
@@ -267,10 +269,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
           st_kl = kl;
           st_ent = ent;
         } else {
-          const float diff = out[0] - rec[D + Ap + 1];
-          const float sq = diff * diff;
-          st_vf = fminf(sq, g.co.vf_clip_param);
-          dl[0] = (sq <= g.co.vf_clip_param) ? g.co.vf_loss_coeff * 2.f * diff * inv_count : 0.f;
+          const VfRow v = vf_row(out[0], rec[D + Ap + 1], g.co.vf_clip_param, g.co.vf_loss_coeff, inv_count);
+          st_vf = v.sq;
+          dl[0] = v.dl;
+          vex = v.ex;
         }
       }
 #pragma unroll
@@ -336,6 +338,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
       const float s = wave_sum(v[c]);
       if (l == 0) sStat[w * (A_ + 4) + c] = s;
     }
+    if (NET == 1) {
+      const double sx = wave_sum(vex);
+      if (l == 0) sVx[w] = sx;
+    }
   }
   __syncthreads();
   const int tile = blockIdx.x;
@@ -354,8 +360,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_fwd_head(FwdArgs g) {
   }
   if (tid < A_ + 4) {
     const float s = sStat[tid] + sStat[A_ + 4 + tid];
-    if (tid < A_) g.part_b3[(size_t)tile * A_ + tid] = s;
-    else g.part_stat[(size_t)tile * 4 + tid - A_] = s;
+    if (tid >= A_) g.part_stat[(size_t)tile * 4 + tid - A_] = s;
+    else if (NET == 0) g.part_b3[(size_t)tile * A_ + tid] = s;
+    else vf_b3_part(sVx[0] + sVx[1], g.co.vf_loss_coeff, g.dyn[RLKS_DYN_INV_COUNT], g.part_b3 + (size_t)tile * 2);
   }
 }
 

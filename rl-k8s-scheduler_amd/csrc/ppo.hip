@@ -461,7 +461,7 @@ static Ws ws_layout(int D, int A, int M, char* base) {
     n.dz2 = (float*)take(4LL * M * HID);
     n.part_b2 = (float*)take(4LL * w.tiles * HID);
     n.part_w3 = (float*)take(4LL * w.tiles * An * HID);
-    n.part_b3 = (float*)take(4LL * w.tiles * An);
+    n.part_b3 = (float*)take(4LL * w.tiles * (net == 0 ? A : 2));  // value net: [tile][hi, lo] (vf_row)
     n.part_stat = (float*)take(4LL * w.tiles * 4);
     n.part_w2 = (float*)take(4LL * w.splits * HID * HID);
     n.part_w1 = (float*)take(4LL * w.tiles * HID * D);
@@ -514,9 +514,8 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     W.pmax = (float*)take(4LL * 4 * SF_PMAX);
     W.tag = (unsigned*)take(4 * 2);
     w.pmax_roll[net] = (float*)take(4LL * 4 * SF_PMAX);
-    W.dzmax = (unsigned*)take(4 * SF_DZ_SLOTS * SF_DZ_STRIDE);
     n.w1h = W.w1h; n.w1l = W.w1l; n.w2ph = W.w2ph; n.w2pl = W.w2pl; n.w2th = W.w2th; n.w2tl = W.w2tl;
-    n.sc = W.sc; n.dzmax = W.dzmax;
+    n.sc = W.sc;
   }
   w.weight_bytes = o;
   for (int net = 0; net < 2; ++net) {
@@ -528,7 +527,7 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     n.part_w1 = (float*)take(4LL * w.blocks * HID * D);
     n.part_b1 = (float*)take(4LL * w.blocks * HID);
     n.part_w3 = (float*)take(4LL * w.fa_parts * An * HID);
-    n.part_b3 = (float*)take(4LL * w.fa_parts * An);
+    n.part_b3 = (float*)take(4LL * w.fa_parts * (net == 0 ? A : 2));  // value net: [part][hi, lo] (vf_row)
     n.part_stat = (float*)take(4LL * w.fa_parts * 4);
     n.part_w2 = (float*)take(4LL * w.splits * SF_W2_PSTRIDE);
     n.part_b2 = (float*)take(4LL * w.splits * HID);
@@ -792,6 +791,30 @@ int rlks_ppo_workspace_bytes(const rlks_mlp_desc* d, int rows, int64_t* bytes) {
   return RLKS_OK;
 }
 
+int rlks_debug_sf_handoff(const rlks_mlp_desc* d, int rows, void* ws, void** out) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(out && ws && rows > 0 && rows % 256 == 0 && d->precision == RLKS_PRECISION_SF16 && !is_wide(d),
+               RLKS_ERR_ARG, "rlks_debug_sf_handoff: split-fp16 descriptor, rows % 256 == 0");
+  const SfWs w = sf_ws_layout(d->obs_dim, d->n_actions, rows, (char*)ws);
+  for (int net = 0; net < 2; ++net) {
+    out[net] = w.n[net].dz2s;
+    out[2 + net] = w.n[net].tile_edz;
+  }
+  return RLKS_OK;
+}
+
+int rlks_debug_wide_bufs(const rlks_mlp_desc* d, int rows, void* ws, void** out) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(out && ws && rows > 0 && is_wide(d), RLKS_ERR_ARG, "rlks_debug_wide_bufs: wide descriptor");
+  const WideWs w = wide_ws_layout(d->obs_dim, d->hidden, d->n_actions, rows, (char*)ws);
+  for (int net = 0; net < 2; ++net) {
+    out[3 * net] = w.n[net].h2;
+    out[3 * net + 1] = w.n[net].out;
+    out[3 * net + 2] = w.n[net].dout;
+  }
+  return RLKS_OK;
+}
+
 // SGD step with Adam fused into the gradient reduction (single rank: no gradient all-reduce between
 // them).  step: the Adam step performed (1-based); prev_fused: the previous SGD step on these
 // parameters was fused, so its reduce left this step's weight maxima in the split's slots.
@@ -852,7 +875,8 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
       R.add(n.part_w2, grad + o[2], nullptr, SF_W2_PSTRIDE, w.splits, H * H, 2 * net);
       R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
       R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, w.fa_parts, An * H);
-      R.add(n.part_b3, grad + o[5], nullptr, An, w.fa_parts, An);
+      if (net == 0) R.add(n.part_b3, grad + o[5], nullptr, An, w.fa_parts, An);
+      else R.add(n.part_b3, grad + o[5], nullptr, 1, 2 * w.fa_parts, 1);  // every hi and lo, in f64
     }
   }
   if (stats && part != 2) {  // per-block columns [policy loss, vf loss, kl, entropy] -> RLKS_STAT_* directly
@@ -961,7 +985,8 @@ int rlks_ppo_grad_phases(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, cons
     R.add(n.part_w2, grad + o[2], nullptr, (int64_t)H * H, w.splits, H * H);
     R.add(n.part_b2, grad + o[3], nullptr, H, w.tiles, H);
     R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, w.tiles, An * H);
-    R.add(n.part_b3, grad + o[5], nullptr, An, w.tiles, An);
+    if (net == 0) R.add(n.part_b3, grad + o[5], nullptr, An, w.tiles, An);
+    else R.add(n.part_b3, grad + o[5], nullptr, 1, 2 * w.tiles, 1);  // every hi and lo, in f64
     if (stats) R.add(n.part_stat, nullptr, w.stat64 + 4 * net, 4, w.tiles, 4);
   }
   hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);

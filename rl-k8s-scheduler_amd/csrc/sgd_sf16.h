@@ -6,8 +6,7 @@
 namespace rlks {
 constexpr int SF_F1_W = 8;          // waves per F1 workgroup (two workgroups per CU); 16 rows each
 constexpr int SF_PMAX = 1024;       // weight-max entries per (parity, kind)
-constexpr int SF_DZ_SLOTS = 64, SF_DZ_STRIDE = 16;
-constexpr int SF_W2_PSTRIDE = 256 * 256;  // floats between F2's dW2 partials (padding them apart: no gain)  // max |dZ2| partial maxima (sgd_sf16.hip dz_slot)
+constexpr int SF_W2_PSTRIDE = 256 * 256;  // floats between F2's dW2 partials (padding them apart: no gain)
 }  // namespace rlks
 
 namespace rlks {
@@ -20,7 +19,6 @@ struct SfNetW {
   float* pmax;        // [2 parity][2 kind: W2, W1a][SF_PMAX] per-block max |w| (k_sf_wmax: entries
                       // 0..15 of each kind; the fused reduce: one entry per reduce block)
   unsigned* tag;      // [2 parity]: the Adam step whose fused reduce filled pmax[parity] (0: none)
-  unsigned* dzmax;    // zeroed here: SF_DZ_SLOTS partial maxima (F1 atomicMax)
 };
 // parity: which half of pmax holds this prep's maxima; the split zeroes the other half, which the
 // fused reduce + Adam of the coming SGD step fills (one entry per reduce block, no atomics) for the
@@ -37,7 +35,6 @@ struct SfNet {
   const float *b2, *w3, *b3;
   const _Float16 *w1h, *w1l, *w2ph, *w2pl, *w2th, *w2tl;
   const float* sc;
-  unsigned* dzmax;
   _Float16* dz2s;  // [M/16 tiles][8 n-steps][hi, lo][64 lanes][8]: dZ2 of each 16-row tile split at
                   // 2^tile_edz, in F1a's lane order (sgd_sf16.hip F1)
   int* tile_edz;  // [M/16]: each 16-row tile's dZ2 split exponent (F1a -> F1b, F2)

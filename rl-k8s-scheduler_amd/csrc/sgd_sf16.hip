@@ -42,12 +42,6 @@ using v4u = __attribute__((ext_vector_type(4))) unsigned;  // 16-byte staging re
 
 constexpr int SF_ROWS = 256;        // minibatch rows must be a multiple of this
 constexpr float SF_H1_SCALE = 16384.f;  // tanh outputs (|h| < 1) scaled by 2^14
-// max |dZ2| of an SGD step as SF_DZ_SLOTS partial maxima, one 64-byte line apart: F1a waves update
-// the slot of (tile mod SF_DZ_SLOTS), F2 takes the max over them.  One address for all 4,096 tile
-// atomics serialised at its L2 channel and cost F1a ~12 us of 93 (profiles/r02d/f1a_atomic_xp).
-__device__ __forceinline__ unsigned* dz_slot(unsigned* base, int tile) {
-  return base + (tile & (SF_DZ_SLOTS - 1)) * SF_DZ_STRIDE;
-}
 
 __device__ __forceinline__ int sf_perm(int s, int h, int j) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
 // P16: element p = 8g + j of a 16x16x32 k-fragment taken from two stacked accumulator tiles
@@ -108,9 +102,6 @@ __device__ __forceinline__ float tanh_abs(float x) {
 // multiply by): tanh x = 1 - 2 r, 1 - tanh^2 x = 4 r (1 - r).  4 VALU ops instead of 6 with the
 // separate scale multiply.
 __device__ __forceinline__ float tanh_r(float kx) { return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(kx) + 1.f); }
-#ifndef SF_TANH_XP
-#define SF_TANH_XP 0
-#endif
 
 // interleave the scheduling region: NM x (1 MFMA, NV VALU) (cdna_hip_programming.md T19); an
 // MFMA leaves 24 of its 32 issue cycles for independent vector work of the same wave
@@ -271,7 +262,6 @@ __global__ __launch_bounds__(256) void k_sf_split(SfPrepArgs g) {
   if (blockIdx.y == 0 && tid == 0) {
     N.sc[0] = s1; N.sc[1] = 1.f / s1; N.sc[4] = (float)e1;
     N.sc[2] = s2; N.sc[3] = 1.f / s2; N.sc[5] = (float)e2;
-    for (int i = 0; i < SF_DZ_SLOTS; ++i) N.dzmax[i * SF_DZ_STRIDE] = 0u;
   }
   // the other parity's entries: the coming fused reduce writes some of them.  The rollout's prep
   // (write_roll) has slots of its own and leaves the SGD steps' parity state (entries and tags) alone.
@@ -322,9 +312,10 @@ __device__ __forceinline__ LossDyn load_dyn(const SfArgs& g) {
 // entropy] terms
 template <int A_, int NET>
 __device__ __forceinline__ void sf_loss_t(const SfArgs& g, const LossDyn& dy, const float (&out)[A_],
-                                          const RecTail<A_>& r, float (&dl)[A_], float (&st)[4]) {
+                                          const RecTail<A_>& r, float (&dl)[A_], float (&st)[4], double& vex) {
   const float inv_count = dy.inv_count;
   st[0] = st[1] = st[2] = st[3] = 0.f;
+  vex = 0.0;
   if (NET == 0) {
     const float* lo = r.lo;
     const float adv = (r.adv - dy.adv_mean) * dy.adv_invstd;
@@ -369,18 +360,18 @@ __device__ __forceinline__ void sf_loss_t(const SfArgs& g, const LossDyn& dy, co
     st[2] = kl;
     st[3] = ent;
   } else {
-    const float diff = out[0] - r.vt;
-    const float sq = diff * diff;
-    st[1] = fminf(sq, g.co.vf_clip_param);
-    dl[0] = (sq <= g.co.vf_clip_param) ? g.co.vf_loss_coeff * 2.f * diff * inv_count : 0.f;
+    const VfRow v = vf_row(out[0], r.vt, g.co.vf_clip_param, g.co.vf_loss_coeff, inv_count);
+    st[1] = v.sq;
+    dl[0] = v.dl;
+    vex = v.ex;
   }
 }
 template <int A_, int NET>
 __device__ __forceinline__ void sf_loss(const SfArgs& g, const float (&out)[A_], int row, float (&dl)[A_],
-                                        float (&st)[4]) {
+                                        float (&st)[4], double& vex) {
   RecTail<A_> r;
   load_tail<A_, NET>(g, row, r);
-  sf_loss_t<A_, NET>(g, load_dyn(g), out, r, dl, st);
+  sf_loss_t<A_, NET>(g, load_dyn(g), out, r, dl, st, vex);
 }
 
 
@@ -514,17 +505,32 @@ __device__ __forceinline__ float row_sum16(float v) {
 }
 
 // Xa = [X | 1 | 0] fragment of a 16-row tile: lane (g, c) holds row row0 + c, columns 8g .. 8g + 7,
-// scaled by the wave's power of two (returned: its exponent) and split
-__device__ __forceinline__ int x_frag(const SfArgs& a, int row0, int c, int g, h8& xh, h8& xl) {
+// scaled by the wave's power of two (returned: its exponent) times sgn (the tile's sign, below) and split
+__device__ __forceinline__ int x_frag(const SfArgs& a, int row0, int c, int g, h8& xh, h8& xl, float sgn = 1.f) {
   float xv[8];
   xa_row8(a.x + (size_t)(row0 + c) * a.x_stride, 8 * g, a.D, a.x_stride, xv);
   float xm = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) xm = fmaxf(xm, fabsf(xv[j]));
   const int ex = sf_exp(wave_max(xm));
-  split8(xv, 0, pow2(ex), xh, xl);
+  split8(xv, 0, sgn * pow2(ex), xh, xl);
   return ex;
 }
+
+// Rounding-bias cancellation.  The f16 MFMAs' fp32 accumulation is not sign-symmetric: averaged over
+// many dot products its error leans negative (tools/micro/mfma_round.hip: mean signed error -1e-10 of
+// sum |a b| over K = 256, ~2 % of the typical error).  A bias gradient sums such errors over all the
+// rows of a minibatch coherently (65,536 of them at c4), where fp32's rounding errors average out:
+// db1 came out ~7x less accurate than an fp32 evaluation at the median (tools/f1b_isolate.py,
+// profiles/r05_precision).  So every 16-row tile runs its products on operands of sign sgn = -1 for
+// odd tiles (+1 even): the error of an odd tile's products leans the other way and undoing the sign
+// afterwards is exact (powers of two and signs fold into the scales that are applied anyway):
+//   F1a: Xa and H1 of the tile enter their MFMAs negated (k_z1, k_z2 undo it), and its dZ2 is handed
+//     to F1b / F2 negated;
+//   F1b: dH1 = dZ2 W2 and dW1a = Xa^T dZ1 then come out negated, undone by u1; Z1's recompute as F1a;
+//   F2: its row splits alternate the same way over whole workgroups (each split's partial of dW2 is
+//     one accumulator chain; odd splits run on negated H1 and negate the partial back).
+__device__ __forceinline__ float tile_sign(int tile) { return (tile & 1) ? -1.f : 1.f; }
 
 // LDS of F1a: the loop region (two half-chunk buffers + W1a) doubles as the epilogue's workgroup
 // slots (dW3 [W][A][HID], then [W][A + 4] db3 / stats); b2 and W3 follow it
@@ -543,9 +549,17 @@ constexpr int f1b_lds_bytes() {
   return 4 * H16 * 2 + 2 * HID * KD * 2;
 }
 
+// The policy head is evaluated relative to its last action: the PPO loss depends on the logits only
+// through their log-softmax, so every row's logit gradients sum to zero (sum_a dL/dz_a = 0) and
+//   z_a - z_{A-1} = (W3[a] - W3[A-1]) H2 + b3[a] - b3[A-1]        (a < A - 1; z_{A-1} - z_{A-1} = 0)
+//   dZ2 = sum_{a < A-1} dl_a (W3[a] - W3[A-1]) (1 - H2^2)
+//   dW3[A-1] = -sum_{a < A-1} dW3[a]
+// which is the same loss and gradient with A - 1 head rows instead of A (at 2 actions: half of the
+// head, of dZ2's products and of the dW3 reduce-scatter, the epilogue's largest part).  AH: head rows.
 template <int A_, int NET, int KD, int W>
 __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   constexpr int NTHR = 64 * W;
+  constexpr int AH = NET == 0 ? A_ - 1 : 1;
   const SfNet& N = g.n[NET];
   extern __shared__ __attribute__((aligned(16))) float lds[];
   _Float16* sCh = reinterpret_cast<_Float16*>(lds);  // [2 buf][2 hi/lo][128][32]
@@ -564,11 +578,24 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
 
   hc_dma<W>(N.w2ph, N.w2pl, 0, 0, sCh, w, l);
   for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i] * SF_2LOG2E;  // H2 = tanh(Z2 + b2): exp2 argument
-  for (int i = tid; i < A_ * HID; i += NTHR) sW3[i] = N.w3[i];
+  __shared__ float s_w3m[W];  // per wave: max |W3 row| entry it staged (the dZ2 scale bound below)
+  __shared__ double s_vx[W];  // value net: per wave, the f64 sum of its rows' v - vt (vf_row)
+  {
+    float m3 = 0.f;
+    for (int i = tid; i < AH * HID; i += NTHR) {
+      const float v = NET == 0 ? N.w3[i] - N.w3[(A_ - 1) * HID + (i & (HID - 1))] : N.w3[i];
+      sW3[i] = v;
+      m3 = fmaxf(m3, fabsf(v));
+    }
+    m3 = wave_max(m3);
+    if (l == 0) s_w3m[w] = m3;
+  }
   w1_stage<KD, NTHR>(N, sW1, tid);
   h8 xh, xl;
-  const int ex = x_frag(g, row0, c, gq, xh, xl);
-  const float k_z1 = N.sc[1] * pow2(-ex) * SF_2LOG2E;  // Z1 accumulator -> 2 log2(e) Z1
+  const float sgn = tile_sign(tile);
+  const int ex = x_frag(g, row0, c, gq, xh, xl, sgn);
+  const float k_z1 = sgn * N.sc[1] * pow2(-ex) * SF_2LOG2E;  // Z1 accumulator -> 2 log2(e) Z1
+  const float h1s = sgn * SF_H1_SCALE;                        // H1 enters Z2's products as sgn 2^14 H1
   vm_drain();
   __syncthreads();
   FA_STAMP(1);
@@ -594,7 +621,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
         }
         float hv[8];  // 2^14 tanh = 2^14 - 2^15 r (the split's fixed H1 scale folded in)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hv[j] = (SF_TANH_XP & 1) ? SF_H1_SCALE * tanh_u(z[j >> 2][j & 3] * k_z1) : fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
+        for (int j = 0; j < 8; ++j) hv[j] = fmaf(-2.f * h1s, tanh_r(z[j >> 2][j & 3] * k_z1), h1s);
         split8(hv, 0, 1.f, bh, bl);
       }
       // fragments one n-tile ahead of their MFMAs, fenced so that only two sets are live
@@ -619,8 +646,8 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
 
   // ---- H2^T = tanh(Z2^T + b2) (lane: rows n = 16 nt + 4g + i of column m = c); head
   // out[a] = b3 + sum_n W3[a][n] H2[n] (partial over the lane's 64 n, then over the four rows)
-  const float k_z2 = N.sc[3] / SF_H1_SCALE * SF_2LOG2E;
-  float out[A_];
+  const float k_z2 = sgn * N.sc[3] / SF_H1_SCALE * SF_2LOG2E;
+  float out[A_];  // NET 0: z_a - z_{A-1}; out[A-1] = 0
 #pragma unroll
   for (int a = 0; a < A_; ++a) out[a] = 0.f;
 #pragma unroll
@@ -631,11 +658,12 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
     float hv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      hv[i] = (SF_TANH_XP & 2) ? tanh_u(fmaf(acc[nt][i], k_z2, bv[i])) : fmaf(-2.f, tanh_r(fmaf(acc[nt][i], k_z2, bv[i])), 1.f);
-      acc[nt][i] = hv[i];
+      const float r = tanh_r(fmaf(acc[nt][i], k_z2, bv[i]));  // H2 = 1 - 2 r; r is kept for 1 - H2^2 = 4 r (1 - r)
+      hv[i] = fmaf(-2.f, r, 1.f);
+      acc[nt][i] = r;
     }
 #pragma unroll
-    for (int a = 0; a < A_; ++a) {
+    for (int a = 0; a < AH; ++a) {
       const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
       out[a] = fmaf(hv[0], t.x, out[a]);
       out[a] = fmaf(hv[1], t.y, out[a]);
@@ -645,26 +673,27 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
     if constexpr (A_ > 4) asm volatile("" ::: "memory");  // keep the W3 reads per n-tile (8 actions: spills)
   }
 #pragma unroll
-  for (int a = 0; a < A_; ++a) out[a] = sum_rows4(out[a]) + N.b3[a];
+  for (int a = 0; a < AH; ++a) out[a] = sum_rows4(out[a]) + (NET == 0 ? N.b3[a] - N.b3[A_ - 1] : N.b3[a]);
   // the dZ2 pass below re-reads W3 from LDS rather than keeping the head's 16 A float4 alive
   // through the dW3 reductions (the compiler would otherwise reuse them and spill)
   asm volatile("" ::: "memory");
   FA_STAMP(4);
   float dl[A_];
   float st[4];
-  sf_loss<A_, NET>(g, out, row0 + c, dl, st);
+  double vex;
+  sf_loss<A_, NET>(g, out, row0 + c, dl, st, vex);
 
   // ---- dW3[a][n] over the tile's rows: reduce-scatter over the 16 lanes of a row (lane c ends
   // with n = 64G + 16 (c >> 2) + 4g + (c & 3) of group G), one slot per wave
-  constexpr int SLOT_B3 = W * A_ * HID;
+  constexpr int SLOT_B3 = W * AH * HID;
 #pragma unroll
-  for (int a = 0; a < A_; ++a)
+  for (int a = 0; a < AH; ++a)
 #pragma unroll
     for (int G = 0; G < 4; ++G) {
       float v[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) v[k] = dl[a] * acc[4 * G + (k >> 2)][k & 3];
-      sSlot[(w * A_ + a) * HID + 64 * G + 16 * (c >> 2) + 4 * gq + (c & 3)] = row_reduce16(v, l);
+      for (int k = 0; k < 16; ++k) v[k] = fmaf(-2.f * dl[a], acc[4 * G + (k >> 2)][k & 3], dl[a]);  // dl H2
+      sSlot[(w * AH + a) * HID + 64 * G + 16 * (c >> 2) + 4 * gq + (c & 3)] = row_reduce16(v, l);
     }
   {  // db3 and the loss stats: row sums (the four rows of the wave hold the same 16 rows m)
     float sv[A_ + 4];
@@ -677,20 +706,39 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
     if (l == 0)
 #pragma unroll
       for (int i = 0; i < A_ + 4; ++i) sSlot[SLOT_B3 + w * (A_ + 4) + i] = sv[i];
+    if constexpr (NET == 1) {  // the value head's bias: exact row differences summed in f64 (vf_row)
+      const double vx = row_sum16d(vex);
+      if (l == 0) s_vx[w] = vx;
+    }
   }
   FA_STAMP(5);
 
-  // ---- dZ2^T = (dl W3) (1 - H2^2), in place of H2 in the accumulators; the tile's max |dZ2| -> its
-  // split exponent; dZ2 -> HBM split at that scale: [tile][s = nt >> 1][hi, lo][lane][4 (nt & 1) + i],
-  // i.e. each lane's eight values of an n-step are the A fragment F1b's same lane reads (pre-split:
-  // neither F1b nor F2 splits it again)
-  float dmx = 0.f;
+  // ---- dZ2^T = (dl W3) (1 - H2^2) 2^edz, in place of H2 in the accumulators, then -> HBM split at
+  // that scale: [tile][s = nt >> 1][hi, lo][lane][4 (nt & 1) + i], i.e. each lane's eight values of an
+  // n-step are the A fragment F1b's same lane reads (pre-split: neither F1b nor F2 splits it again).
+  // The tile's exponent edz comes from the bound |dZ2| <= sum_a |dl_a| max |W3| (|1 - H2^2| <= 1): a
+  // wave max of one value per lane instead of one over the 64 products, and the power of two is folded
+  // into dl (exactly), so the products come out scaled.  The bound can sit a few binades above the
+  // tile's largest element; the split keeps all 22 bits of every element down to 2^-17 of the scale.
+  float w3m = s_w3m[0];
+#pragma unroll
+  for (int ww = 1; ww < W; ++ww) w3m = fmaxf(w3m, s_w3m[ww]);
+  float bnd = 0.f;
+#pragma unroll
+  for (int a = 0; a < AH; ++a) bnd += fabsf(dl[a]);
+  bnd = wave_max(bnd * w3m);
+  const int edz = bnd > 0.f ? sf_exp(bnd) : 120;  // an all-zero tile: the largest exponent (F2 takes the min)
+  {
+    const float sdz = sgn * pow2(edz);  // (handed over with the tile's sign)
+#pragma unroll
+    for (int a = 0; a < AH; ++a) dl[a] *= sdz;
+  }
 #pragma unroll
   for (int nt = 0; nt < 16; ++nt) {
     const int n0 = 16 * nt + 4 * gq;
     float gs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int a = 0; a < A_; ++a) {
+    for (int a = 0; a < AH; ++a) {
       const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);
       gs[0] = fmaf(dl[a], t.x, gs[0]);
       gs[1] = fmaf(dl[a], t.y, gs[1]);
@@ -699,16 +747,12 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float h2 = acc[nt][i];
-      acc[nt][i] = gs[i] * (1.f - h2 * h2);
-      dmx = fmaxf(dmx, fabsf(acc[nt][i]));
+      const float r = acc[nt][i];
+      acc[nt][i] = gs[i] * (4.f * fmaf(-r, r, r));  // (no cancellation where H2 saturates, unlike 1 - H2^2)
     }
     if constexpr (A_ > 4) asm volatile("" ::: "memory");
   }
-  dmx = wave_max(dmx);
-  const int edz = dmx > 0.f ? sf_exp(dmx) : 120;  // an all-zero tile: the largest exponent (F2 takes the min)
   {
-    const float sdz = pow2(edz);
     _Float16* dst = N.dz2s + (size_t)tile * (16 * HID * 2) + l * 8;
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
@@ -716,7 +760,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         _Float16 a, b;
-        split1(acc[2 * st + (j >> 2)][j & 3] * sdz, a, b);
+        split1(acc[2 * st + (j >> 2)][j & 3], a, b);
         hi[j] = a;
         lo[j] = b;
       }
@@ -725,7 +769,6 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
     }
   }
   if (l == 0) {
-    atomicMax(dz_slot(N.dzmax, tile), __float_as_uint(dmx));
     N.tile_edz[tile] = edz;
     N.tile_ex[tile] = ex;
   }
@@ -734,17 +777,35 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   __syncthreads();
   const int blk = blockIdx.x;
   for (int e = tid; e < A_ * HID; e += NTHR) {
+    const int a = e >> 8, n = e & (HID - 1);
     float s = 0.f;
+    if (a < AH) {
 #pragma unroll
-    for (int ww = 0; ww < W; ++ww) s += sSlot[ww * A_ * HID + e];
+      for (int ww = 0; ww < W; ++ww) s += sSlot[(ww * AH + a) * HID + n];
+    } else {  // the policy's last action: dW3[A-1] = -sum_{a < A-1} dW3[a]
+#pragma unroll
+      for (int b = 0; b < AH; ++b) {
+        float sb = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) sb += sSlot[(ww * AH + b) * HID + n];
+        s += sb;
+      }
+      s = -s;
+    }
     N.part_w3[(size_t)blk * A_ * HID + e] = s;
   }
   if (tid < A_ + 4) {
     float s = 0.f;
 #pragma unroll
     for (int ww = 0; ww < W; ++ww) s += sSlot[SLOT_B3 + ww * (A_ + 4) + tid];
-    if (tid < A_) N.part_b3[(size_t)blk * A_ + tid] = s;
-    else N.part_stat[(size_t)blk * 4 + tid - A_] = s;
+    if (tid >= A_) N.part_stat[(size_t)blk * 4 + tid - A_] = s;
+    else if (NET == 0) N.part_b3[(size_t)blk * A_ + tid] = s;
+    else {  // [blk][hi, lo]
+      double vx = 0.0;
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) vx += s_vx[ww];
+      vf_b3_part(vx, g.co.vf_loss_coeff, load_dyn(g).inv_count, N.part_b3 + (size_t)blk * 2);
+    }
   }
 }
 
@@ -827,8 +888,9 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1
   // sat 2^8-2^12 below it and their lo halves fell into fp16 subnormals, dW1 / db1 ~5x less accurate
   // per element than fp32); then dW1a^T = Xa^T dZ1 per k-tile
   h8 xh, xl;
-  const int ex = x_frag(g, row0, c, gq, xh, xl);
-  const float sx = pow2(ex), k_z1 = N.sc[1] / sx * SF_2LOG2E;
+  const float sgn = tile_sign(tile);
+  const int ex = x_frag(g, row0, c, gq, xh, xl, sgn);
+  const float sx = pow2(ex), k_z1 = sgn * N.sc[1] / sx * SF_2LOG2E;
   // 1 - H1^2 = 4 r (1 - r): the 4 joins the unscaling power of two
   float zmx = 0.f;
   const _Float16* w1b = sW1 + w1_off<KD>(c, gq & (KD / 8 - 1));  // row c; rows 16 kt + c at immediates
@@ -845,7 +907,7 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1
     }
   }
   const int ez = sf_exp(wave_max(zmx));
-  const float sz1 = pow2(ez), u1 = pow2(2 - ex - edz - (int)N.sc[5] - ez);
+  const float sz1 = pow2(ez), u1 = sgn * pow2(2 - ex - edz - (int)N.sc[5] - ez);  // (sgn: F1a's tile sign)
   h4 xth[DT], xtl[DT];  // Xa^T (16x16x16 A operand): rows d = 16 dt + c, columns m = 4g + j
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
@@ -982,7 +1044,9 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
 #pragma unroll
   for (int i = 0; i < F2_THREADS / 64; ++i) emin = min(emin, (int)s_emin[i]);
   const int E = __builtin_amdgcn_readfirstlane(emin);
-  const float unscale = pow2(-14 - E);
+  // this split's sign (tile_sign: odd splits run their products on -H1 and negate the partial back)
+  const float ssgn = tile_sign(blockIdx.x);
+  const float unscale = ssgn * pow2(-14 - E);
 
   // per-lane fragment bases (halves within a buffer):
   //   A (transposed reads): lane 4 q + p of its 16-lane group addresses row 4 h + q (+ 16 s, + 8 for
@@ -1092,7 +1156,7 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
   auto store_h1 = [&](_Float16* img) {
     // X scale of the chunk from F1a's per-tile exponents (the larger max: the smaller exponent)
     const int ex = min(xe.x, xe.y);
-    const float sx = pow2(ex), k_z1 = inv_w1 * pow2(-ex) * SF_2LOG2E;
+    const float sx = ssgn * pow2(ex), k_z1 = ssgn * inv_w1 * pow2(-ex) * SF_2LOG2E;
     f32x16 z;
 #pragma unroll
     for (int q = 0; q < 16; ++q) z[q] = 0.f;
@@ -1114,7 +1178,8 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
       z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wh[kb], z, 0, 0, 0);
     }
     // rows of tile 2t + (q >> 3): H1 split at 2^(14 + E - e_T) (<= 2^14)
-    const float hs0 = pow2(14 + E - de.x), hs1 = pow2(14 + E - de.y);
+    // (the chunk's odd tile arrives negated from F1a: -hs1 undoes it)
+    const float hs0 = ssgn * pow2(14 + E - de.x), hs1 = -ssgn * pow2(14 + E - de.y);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float hs = i < 2 ? hs0 : hs1;
@@ -1122,7 +1187,7 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         _Float16 a, b;
-        split1((SF_TANH_XP & 1) ? hs * tanh_u(z[4 * i + j] * k_z1) : fmaf(-2.f * hs, tanh_r(z[4 * i + j] * k_z1), hs), a, b);
+        split1(fmaf(-2.f * hs, tanh_r(z[4 * i + j] * k_z1), hs), a, b);
         hh[j] = a;
         hl[j] = b;
       }
@@ -1134,7 +1199,7 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
   // production of the loaded chunk into img; counted: add its dZ2 to db2
   auto produce = [&](_Float16* img, bool counted) {
     if constexpr (KB > 2) load_w1();
-    const float s0 = counted ? pow2(-de.x) : 0.f, s1 = counted ? pow2(-de.y) : 0.f;
+    const float s0 = counted ? pow2(-de.x) : 0.f, s1 = counted ? -pow2(-de.y) : 0.f;  // (odd tile: negated)
     store_dz(img, s0, s1);
     store_h1(img);
   };
@@ -1293,7 +1358,7 @@ __device__ __forceinline__ void fwd16_body(const SfFwdArgs& g) {
         }
         float hv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hv[j] = (SF_TANH_XP & 8) ? SF_H1_SCALE * tanh_u(z[j >> 2][j & 3] * k_z1) : fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
+        for (int j = 0; j < 8; ++j) hv[j] = fmaf(-2.f * SF_H1_SCALE, tanh_r(z[j >> 2][j & 3] * k_z1), SF_H1_SCALE);
         split8(hv, 0, 1.f, bh, bl);
       }
       const _Float16* buf = sCh + ph * 2 * H16;
@@ -1324,7 +1389,7 @@ __device__ __forceinline__ void fwd16_body(const SfFwdArgs& g) {
     const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
     float hv[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) hv[i] = (SF_TANH_XP & 8) ? tanh_u(fmaf(acc[nt][i], k_z2, bv[i])) : fmaf(-2.f, tanh_r(fmaf(acc[nt][i], k_z2, bv[i])), 1.f);
+    for (int i = 0; i < 4; ++i) hv[i] = fmaf(-2.f, tanh_r(fmaf(acc[nt][i], k_z2, bv[i])), 1.f);
 #pragma unroll
     for (int a = 0; a < A_; ++a) {
       const float4 t = *reinterpret_cast<const float4*>(sW3 + a * HID + n0);

@@ -9,7 +9,7 @@
 // Per net and SGD step (M minibatch rows; W1 [H][D], W2 [H][H], W3 [A][H] torch layouts):
 //   H1 = tanh(X W1^T + b1)   H2 = tanh(H1 W2^T + b2)   out = H2 W3^T + b3          (NT GEMMs)
 //   k_wide_loss_pi / _vf: dout [M][A] (+ per-block loss stats)
-//   dW3 = dout^T H2 (TN)   db3 = colsum(dout)
+//   dW3 = dout^T H2 (TN)   db3 = colsum(dout) (value net: k_wide_vb3, exact row differences in f64)
 //   dZ2 = (dout W3) * (1 - H2^2) (NN, fused)   dW2 = dZ2^T H1 (TN)   db2 = colsum(dZ2)
 //   dZ1 = (dZ2 W2) * (1 - H1^2) (NN, fused)    dW1 = dZ1^T X  (TN)   db1 = colsum(dZ1)
 // The three H x H GEMMs (Z2, dZ1, dW2) run on the pre-split kernel (gemm_ps.hip): H1 is written as
@@ -61,12 +61,12 @@ WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
   w.xl = (_Float16*)take(2LL * Mp * D);
   w.rew64 = (double*)take(8LL * M);
   {  // weight-gradient partials: dW3 [A][H], dW2 [H][H], dW1 [H][D] (K = M), column sums of M rows
-    int64_t pf = (int64_t)colsum_splits(M) * H;
+    int64_t pf = (int64_t)2 * colsum_splits(M) * H;  // (hi, lo planes)
     pf = std::max(pf, (int64_t)gemm_splits(A, H, M) * A * H);
     pf = std::max(pf, (int64_t)gemm_ps_splits(H, H, Mp) * H * H);
     pf = std::max(pf, (int64_t)gemm_ps_splits(H, D, Mp) * H * D);
     pf = std::max(pf, (int64_t)gemm_splits(H, D, M) * H * D);
-    pf = std::max(pf, (int64_t)((M + 511) / 512) * H);  // k_wide_dz2's db2 partials (DZ_ROWS x DZ_RT rows each)
+    pf = std::max(pf, (int64_t)2 * ((M + 511) / 512) * H);  // k_wide_dz2's db2 partials (DZ_ROWS x DZ_RT rows each; hi, lo)
     w.part = (float*)take(4 * pf);
   }
   w.stat_slots = (unsigned*)take(4 * 4);
@@ -84,29 +84,48 @@ __global__ __launch_bounds__(LOSS_ROWS) void k_wide_loss_vf(const float* __restr
                                                           const float* __restrict__ dyn, float* __restrict__ dout,
                                                           float* __restrict__ part_stat, unsigned* __restrict__ dmax) {
   __shared__ float red[LOSS_ROWS / 64];
+  __shared__ double redx[LOSS_ROWS / 64];
   const int m = blockIdx.x * LOSS_ROWS + threadIdx.x;
   float vl = 0.f, mx_d = 0.f;
+  double ex = 0.0;
   if (m < M) {
-    const float* rec = x + (size_t)m * stride;
-    const float diff = out[m] - rec[D + A + 1];
-    const float sq = diff * diff;
-    vl = fminf(sq, co.vf_clip_param);
-    const float d = (sq <= co.vf_clip_param) ? co.vf_loss_coeff * 2.f * diff * dyn[RLKS_DYN_INV_COUNT] : 0.f;
-    dout[m] = d;
-    mx_d = fabsf(d);
+    const VfRow v = vf_row(out[m], x[(size_t)m * stride + D + A + 1], co.vf_clip_param, co.vf_loss_coeff,
+                           dyn[RLKS_DYN_INV_COUNT]);
+    vl = v.sq;
+    dout[m] = v.dl;
+    mx_d = fabsf(v.dl);
+    ex = v.ex;
   }
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float s = wave_sum(vl);
-  if (l == 0) red[w] = s;
+  const double sx = wave_sum(ex);
+  if (l == 0) {
+    red[w] = s;
+    redx[w] = sx;
+  }
   mx_d = wave_max(mx_d);
   if (l == 0) atomicMax(dmax, __float_as_uint(mx_d));
   __syncthreads();
-  if (threadIdx.x < 4) {
+  if (threadIdx.x < 2) {  // slot 1: the vf loss stat; slots 2, 3 (unused by the value net's stats): db3 hi, lo
     float t = 0.f;
     if (threadIdx.x == 1)
       for (int j = 0; j < LOSS_ROWS / 64; ++j) t += red[j];
     part_stat[(size_t)blockIdx.x * 4 + threadIdx.x] = t;
+  } else if (threadIdx.x == 2) {
+    double t = 0.0;
+    for (int j = 0; j < LOSS_ROWS / 64; ++j) t += redx[j];
+    vf_b3_part(t, co.vf_loss_coeff, dyn[RLKS_DYN_INV_COUNT], part_stat + (size_t)blockIdx.x * 4 + 2);
   }
+}
+
+// the value head's bias gradient: every block's (hi, lo) pair of k_wide_loss_vf summed in f64, fixed
+// order (64 lanes over strided blocks, then the lanes)
+__global__ __launch_bounds__(64) void k_wide_vb3(const float* __restrict__ part_stat, int blocks, float* __restrict__ out) {
+  double t = 0.0;
+  for (int b = threadIdx.x; b < blocks; b += 64)
+    t += (double)part_stat[(size_t)b * 4 + 2] + (double)part_stat[(size_t)b * 4 + 3];
+  t = wave_sum(t);
+  if (threadIdx.x == 0) out[0] = (float)t;
 }
 
 // the policy net's loss with one wave per row and one lane per action (A <= 64; 16 waves per block of
@@ -114,49 +133,62 @@ __global__ __launch_bounds__(LOSS_ROWS) void k_wide_loss_vf(const float* __restr
 // logits of a row are one coalesced load each, the softmax sums wave reductions.  (One thread per row,
 // looping over 64 actions with row-strided loads, took 0.29 ms per SGD step at c5: one wave per SIMD
 // and 64 cache lines per load instruction.)  Same per-block stats layout as k_wide_loss_vf.
+// The loss and dL/dlogits are evaluated in f64 from the fp32 logits and rounded once: every bias
+// gradient downstream (db2 = colsum((dout W3)(1 - H2^2)), db1) is a sum over rows that cancels, and
+// at the elements where it cancels most the fp32 loss arithmetic's few-ulp error per row (softmax,
+// log-sum-exp, ratio) was the largest part of the result's error (tools/wide_b2_isolate.py,
+// profiles/r05_precision).  ~a few hundred DP ops per row: noise beside the step's GEMMs.
 constexpr int LOSS_PI_WAVES = 16;  // waves per policy-loss block: LOSS_ROWS / 16 rows each (4 waves per SIMD)
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
 __global__ __launch_bounds__(64 * LOSS_PI_WAVES) void k_wide_loss_pi(const float* __restrict__ out, const float* __restrict__ x,
                                                           int stride, int M, int D, int A, rlks_ppo_coeffs co,
                                                           const float* __restrict__ dyn, float* __restrict__ dout,
                                                           float* __restrict__ part_stat, unsigned* __restrict__ dmax) {
   constexpr int RPW = LOSS_ROWS / LOSS_PI_WAVES;  // rows per wave
-  __shared__ float red[4][LOSS_PI_WAVES];
+  __shared__ double red[3][LOSS_PI_WAVES];
+  __shared__ float redm[LOSS_PI_WAVES];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const bool on = l < A;
-  const float inv_count = dyn[RLKS_DYN_INV_COUNT], klc = dyn[RLKS_DYN_KL_COEFF];
-  const float adv_mean = dyn[RLKS_DYN_ADV_MEAN], adv_invstd = dyn[RLKS_DYN_ADV_INVSTD];
-  const float lo_c = 1.f - co.clip_param, hi_c = 1.f + co.clip_param;
-  float st0 = 0.f, st2 = 0.f, st3 = 0.f, mx_d = 0.f;
+  const double inv_count = dyn[RLKS_DYN_INV_COUNT], klc = dyn[RLKS_DYN_KL_COEFF];
+  const double adv_mean = dyn[RLKS_DYN_ADV_MEAN], adv_invstd = dyn[RLKS_DYN_ADV_INVSTD];
+  const double lo_c = 1.0 - (double)co.clip_param, hi_c = 1.0 + (double)co.clip_param;
+  const double ent_c = co.entropy_coeff;
+  double st0 = 0.0, st2 = 0.0, st3 = 0.0;
+  float mx_d = 0.f;
   for (int i = 0; i < RPW; ++i) {
     const int m = blockIdx.x * LOSS_ROWS + w * RPW + i;
     if (m >= M) break;
     const float* rec = x + (size_t)m * stride;
-    const float lg = on ? out[(size_t)m * A + l] : -INFINITY, lo = on ? rec[D + l] : -INFINITY;
-    const float adv = (rec[D + A] - adv_mean) * adv_invstd;
-    const float logp_old = rec[D + A + 2];
+    const double lg = on ? (double)out[(size_t)m * A + l] : -INFINITY, lo = on ? (double)rec[D + l] : -INFINITY;
+    const double adv = ((double)rec[D + A] - adv_mean) * adv_invstd;
+    const double logp_old = rec[D + A + 2];
     const int act = (int)rec[D + A + 3];
-    const float mx = wave_max(lg), mo = wave_max(lo);
-    const float lse = mx + logf(wave_sum(on ? expf(lg - mx) : 0.f)), lso = mo + logf(wave_sum(on ? expf(lo - mo) : 0.f));
-    const float lp = lg - lse, p = on ? expf(lp) : 0.f, lpo = lo - lso, po = on ? expf(lpo) : 0.f;
-    const float kl = wave_sum(on ? po * (lpo - lp) : 0.f);
-    const float ent = -wave_sum(on ? p * lp : 0.f);
-    const float lpa = wave_sum(l == act ? lp : 0.f);
-    const float ratio = expf(lpa - logp_old);
-    const float rc = fminf(fmaxf(ratio, lo_c), hi_c);
-    const float s1 = adv * ratio, s2 = adv * rc;
+    const double mx = wave_max_d(lg), mo = wave_max_d(lo);
+    const double lse = mx + log(wave_sum(on ? exp(lg - mx) : 0.0)), lso = mo + log(wave_sum(on ? exp(lo - mo) : 0.0));
+    const double lp = lg - lse, p = on ? exp(lp) : 0.0, lpo = lo - lso, po = on ? exp(lpo) : 0.0;
+    const double kl = wave_sum(on ? po * (lpo - lp) : 0.0);
+    const double ent = -wave_sum(on ? p * lp : 0.0);
+    const double lpa = wave_sum(l == act ? lp : 0.0);
+    const double ratio = exp(lpa - logp_old);
+    const double rc = fmin(fmax(ratio, lo_c), hi_c);
+    const double s1 = adv * ratio, s2 = adv * rc;
     // torch.min backward splits ties evenly; torch.clamp passes the gradient on [lo, hi]
-    const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
-    const float inr = (ratio >= lo_c && ratio <= hi_c) ? 1.f : 0.f;
-    const float dr = -adv * (w1 + (1.f - w1) * inr) * ratio;
+    const double w1 = s1 < s2 ? 1.0 : (s1 == s2 ? 0.5 : 0.0);
+    const double inr = (ratio >= lo_c && ratio <= hi_c) ? 1.0 : 0.0;
+    const double dr = -adv * (w1 + (1.0 - w1) * inr) * ratio;
     if (on) {
-      float d = dr * ((l == act ? 1.f : 0.f) - p);
+      double d = dr * ((l == act ? 1.0 : 0.0) - p);
       d += klc * (p - po);
-      d += co.entropy_coeff * p * (lp + ent);
-      d *= inv_count;
-      dout[(size_t)m * A + l] = d;
-      mx_d = fmaxf(mx_d, fabsf(d));
+      d += ent_c * p * (lp + ent);
+      const float df = (float)(d * inv_count);
+      dout[(size_t)m * A + l] = df;
+      mx_d = fmaxf(mx_d, fabsf(df));
     }
-    st0 -= fminf(s1, s2);
+    st0 -= fmin(s1, s2);
     st2 += kl;
     st3 += ent;
   }
@@ -165,20 +197,20 @@ __global__ __launch_bounds__(64 * LOSS_PI_WAVES) void k_wide_loss_pi(const float
     red[0][w] = st0;
     red[1][w] = st2;
     red[2][w] = st3;
-    red[3][w] = mx_d;
+    redm[w] = mx_d;
   }
   __syncthreads();
   if (threadIdx.x == 64) {  // one atomic per block (single-address atomics serialise at their L2 channel)
     float m = 0.f;
-    for (int j = 0; j < LOSS_PI_WAVES; ++j) m = fmaxf(m, red[3][j]);
+    for (int j = 0; j < LOSS_PI_WAVES; ++j) m = fmaxf(m, redm[j]);
     atomicMax(dmax, __float_as_uint(m));
   }
   if (threadIdx.x < 4) {
     const int k = threadIdx.x;
-    float s = 0.f;
+    double s = 0.0;
     if (k != 1)
       for (int j = 0; j < LOSS_PI_WAVES; ++j) s += red[k == 0 ? 0 : k - 1][j];
-    part_stat[(size_t)blockIdx.x * 4 + k] = s;
+    part_stat[(size_t)blockIdx.x * 4 + k] = (float)s;
   }
 }
 
@@ -231,7 +263,8 @@ __global__ void k_wide_sample(EnvView v, const float* __restrict__ logits, int A
 // GEMM's K pipeline (its tile prologue and epilogue were the whole 0.71 ms), so plain fp32 FMAs in k
 // order on 64-row x 256-column tiles (8 per block): dout^T and W3 tiles in LDS (K chunks of 32), 8 x 8
 // outputs per thread, H2 read and dZ2 written as float4 rows; max |dZ2| -> slot (one atomic per
-// block); db2 as per-block column sums (a fixed order), summed by launch_split_reduce
+// block); db2 as per-block column sums in f64 (a fixed order; hi + lo planes), summed by launch_split_reduce.
+// 1 - H2^2 as one fma (a single rounding where H2 saturates)
 constexpr int DZ_ROWS = 64, DZ_COLS = 256, DZ_K = 32, DZ_RT = 8;  // DZ_RT row tiles per block
 __global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout, const float* __restrict__ w3,
                                                   const float* __restrict__ h2, float* __restrict__ dz, int M, int H,
@@ -242,7 +275,8 @@ __global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout
   const int n0 = blockIdx.x * DZ_COLS;
   int n = n0 + 8 * cg;  // this thread's 8 columns (H % 8 == 0: host check)
   if (!dcheck(n + 8 <= H || n0 + DZ_COLS > H, DC_WIDE_COL, n)) n = H - 8;
-  float mx = 0.f, cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // max |dZ2|, db2: this thread's column sums
+  float mx = 0.f;  // max |dZ2|
+  double cs[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // db2: this thread's column sums (f64)
   for (int rt = 0; rt < DZ_RT; ++rt) {
     const int m0 = (blockIdx.y * DZ_RT + rt) * DZ_ROWS;
     if (m0 >= M) break;
@@ -287,9 +321,9 @@ __global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          o[j] = acc[i][j] * (1.f - gv[j] * gv[j]);
+          o[j] = acc[i][j] * fmaf(-gv[j], gv[j], 1.f);
           mx = fmaxf(mx, fabsf(o[j]));
-          cs[j] += o[j];
+          cs[j] += (double)o[j];
         }
         float4* dp = reinterpret_cast<float4*>(dz + (size_t)m * H + n);
         dp[0] = make_float4(o[0], o[1], o[2], o[3]);
@@ -302,16 +336,18 @@ __global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout
   if ((tid & 63) == 0) red[tid >> 6] = mx;
   // db2 partial of the block's rows: the 8 row groups' column sums combined in a fixed order
   __syncthreads();  // (every thread is past its last read of sB)
-  float* sC = &sB[0][0];  // [8 rg][256]
+  double* sC = reinterpret_cast<double*>(&sB[0][0]);  // [8 rg][256] (16 KB of sB's 32)
 #pragma unroll
   for (int j = 0; j < 8; ++j) sC[rg * DZ_COLS + 8 * cg + j] = cs[j];
   __syncthreads();
   if (tid == 0) atomicMax(cmax_slot, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
-  if (n0 + tid < H) {
-    float t = 0.f;
+  if (n0 + tid < H) {  // the block's column sum as an exact-ish hi + lo pair: planes y and gridDim.y + y
+    double t = 0.0;
 #pragma unroll
     for (int g = 0; g < 8; ++g) t += sC[g * DZ_COLS + tid];
-    part_db2[(size_t)blockIdx.y * H + n0 + tid] = t;
+    const float hi = (float)t;
+    part_db2[(size_t)blockIdx.y * H + n0 + tid] = hi;
+    part_db2[(size_t)(gridDim.y + blockIdx.y) * H + n0 + tid] = (float)(t - (double)hi);
   }
 }
 
@@ -445,7 +481,12 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     if (int rc = gemm(n.dout, An, 1, n.h2, H, 0, g + o[4], H, An, H, M, GEMM_STORE, nullptr, nullptr, 0,
                       sl + SL_DOUT, sl + SL_H2, nullptr, s, w.part))
       return rc;
-    if (int rc = launch_colsum(n.dout, M, An, An, g + o[5], 0, w.part, s)) return rc;
+    if (net == 0) {
+      if (int rc = launch_colsum(n.dout, M, An, An, g + o[5], 0, w.part, s)) return rc;
+    } else {
+      hipLaunchKernelGGL(k_wide_vb3, dim3(1), dim3(64), 0, s, n.part_stat, w.blocks, g + o[5]);
+      RLKS_LAUNCHED();
+    }
     // dZ2 = (dout W3) (1 - H2^2); dW2 = dZ2^T H1; db2
     RLKS_REQUIRE(H % 8 == 0, RLKS_ERR_UNSUPPORTED, "wide path: hidden width must be a multiple of 8");
     const int dz_blocks = (int)cdiv(M, DZ_ROWS * DZ_RT);
@@ -453,7 +494,7 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
                        An, sl + SL_DZ2, w.part);
     RLKS_LAUNCHED();
     // db2 from the dZ2 kernel's per-block column sums (before dW2's split-K reuses the partial buffer)
-    if (int rc = launch_split_reduce(w.part, dz_blocks, 1, H, g + o[3], H, 0, s)) return rc;
+    if (int rc = launch_split_reduce(w.part, 2 * dz_blocks, 1, H, g + o[3], H, 0, s)) return rc;  // hi + lo planes
     if (int rc = launch_split_planes(w.dza, M, H, H, sl + SL_DZ2, 0, w.dzh, w.dzl, H, s)) return rc;
     {  // dW2[n][k] = sum_m dZ2[m][n] H1[m][k]: both operands K-major planes, split over the rows
       PsArgs a{};

@@ -93,6 +93,8 @@ SIGNATURES = {
     "rlks_env_mt_discard": [_P, _P, _P, _P],
     "rlks_env_mt_words": [_P, C.c_int, _P, C.c_int, _P],
     "rlks_debug_checks": [_P],
+    "rlks_debug_sf_handoff": [C.POINTER(MlpDesc), _I, _P, _P],
+    "rlks_debug_wide_bufs": [C.POINTER(MlpDesc), _I, _P, _P],
     "rlks_sample_categorical": [_P, C.c_int, C.c_int, _P, C.c_ulonglong, C.c_int, _P, _P, _P],
     "rlks_env_reset": [_P, _P, _P, _P],
     "rlks_env_step": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
@@ -175,6 +177,8 @@ def lib() -> C.CDLL:
         _warn_if_stale()
         handle = C.CDLL(str(LIB_PATH))
         for name, argtypes in SIGNATURES.items():
+            if name.startswith("rlks_debug_") and not hasattr(handle, name):
+                continue  # diagnostics entry points of later builds (an older variant library for A/B runs)
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = _RESTYPES.get(name, C.c_int)

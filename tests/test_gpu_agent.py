@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 
 import oracle
-from parity import close_as_fp32, grad_close_as_fp32
+from parity import close_as_fp32, grad_close_as_fp32, rel_errors
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -116,7 +116,7 @@ def test_rollouts_carry_observations_and_sample_exactly(N, T):
             for t in (0, 1, T):
                 x = b["obs"][t][:4096]
                 el, ev = oracle.mlp_forward(flat, algo.params.offsets, 6, 256, 2, x)
-                fl, fv = oracle.mlp_forward(flat, algo.params.offsets, 6, 256, 2, x, dtype=np.float32)
+                fl, fv = oracle.mlp_forward_fp32_band(flat, algo.params.offsets, 6, 256, 2, x)
                 close_as_fp32(b["values"][t][:4096], ev, fv, what=f"values[{t}]")
                 if t < T:
                     close_as_fp32(b["logits"][t][:4096], el, fl, what=f"logits[{t}]")
@@ -300,9 +300,9 @@ def test_c4_shard_rollout_and_gradient():
     eg, est = oracle.ppo_loss_grad(algo.params.flat.cpu().numpy(), algo.params.offsets, 6, 256, 2,
                                    algo.mbuf.cpu().numpy(), kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]),
                                    adv_inv_std=float(dyn[1]), scale=True)
-    eg32, _ = oracle.ppo_loss_grad(algo.params.flat.cpu().numpy(), algo.params.offsets, 6, 256, 2,
-                                   algo.mbuf.cpu().numpy(), kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]),
-                                   adv_inv_std=float(dyn[1]), dtype=np.float32)
+    eg32 = oracle.ppo_loss_grad_fp32_band(algo.params.flat.cpu().numpy(), algo.params.offsets, 6, 256, 2,
+                                          algo.mbuf.cpu().numpy(), kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]),
+                                          adv_inv_std=float(dyn[1]))
     g = algo.grad.cpu().numpy()
     for i, (name, _, _) in enumerate(TENSOR_NAMES):
         o, n_ = algo.params.offsets[i], int(np.prod(algo.params.shapes[i]))
@@ -419,15 +419,13 @@ def test_sf16_gradient_per_element(rows, D, H, A, precision):
     flat = p.flat.cpu().numpy()
     kw = dict(kl_coeff=0.2, adv_mean=0.3, adv_inv_std=0.7)
     g64, _ = oracle.ppo_loss_grad(flat, p.offsets, D, H, A, mb, **kw)
-    g32, _ = oracle.ppo_loss_grad(flat, p.offsets, D, H, A, mb, dtype=np.float32, **kw)
-    g32 = g32.astype(np.float64)
+    g32 = oracle.ppo_loss_grad_fp32_band(flat, p.offsets, D, H, A, mb, **kw)
     rs, r32 = [], []
     for i, shp in enumerate(p.shapes):
         o, n = p.offsets[i], int(np.prod(shp))
-        ref = g64[o:o + n]
-        keep = np.abs(ref) > 1e-6 * np.abs(ref).max()
-        rs.append(np.abs(gs[o:o + n] - ref)[keep] / np.abs(ref[keep]))
-        r32.append(np.abs(g32[o:o + n] - ref)[keep] / np.abs(ref[keep]))
+        e, e32 = rel_errors(gs[o:o + n], g64[o:o + n], [r[o:o + n] for r in g32])
+        rs.append(e)
+        r32.append(e32)
     rs, r32 = np.concatenate(rs), np.concatenate(r32)
     qs = (50, 99, 99.9)
     a, b = np.percentile(rs, qs), np.percentile(r32, qs)

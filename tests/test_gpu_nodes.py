@@ -151,7 +151,7 @@ def test_ppo_on_node_envs(C, nodes, H, N, T, mb, precision):
     flat = algo.params.flat.cpu().numpy()
     for t in (0, T // 2, T):
         el, ev = oracle.mlp_forward(flat, algo.params.offsets, 3 * C, H, C, b["obs"][t])
-        fl, fv = oracle.mlp_forward(flat, algo.params.offsets, 3 * C, H, C, b["obs"][t], dtype=np.float32)
+        fl, fv = oracle.mlp_forward_fp32_band(flat, algo.params.offsets, 3 * C, H, C, b["obs"][t])
         close_as_fp32(b["values"][t], ev, fv, what=f"values[{t}]")
         if t < T:
             close_as_fp32(b["logits"][t], el, fl, what=f"logits[{t}]")
@@ -169,7 +169,7 @@ def test_ppo_on_node_envs(C, nodes, H, N, T, mb, precision):
               algo.ws.numel(), None)
     kw = dict(kl_coeff=float(dyn[2]), adv_mean=float(dyn[0]), adv_inv_std=float(dyn[1]))
     eg, est = oracle.ppo_loss_grad(flat, algo.params.offsets, 3 * C, H, C, mbh, **kw, scale=True)
-    eg32, _ = oracle.ppo_loss_grad(flat, algo.params.offsets, 3 * C, H, C, mbh, dtype=np.float32, **kw)
+    eg32 = oracle.ppo_loss_grad_fp32_band(flat, algo.params.offsets, 3 * C, H, C, mbh, **kw)
     g = algo.grad.cpu().numpy()
     assert np.linalg.norm(g - eg) <= 1e-5 * np.linalg.norm(eg)
     grad_close_as_fp32(g, eg, eg32, algo.params.offsets, algo.params.shapes, scale=est["scale"])
@@ -210,7 +210,7 @@ def test_node_rollout_ragged_lanes(C, N, T):
     flat = algo.params.flat.cpu().numpy()
     for t in (0, 1, T):
         el, ev = oracle.mlp_forward(flat, algo.params.offsets, 3 * C, 256, C, b["obs"][t])
-        fl, fv = oracle.mlp_forward(flat, algo.params.offsets, 3 * C, 256, C, b["obs"][t], dtype=np.float32)
+        fl, fv = oracle.mlp_forward_fp32_band(flat, algo.params.offsets, 3 * C, 256, C, b["obs"][t])
         close_as_fp32(b["values"][t], ev, fv, what=f"values[{t}]")
         if t < T:
             close_as_fp32(b["logits"][t], el, fl, what=f"logits[{t}]")
@@ -266,7 +266,7 @@ def test_node_rollout_full_c3_size():
     rows = slice(0, 16384)   # a quarter of the lanes: the fp64 / fp32 CPU forwards stay in seconds
     for t in (0, T):
         el, ev = oracle.mlp_forward(flat, algo.params.offsets, 24, 256, 8, b["obs"][t][rows])
-        fl, fv = oracle.mlp_forward(flat, algo.params.offsets, 24, 256, 8, b["obs"][t][rows], dtype=np.float32)
+        fl, fv = oracle.mlp_forward_fp32_band(flat, algo.params.offsets, 24, 256, 8, b["obs"][t][rows])
         close_as_fp32(b["values"][t][rows], ev, fv, what=f"values[{t}]")
         if t < T:
             close_as_fp32(b["logits"][t][rows], el, fl, what=f"logits[{t}]")

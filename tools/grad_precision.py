@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-tensor precision of the SGD-step gradient against the float64 oracle, beside a float32
-reference of the same computation (the diagnostic behind tests/parity.py's bias-tensor checks).
+reference band of the same computation (oracle.ppo_loss_grad_fp32_band, element-wise worst of
+three fp32 evaluations; the diagnostic behind tests/parity.py's bias-tensor checks).
 
   RLKS_LIB=<variant .so> python3 tools/grad_precision.py [--quick] [--json out.json]
 
@@ -41,7 +42,7 @@ def run_case(path, rows, D, H, A, seed_off=0):
     p.desc.precision = 1 if path == "sf16" else _lib.RLKS_PRECISION_WIDE
     # inputs and oracle results cached per case, so that every library variant sees the same
     # minibatch (its generation runs the library's forward) and the oracle runs once
-    cache = ROOT / "gpurun_out" / "grad_precision_cache" / f"{path}_{rows}_{D}_{H}_{A}_{seed_off}.npz"
+    cache = Path(os.environ.get("TMPDIR", "/tmp")) / "rlks_grad_precision_cache" / f"{path}_{rows}_{D}_{H}_{A}_{seed_off}.npz"
     if cache.exists():
         z = np.load(cache)
         mb = z["mb"]
@@ -65,21 +66,24 @@ def run_case(path, rows, D, H, A, seed_off=0):
     kw = dict(entropy_coeff=0.01, kl_coeff=klc, adv_mean=adv_mean, adv_inv_std=adv_invstd)
     flat = p.flat.cpu().numpy()
     if z is not None:
-        eg, est, eg32 = z["eg"], {"scale": z["scale"]}, z["eg32"]
+        eg, est, band = z["eg"], {"scale": z["scale"]}, list(z["band"])
     else:
         eg, est = oracle.ppo_loss_grad(flat, p.offsets, D, H, A, mb, scale=True, **kw)
-        eg32, _ = oracle.ppo_loss_grad(flat, p.offsets, D, H, A, mb, dtype=np.float32, **kw)
+        band = oracle.ppo_loss_grad_fp32_band(flat, p.offsets, D, H, A, mb, **kw)
         cache.parent.mkdir(parents=True, exist_ok=True)
-        np.savez(cache, mb=mb, eg=eg, scale=est["scale"], eg32=eg32)
+        np.savez(cache, mb=mb, eg=eg, scale=est["scale"], band=np.stack(band))
     out = []
     for i, (name, kind, net) in enumerate(TENSOR_NAMES):
         o, n = p.offsets[i], int(np.prod(p.shapes[i]))
-        a, b, c = g[o:o + n], eg[o:o + n], np.asarray(eg32[o:o + n], np.float64)
+        a, b = g[o:o + n], eg[o:o + n]
+        c = [np.asarray(r[o:o + n], np.float64) for r in band]
         s = np.asarray(est["scale"][o:o + n], np.float64)
         keep = np.abs(b) > 1e-6 * np.abs(b).max()
-        e, e32 = np.abs(a - b)[keep] / np.abs(b[keep]), np.abs(c - b)[keep] / np.abs(b[keep])
+        e = np.abs(a - b)[keep] / np.abs(b[keep])
+        e32 = np.max([np.abs(r - b)[keep] for r in c], axis=0) / np.abs(b[keep])
         ks = s > 0
-        es, es32 = np.abs(a - b)[ks] / s[ks], np.abs(c - b)[ks] / s[ks]
+        es = np.abs(a - b)[ks] / s[ks]
+        es32 = np.max([np.abs(r - b)[ks] for r in c], axis=0) / s[ks]
         rec = {"tensor": i, "name": f"{'pi' if net == 0 else 'vf'}.{kind}", "n": int(keep.sum()),
                "rel_max": float(e.max()), "rel_max_fp32": float(e32.max()),
                "rel_p99": float(np.percentile(e, 99)), "rel_p99_fp32": float(np.percentile(e32, 99)),
