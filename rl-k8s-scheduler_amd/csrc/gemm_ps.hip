@@ -109,11 +109,12 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   }
   const int n0 = bx * PT, m0 = by * PT;
   const int ea = op_exp(g.a), eb = op_exp(g.b);
-  // rounding-bias cancellation (sgd_sf16.hip tile_sign): workgroups alternate the sign of their A
-  // fragments by row block and split layer, and unscale negates the result back, so the slight negative
-  // lean of the MFMA accumulation does not add up coherently over the row blocks / splits that a
-  // gradient (or the next layer's bias gradient) sums
-  const bool neg = ((by + (int)blockIdx.z) & 1) != 0;
+  // rounding-bias cancellation (sgd_sf16.hip tile_sign) in the dZ1 GEMM: workgroups alternate the
+  // sign of their A fragments by row block, and unscale negates the result back, so the slight
+  // negative lean of the MFMA accumulation does not add up coherently in db1 = colsum(dZ1).  Only
+  // here: without it pi.b1 sat at 4.4x fp32 (p50, 4096 rows); on every GEMM it cost 3-4.5% of their
+  // time for no measurable gain (profiles/r05_precision)
+  const bool neg = EPI == PS_DTANH && ((by + (int)blockIdx.z) & 1) != 0;
   const unsigned nmask = neg ? 0x80008000u : 0u;
   const float unscale = (neg ? -1.f : 1.f) * ldexpf(1.f, -ea - eb);
   // this workgroup's K range (split-K: layer z)

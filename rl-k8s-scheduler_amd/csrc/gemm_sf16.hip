@@ -157,9 +157,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int wm = w >> 1, wn = w & 1;
   const int n0 = blockIdx.x * GT, m0 = blockIdx.y * GT;
   const int ea = sf_exp(__uint_as_float(*g.amax)), eb = sf_exp(__uint_as_float(*g.bmax));
-  // rounding-bias cancellation (gemm_ps.hip, sgd_sf16.hip tile_sign): A enters negated in odd row
-  // blocks / split layers, and the result is negated back
-  const float sg = ((blockIdx.y + blockIdx.z) & 1) ? -1.f : 1.f;
+  // rounding-bias cancellation in the dZ1 GEMM (gemm_ps.hip, sgd_sf16.hip tile_sign): A enters
+  // negated in odd row blocks / split layers, and the result is negated back
+  const float sg = (EPI == GEMM_DTANH && ((blockIdx.y + blockIdx.z) & 1)) ? -1.f : 1.f;
   const float sa = sg * ldexpf(1.f, ea), sb = ldexpf(1.f, eb), unscale = sg * ldexpf(1.f, -ea - eb);
 
   // register ring of two chunks per operand: while chunk c is multiplied, chunks c + 1 (parked in
@@ -361,9 +361,37 @@ __global__ __launch_bounds__(256) void k_split_reduce(const float* __restrict__ 
   }
 }
 
+// the same for few outputs over many layers (bias column sums: 2,048 columns x 256 hi / lo layers at
+// c5, where one thread per output left 8 workgroups summing 256 values each): 32 outputs x 8 layer
+// groups per workgroup, each group summing its layers z = zg, zg + 8, ... in order, the 8 group sums
+// then added in order (a fixed order: deterministic)
+constexpr int SR_COLS = 32, SR_ZG = 8;
+__global__ __launch_bounds__(SR_COLS * SR_ZG) void k_split_reduce_narrow(const float* __restrict__ part, int splits, int n,
+                                                                         float* __restrict__ out, int accumulate) {
+  __shared__ double red[SR_ZG][SR_COLS];
+  const int c = threadIdx.x % SR_COLS, zg = threadIdx.x / SR_COLS;
+  const int i = blockIdx.x * SR_COLS + c;
+  double t = 0.0;
+  if (i < n)
+    for (int z = zg; z < splits; z += SR_ZG) t += (double)part[(size_t)z * n + i];
+  red[zg][c] = t;
+  __syncthreads();
+  if (zg == 0 && i < n) {
+#pragma unroll
+    for (int g = 1; g < SR_ZG; ++g) t += red[g][c];
+    out[i] = accumulate ? out[i] + (float)t : (float)t;
+  }
+}
+
 int launch_split_reduce(const float* part, int splits, int rows, int cols, float* out, int ld, int accumulate,
                         hipStream_t s) {
   const size_t n = (size_t)rows * cols;
+  if (ld == cols && n <= 16384 && splits >= 2 * SR_ZG) {
+    hipLaunchKernelGGL(k_split_reduce_narrow, dim3((unsigned)cdiv((int64_t)n, SR_COLS)), dim3(SR_COLS * SR_ZG), 0, s,
+                       part, splits, (int)n, out, accumulate);
+    RLKS_LAUNCHED();
+    return RLKS_OK;
+  }
   const unsigned blocks = (unsigned)std::min<size_t>(4096, (n + 255) / 256);
   hipLaunchKernelGGL(k_split_reduce, dim3(blocks), dim3(256), 0, s, part, splits, rows, cols, out, ld, accumulate);
   RLKS_LAUNCHED();

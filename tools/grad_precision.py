@@ -99,12 +99,13 @@ def run_case(path, rows, D, H, A, seed_off=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="the small cases only")
+    ap.add_argument("--path", choices=["sf16", "wide"], default=None, help="one path's cases only")
     ap.add_argument("--json", default=None)
     ap.add_argument("--seeds", type=int, default=1)
     args = ap.parse_args()
     res = {"lib": os.environ.get("RLKS_LIB", "librlks.so"), "cases": []}
     for case in CASES:
-        if args.quick and case[1] > 4096:
+        if (args.quick and case[1] > 4096) or (args.path and case[0] != args.path):
             continue
         for so in range(args.seeds):
             recs = run_case(*case, seed_off=so)

@@ -10,6 +10,6 @@ for L in "$@"; do
 import csv,glob
 f=glob.glob("$O/$L/**/w_kernel_stats.csv", recursive=True)[0]
 print("$L")
-for r in list(csv.DictReader(open(f)))[:9]: print("  ", r["Name"][:58], r["Calls"], round(float(r["AverageNs"])/1e3,1))
+for r in list(csv.DictReader(open(f)))[:18]: print("  ", r["Name"][:58], r["Calls"], round(float(r["AverageNs"])/1e3,1), round(float(r["TotalDurationNs"])/1e6,3))
 PY
 done
