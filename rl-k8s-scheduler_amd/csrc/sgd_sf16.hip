@@ -61,25 +61,47 @@ __device__ __forceinline__ void split1(float x, _Float16& hi, _Float16& lo) {
   hi = (_Float16)x;
   lo = (_Float16)(x - (float)hi);
 }
+// the same for a pair, packed: hi = f16(x) by v_cvt_pk_f16_f32 (round to nearest even), lo = f16(x -
+// hi) by v_fma_mix{lo,hi}_f16, which forms x - hi exactly and rounds once: the same bits as split1's
+// cvt / cvt back / sub / cvt, in 3 instructions a pair instead of ~6 (tools/micro/mix_split.hip
+// compares the two on 4M random pairs on the GPU: identical)
+typedef _Float16 hf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2(float x0, float x1, unsigned& hi, unsigned& lo) {
+  const hf2 h = {(_Float16)x0, (_Float16)x1};
+  hi = __builtin_bit_cast(unsigned, h);
+  unsigned l;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(l)
+      : "v"(x0), "v"(hi), "v"(x1));
+  lo = l;
+}
+// 8 values -> (hi, lo) fragments
+__device__ __forceinline__ void split8v(const float (&x)[8], h8& hi, h8& lo) {
+  v4u h, l;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned a, b;
+    split2(x[2 * q], x[2 * q + 1], a, b);
+    h[q] = a;
+    l[q] = b;
+  }
+  hi = __builtin_bit_cast(h8, h);
+  lo = __builtin_bit_cast(h8, l);
+}
 // elements [o, o + 8) of v, times s
 template <int N>
 __device__ __forceinline__ void split8(const float (&v)[N], int o, float s, h8& hi, h8& lo) {
+  float x[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    _Float16 a, b;
-    split1(v[o + j] * s, a, b);
-    hi[j] = a;
-    lo[j] = b;
-  }
+  for (int j = 0; j < 8; ++j) x[j] = v[o + j] * s;
+  split8v(x, hi, lo);
 }
 __device__ __forceinline__ void split16(const f32x16& v, int o, float s, h8& hi, h8& lo) {
+  float x[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    _Float16 a, b;
-    split1(v[o + j] * s, a, b);
-    hi[j] = a;
-    lo[j] = b;
-  }
+  for (int j = 0; j < 8; ++j) x[j] = v[o + j] * s;
+  split8v(x, hi, lo);
 }
 
 // exponent e with mx 2^e in [2^14, 2^15); 0 for mx = 0 / non-finite
@@ -381,6 +403,7 @@ __device__ __forceinline__ void sf_loss(const SfArgs& g, const float (&out)[A_],
 __device__ unsigned long long g_fa_stamps[2][8192][8];
 #define FA_STAMP(i) \
   if (l == 0 && tile < 8192) g_fa_stamps[NET][tile][i] = __builtin_amdgcn_s_memtime()
+
 #define FA_HWID()                                                                                   \
   if (l == 0 && tile < 8192)                                                                        \
   g_fa_stamps[NET][tile][7] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |       \
@@ -466,6 +489,22 @@ __device__ __forceinline__ void w1_stage(const SfNet& N, _Float16* sW1, int tid)
     *reinterpret_cast<v4u*>(sW1 + arr * HID * KD + w1_off<KD>(k, q)) = v;
   }
 }
+// the same copy as w1_stage through the LDS DMA (global_load_lds, 1 KB per wave instruction): no
+// register round trip, so it is in flight beside the W2 chunk and the X rows (F1a's prologue)
+template <int KD, int W>
+__device__ __forceinline__ void w1_dma(const SfNet& N, _Float16* sW1, int w, int l) {
+  constexpr int PER_PLANE = HID * KD / 8 / 64;  // wave instructions per plane
+  static_assert((2 * PER_PLANE) % W == 0, "W1a planes split evenly over the waves");
+#pragma unroll
+  for (int i = 0; i < 2 * PER_PLANE / W; ++i) {
+    const int blk = (2 * PER_PLANE / W) * w + i, arr = blk / PER_PLANE, j = blk - arr * PER_PLANE;
+    const int pc = 64 * j + l, k = pc / (KD / 8), qs = pc - k * (KD / 8);
+    const int q = KD == 32 ? (qs ^ sw16(k)) : qs;
+    const _Float16* src = (arr ? N.w1l : N.w1h) + k * KD + 8 * q;
+    _Float16* dst = sW1 + arr * HID * KD + j * 512;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+}
 // W1a fragment of rows k = 16 kt + c, columns d = 8g + j: lanes with 8g >= KD read a duplicate
 // piece (finite; the Xa fragment is zero there)
 template <int KD>
@@ -506,6 +545,14 @@ __device__ __forceinline__ float row_sum16(float v) {
 
 // Xa = [X | 1 | 0] fragment of a 16-row tile: lane (g, c) holds row row0 + c, columns 8g .. 8g + 7,
 // scaled by the wave's power of two (returned: its exponent) times sgn (the tile's sign, below) and split
+__device__ __forceinline__ int x_split(const float (&xv)[8], h8& xh, h8& xl, float sgn) {
+  float xm = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) xm = fmaxf(xm, fabsf(xv[j]));
+  const int ex = sf_exp(wave_max(xm));
+  split8(xv, 0, sgn * pow2(ex), xh, xl);
+  return ex;
+}
 __device__ __forceinline__ int x_frag(const SfArgs& a, int row0, int c, int g, h8& xh, h8& xl, float sgn = 1.f) {
   float xv[8];
   xa_row8(a.x + (size_t)(row0 + c) * a.x_stride, 8 * g, a.D, a.x_stride, xv);
@@ -570,30 +617,47 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
 
   // w wave-uniform (readfirstlane): tile bases stay in SGPRs, stores use a 32-bit lane offset
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
+  // Prologue: every global load of the first group goes out before any result is used (the W2
+  // half-chunk and W1a planes by LDS DMA, the tile's X rows, b2 and W3 into registers), so the
+  // workgroup waits for one memory round trip instead of four in a row
   int tile = blockIdx.x * W + w;
   if (!dcheck(tile < g.M / 16, DC_SGD_TILE, tile)) tile = g.M / 16 - 1;
   const int row0 = tile * 16;
   FA_STAMP(0);
   FA_HWID();
-
   hc_dma<W>(N.w2ph, N.w2pl, 0, 0, sCh, w, l);
-  for (int i = tid; i < HID; i += NTHR) sB2[i] = N.b2[i] * SF_2LOG2E;  // H2 = tanh(Z2 + b2): exp2 argument
+  w1_dma<KD, W>(N, sW1, w, l);
+  float xv[8];
+  xa_row8(g.x + (size_t)(row0 + c) * g.x_stride, 8 * gq, g.D, g.x_stride, xv);
   __shared__ float s_w3m[W];  // per wave: max |W3 row| entry it staged (the dZ2 scale bound below)
   __shared__ double s_vx[W];  // value net: per wave, the f64 sum of its rows' v - vt (vf_row)
   {
+    constexpr int NW3 = (AH * HID + NTHR - 1) / NTHR;
+    const float b2v = tid < HID ? N.b2[tid] : 0.f;
+    float w3v[NW3], w3l[NW3];
+#pragma unroll
+    for (int j = 0; j < NW3; ++j) {
+      const int i = tid + j * NTHR;
+      w3v[j] = i < AH * HID ? N.w3[i] : 0.f;
+      w3l[j] = (NET == 0 && i < AH * HID) ? N.w3[(A_ - 1) * HID + (i & (HID - 1))] : 0.f;
+    }
+    if (tid < HID) sB2[tid] = b2v * SF_2LOG2E;  // H2 = tanh(Z2 + b2): exp2 argument
     float m3 = 0.f;
-    for (int i = tid; i < AH * HID; i += NTHR) {
-      const float v = NET == 0 ? N.w3[i] - N.w3[(A_ - 1) * HID + (i & (HID - 1))] : N.w3[i];
-      sW3[i] = v;
-      m3 = fmaxf(m3, fabsf(v));
+#pragma unroll
+    for (int j = 0; j < NW3; ++j) {
+      const int i = tid + j * NTHR;
+      if (i < AH * HID) {
+        const float v = w3v[j] - w3l[j];
+        sW3[i] = v;
+        m3 = fmaxf(m3, fabsf(v));
+      }
     }
     m3 = wave_max(m3);
     if (l == 0) s_w3m[w] = m3;
   }
-  w1_stage<KD, NTHR>(N, sW1, tid);
   h8 xh, xl;
   const float sgn = tile_sign(tile);
-  const int ex = x_frag(g, row0, c, gq, xh, xl, sgn);
+  const int ex = x_split(xv, xh, xl, sgn);
   const float k_z1 = sgn * N.sc[1] * pow2(-ex) * SF_2LOG2E;  // Z1 accumulator -> 2 log2(e) Z1
   const float h1s = sgn * SF_H1_SCALE;                        // H1 enters Z2's products as sgn 2^14 H1
   vm_drain();
@@ -729,7 +793,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   bnd = wave_max(bnd * w3m);
   const int edz = bnd > 0.f ? sf_exp(bnd) : 120;  // an all-zero tile: the largest exponent (F2 takes the min)
   {
-    const float sdz = sgn * pow2(edz);  // (handed over with the tile's sign)
+    const float sdz = sgn * pow2(edz + 2);  // (handed over with the tile's sign; x4: 1 - H2^2 = 4 r (1 - r))
 #pragma unroll
     for (int a = 0; a < AH; ++a) dl[a] *= sdz;
   }
@@ -748,7 +812,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float r = acc[nt][i];
-      acc[nt][i] = gs[i] * (4.f * fmaf(-r, r, r));  // (no cancellation where H2 saturates, unlike 1 - H2^2)
+      acc[nt][i] = gs[i] * fmaf(-r, r, r);  // (no cancellation where H2 saturates, unlike 1 - H2^2)
     }
     if constexpr (A_ > 4) asm volatile("" ::: "memory");
   }
@@ -757,13 +821,10 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       h8 hi, lo;
+      float x[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        _Float16 a, b;
-        split1(acc[2 * st + (j >> 2)][j & 3], a, b);
-        hi[j] = a;
-        lo[j] = b;
-      }
+      for (int j = 0; j < 8; ++j) x[j] = acc[2 * st + (j >> 2)][j & 3];
+      split8v(x, hi, lo);
       *reinterpret_cast<h8*>(dst + st * 1024) = hi;
       *reinterpret_cast<h8*>(dst + st * 1024 + 512) = lo;
     }
@@ -1183,14 +1244,13 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float hs = i < 2 ? hs0 : hs1;
-      h4 hh, hl;
+      float x[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        _Float16 a, b;
-        split1(fmaf(-2.f * hs, tanh_r(z[4 * i + j] * k_z1), hs), a, b);
-        hh[j] = a;
-        hl[j] = b;
-      }
+      for (int j = 0; j < 4; ++j) x[j] = fmaf(-2.f * hs, tanh_r(z[4 * i + j] * k_z1), hs);
+      unsigned a0, b0, a1, b1;
+      split2(x[0], x[1], a0, b0);
+      split2(x[2], x[3], a1, b1);
+      const h4 hh = __builtin_bit_cast(h4, make_uint2(a0, a1)), hl = __builtin_bit_cast(h4, make_uint2(b0, b1));
       const int off = hoff + (i >> 1) * HID * 16 + 4 * (i & 1);
       *reinterpret_cast<h4*>(img + off) = hh;
       *reinterpret_cast<h4*>(img + off + F2_BPLANE) = hl;
