@@ -109,15 +109,17 @@ ROOFLINE_KERNELS = ("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1", "k_sf_fw
 
 
 def algo_bytes_per_launch(name, rows, D=6, H=256, A=2):
-    """compulsory HBM bytes of one launch of a split-fp16 SGD kernel over `rows` minibatch rows
-    (DESIGN.md "Algorithmic bytes"): each net's pass reads the row's record (fp32, mb_stride
-    floats; F2 only its obs columns), F1a writes both nets' dZ2 (fp32, 2 x H x 4 B a row), F1b
-    and F2 read it back.  Weights (< 0.5 MB) and the per-block weight-gradient partials are not
-    counted: they are the overhead traffic_over_algorithmic exposes."""
+    """algorithmic HBM bytes of one launch of a split-fp16 SGD kernel over `rows` minibatch rows
+    (DESIGN.md "Algorithmic bytes"): only the step's own inputs the kernel must read, each once --
+    F1a the row's record (fp32, mb_stride floats; both nets use the same bytes), F1b and F2 its obs
+    columns (D floats).  The dZ2 hand-off F1a writes and F1b / F2 read back, the per-block weight-
+    gradient partials and the weights (< 0.5 MB) are not algorithmic: they are the overhead
+    traffic_over_algorithmic exposes."""
     rec = (D + A + 4 + 3) // 4 * 4 * 4
-    dz = 2 * H * 4
-    per_row = {"k_sf_fwd": 2 * rec + dz, "k_sf_bwd": 2 * rec + dz, "k_sf_dw2": 2 * D * 4 + dz}.get(name)
+    per_row = {"k_sf_fwd": rec, "k_sf_bwd": 4 * D, "k_sf_dw2": 4 * D}.get(name)
     return None if per_row is None else per_row * rows
+
+
 ENV_BYTES_PER_STEP = 4 + 8 + 24 + 4 + 1  # action, step r/w, obs, reward, done (SURVEY §8d)
 # what the 2-cloud step kernel must move per env-step: action 4, step r/w 8, episode 4 (Philox
 # counter), obs 24, reward 8 (the reference's float64), terminated 1

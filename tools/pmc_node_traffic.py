@@ -3,27 +3,33 @@
 tools/node_step_time.py, gfx950 correction FETCH x 2) to profiles/pmc_traffic.json (key k_node_step:
 the c3 stationary-churn case bench.py reports traffic for).
 
-usage: pmc_node_traffic.py <fetch counter csv> <write counter csv> <source> [pmc_traffic.json]"""
+usage: pmc_node_traffic.py <fetch counter csv> <write counter csv> <source> [pmc_traffic.json] [--first-half]"""
 import collections
 import csv
 import json
 import sys
 
 
-def per_kernel(path, counter):
+def per_kernel(path, counter, first_half=False):
+    """per-launch average per kernel name; first_half: only the earlier half of the dispatches (a
+    node_step_time.py run over both legs runs the stationary one first, under the same kernel name)"""
     d = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
+    for r in rows:
         if r["Counter_Name"] == counter and "k_node_step" in r["Kernel_Name"]:
             d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    if first_half:
+        d = {k: v[: max(1, len(v) // 2)] for k, v in d.items()}
     return {k: sum(v) / len(v) for k, v in d.items()}
 
 
 def main():
-    fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE"), per_kernel(sys.argv[2], "WRITE_SIZE")
+    half = "--first-half" in sys.argv
+    sys.argv = [a for a in sys.argv if a != "--first-half"]
+    fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE", half), per_kernel(sys.argv[2], "WRITE_SIZE", half)
     dst = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
     out = json.load(open(dst))
-    # the stationary-churn launch: the survival table read through L2 (the <false, ...> instance)
-    keep = [k for k in fetch if "<false" in k] or list(fetch)
+    keep = list(fetch)
     for k in keep[:1]:
         f = fetch[k]
         key = "k_node_step"
