@@ -63,10 +63,12 @@ int launch_split_planes(const float* x, int rows, int cols, int ld, const unsign
 // split count for an M x N x K weight-gradient GEMM (enough workgroups to fill 256 CUs)
 int gemm_splits(int M, int N, int K);
 int launch_absmax(const float* x, int rows, int cols, int ld, unsigned* slot, hipStream_t s);
-// column sums out[c] (+)= sum_r x[r][c]; with `part` ([colsum_splits(rows)][cols] floats) the rows
-// are split over workgroups and reduced in a fixed order
+// column sums out[c] (+)= sum_r x[r][c] (with wt: sum_r wt[r] x[r][c]), in f64; with `part`
+// ([2][colsum_splits(rows)][cols] floats: hi, lo planes) the rows are split over workgroups and
+// reduced in a fixed order
 int colsum_splits(int rows);
 int launch_colsum(const float* x, int rows, int cols, int ld, float* out, int accumulate, float* part,
-                  hipStream_t s);
+                  hipStream_t s,
+                  const float* wt = nullptr);
 
 }  // namespace rlks

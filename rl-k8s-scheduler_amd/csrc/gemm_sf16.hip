@@ -320,8 +320,10 @@ __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int
 // column sums of a [rows][cols] matrix over the row range of layer blockIdx.y (rows_per rows):
 // out[y * cols + c] (or, with one layer, out[c] (+)=) = sum_r x[r][c]; one thread per column, f64.
 // Several layers: each layer's f64 sum as hi (plane y) + lo (plane gridDim.y + y), both reduced
+// With weights wt (one per row): sum_r wt[r] x[r][c], each product formed in f64 (a column-weighted
+// sum: the value head's dW3 = dout^T H2 at one output, memory-bound, wide_mlp.hip).
 __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ x, int rows, int cols, int ld, int rows_per,
-                                                float* __restrict__ out, int accumulate) {
+                                                float* __restrict__ out, int accumulate, const float* __restrict__ wt) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
   const int r0 = blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
@@ -329,13 +331,16 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ x, int
   int rr = r0;
   // 8 independent loads in flight per thread, summed in row order (same result as the plain loop)
   for (; rr + 8 <= r1; rr += 8) {
-    float v[8];
+    float v[8], u[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = x[(size_t)(rr + j) * ld + c];
+    for (int j = 0; j < 8; ++j) {
+      v[j] = x[(size_t)(rr + j) * ld + c];
+      u[j] = wt ? wt[rr + j] : 1.f;
+    }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += (double)v[j];
+    for (int j = 0; j < 8; ++j) s += (double)u[j] * (double)v[j];
   }
-  for (; rr < r1; ++rr) s += (double)x[(size_t)rr * ld + c];
+  for (; rr < r1; ++rr) s += (double)(wt ? wt[rr] : 1.f) * (double)x[(size_t)rr * ld + c];
   if (gridDim.y > 1) {
     const float hi = (float)s;
     out[(size_t)blockIdx.y * cols + c] = hi;
@@ -458,11 +463,11 @@ int launch_absmax(const float* x, int rows, int cols, int ld, unsigned* slot, hi
 int colsum_splits(int rows) { return std::min(128, std::max(1, rows / 512)); }
 
 int launch_colsum(const float* x, int rows, int cols, int ld, float* out, int accumulate, float* part,
-                  hipStream_t s) {
+                  hipStream_t s, const float* wt) {
   const int sp = part ? colsum_splits(rows) : 1;
   const int rows_per = cdiv(rows, sp);
   hipLaunchKernelGGL(k_colsum, dim3(cdiv(cols, 256), sp), dim3(256), 0, s, x, rows, cols, ld, rows_per,
-                     sp > 1 ? part : out, accumulate);
+                     sp > 1 ? part : out, accumulate, wt);
   RLKS_LAUNCHED();
   if (sp == 1) return RLKS_OK;
   return launch_split_reduce(part, 2 * sp, 1, cols, out, cols, accumulate, s);

@@ -15,7 +15,7 @@ struct WideNet {
 };
 struct WideWs {
   WideNet n[2];
-  float *dza, *dzb;  // [M][H] dZ2 / dZ1
+  float* dzb;  // [M][H] dZ1 (dZ2 goes straight to the dzh / dzl planes)
   _Float16 *dzh, *dzl;  // dZ2 planes [M][H]
   _Float16 *xh, *xl;    // X planes [M][D] (obs_dim D a multiple of 32)
   double* rew64;     // [M] env-step scratch (rollout)

@@ -25,7 +25,8 @@ namespace rlks {
 
 constexpr int LOSS_ROWS = 256;  // rows per loss block (stats partials)
 
-enum { SL_X = 0, SL_W1, SL_W2, SL_W3, SL_H1, SL_H2, SL_DOUT, SL_DZ2, SL_DZ1, SL_N = 16 };
+using h8 = __attribute__((ext_vector_type(8))) _Float16;
+enum { SL_X = 0, SL_W1, SL_W2, SL_W3, SL_H1, SL_H2, SL_DOUT, SL_DZ2, SL_DZ1, SL_DSUM, SL_N = 16 };  // SL_DSUM: max_m sum_a |dout|
 
 WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
   WideWs w{};
@@ -53,7 +54,6 @@ WideWs wide_ws_layout(int D, int H, int A, int M, char* base) {
     n.slots = (unsigned*)take(4 * SL_N);
     n.part_stat = (float*)take(4LL * w.blocks * 4);
   }
-  w.dza = (float*)take(4LL * M * H);
   w.dzb = (float*)take(4LL * M * H);
   w.dzh = (_Float16*)take(2LL * Mp * H);
   w.dzl = (_Float16*)take(2LL * Mp * H);
@@ -147,10 +147,12 @@ __device__ __forceinline__ double wave_max_d(double v) {
 __global__ __launch_bounds__(64 * LOSS_PI_WAVES) void k_wide_loss_pi(const float* __restrict__ out, const float* __restrict__ x,
                                                           int stride, int M, int D, int A, rlks_ppo_coeffs co,
                                                           const float* __restrict__ dyn, float* __restrict__ dout,
-                                                          float* __restrict__ part_stat, unsigned* __restrict__ dmax) {
+                                                          float* __restrict__ part_stat, unsigned* __restrict__ dmax,
+                                                          unsigned* __restrict__ dsum) {
   constexpr int RPW = LOSS_ROWS / LOSS_PI_WAVES;  // rows per wave
   __shared__ double red[3][LOSS_PI_WAVES];
-  __shared__ float redm[LOSS_PI_WAVES];
+  __shared__ float redm[LOSS_PI_WAVES], reds[LOSS_PI_WAVES];
+  float mx_s = 0.f;  // max over the wave's rows of sum_a |dout|: k_wide_dz2's split bound
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const bool on = l < A;
   const double inv_count = dyn[RLKS_DYN_INV_COUNT], klc = dyn[RLKS_DYN_KL_COEFF];
@@ -180,14 +182,16 @@ __global__ __launch_bounds__(64 * LOSS_PI_WAVES) void k_wide_loss_pi(const float
     const double w1 = s1 < s2 ? 1.0 : (s1 == s2 ? 0.5 : 0.0);
     const double inr = (ratio >= lo_c && ratio <= hi_c) ? 1.0 : 0.0;
     const double dr = -adv * (w1 + (1.0 - w1) * inr) * ratio;
+    float df = 0.f;
     if (on) {
       double d = dr * ((l == act ? 1.0 : 0.0) - p);
       d += klc * (p - po);
       d += ent_c * p * (lp + ent);
-      const float df = (float)(d * inv_count);
+      df = (float)(d * inv_count);
       dout[(size_t)m * A + l] = df;
       mx_d = fmaxf(mx_d, fabsf(df));
     }
+    mx_s = fmaxf(mx_s, wave_sum(fabsf(df)));
     st0 -= fmin(s1, s2);
     st2 += kl;
     st3 += ent;
@@ -198,12 +202,17 @@ __global__ __launch_bounds__(64 * LOSS_PI_WAVES) void k_wide_loss_pi(const float
     red[1][w] = st2;
     red[2][w] = st3;
     redm[w] = mx_d;
+    reds[w] = mx_s;
   }
   __syncthreads();
   if (threadIdx.x == 64) {  // one atomic per block (single-address atomics serialise at their L2 channel)
-    float m = 0.f;
-    for (int j = 0; j < LOSS_PI_WAVES; ++j) m = fmaxf(m, redm[j]);
+    float m = 0.f, ms = 0.f;
+    for (int j = 0; j < LOSS_PI_WAVES; ++j) {
+      m = fmaxf(m, redm[j]);
+      ms = fmaxf(ms, reds[j]);
+    }
     atomicMax(dmax, __float_as_uint(m));
+    atomicMax(dsum, __float_as_uint(ms));
   }
   if (threadIdx.x < 4) {
     const int k = threadIdx.x;
@@ -267,15 +276,32 @@ __global__ void k_wide_sample(EnvView v, const float* __restrict__ logits, int A
 // 1 - H2^2 as one fma (a single rounding where H2 saturates)
 constexpr int DZ_ROWS = 64, DZ_COLS = 256, DZ_K = 32, DZ_RT = 8;  // DZ_RT row tiles per block
 __global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout, const float* __restrict__ w3,
-                                                  const float* __restrict__ h2, float* __restrict__ dz, int M, int H,
-                                                  int K, unsigned* __restrict__ cmax_slot, float* __restrict__ part_db2) {
+                                                  const float* __restrict__ h2, _Float16* __restrict__ dzh,
+                                                  _Float16* __restrict__ dzl, int M, int H, int K,
+                                                  const unsigned* __restrict__ dsum_slot,
+                                                  const unsigned* __restrict__ w3_slot, unsigned* __restrict__ cmax_slot,
+                                                  float* __restrict__ part_db2) {
+  // dZ2's planes scale from the bound |dZ2| <= max_m sum_a |dout[m][a]| max |W3| (|1 - H2^2| <= 1),
+  // known before any dZ2 exists, so the planes are written here (no fp32 dZ2 round trip through HBM
+  // and a split pass); the bound goes to cmax_slot for the GEMMs that read the planes (gemm_ps.hip
+  // ps_exp: the same exponent)
+  const float bnd = __uint_as_float(*dsum_slot) * __uint_as_float(*w3_slot);
+  float ds;
+  {
+    int e = 0;
+    if (bnd > 0.f && bnd <= 3.4e38f) {
+      (void)frexpf(bnd, &e);
+      e = min(max(15 - e, -120), 120);
+    }
+    ds = ldexpf(1.f, e);
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *cmax_slot = __float_as_uint(bnd);
   __shared__ __attribute__((aligned(16))) float sA[DZ_K][DZ_ROWS + 4];  // dout^T chunk (padded: the transposing stores)
   __shared__ __attribute__((aligned(16))) float sB[DZ_K][DZ_COLS];      // W3 chunk; at the end the db2 sums
   const int tid = threadIdx.x, cg = tid & 31, rg = tid >> 5;
   const int n0 = blockIdx.x * DZ_COLS;
   int n = n0 + 8 * cg;  // this thread's 8 columns (H % 8 == 0: host check)
   if (!dcheck(n + 8 <= H || n0 + DZ_COLS > H, DC_WIDE_COL, n)) n = H - 8;
-  float mx = 0.f;  // max |dZ2|
   double cs[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // db2: this thread's column sums (f64)
   for (int rt = 0; rt < DZ_RT; ++rt) {
     const int m0 = (blockIdx.y * DZ_RT + rt) * DZ_ROWS;
@@ -318,29 +344,26 @@ __global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout
         const float4* hp = reinterpret_cast<const float4*>(h2 + (size_t)m * H + n);
         const float4 g0 = hp[0], g1 = hp[1];
         const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-        float o[8];
+        h8 hv, lv;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          o[j] = acc[i][j] * fmaf(-gv[j], gv[j], 1.f);
-          mx = fmaxf(mx, fabsf(o[j]));
-          cs[j] += (double)o[j];
+          const float o = acc[i][j] * fmaf(-gv[j], gv[j], 1.f);
+          cs[j] += (double)o;
+          const _Float16 t = (_Float16)(o * ds);
+          hv[j] = t;
+          lv[j] = (_Float16)(o * ds - (float)t);
         }
-        float4* dp = reinterpret_cast<float4*>(dz + (size_t)m * H + n);
-        dp[0] = make_float4(o[0], o[1], o[2], o[3]);
-        dp[1] = make_float4(o[4], o[5], o[6], o[7]);
+        *reinterpret_cast<h8*>(dzh + (size_t)m * H + n) = hv;
+        *reinterpret_cast<h8*>(dzl + (size_t)m * H + n) = lv;
       }
     }
   }
-  mx = wave_max(mx);
-  __shared__ float red[4];
-  if ((tid & 63) == 0) red[tid >> 6] = mx;
   // db2 partial of the block's rows: the 8 row groups' column sums combined in a fixed order
   __syncthreads();  // (every thread is past its last read of sB)
   double* sC = reinterpret_cast<double*>(&sB[0][0]);  // [8 rg][256] (16 KB of sB's 32)
 #pragma unroll
   for (int j = 0; j < 8; ++j) sC[rg * DZ_COLS + 8 * cg + j] = cs[j];
   __syncthreads();
-  if (tid == 0) atomicMax(cmax_slot, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
   if (n0 + tid < H) {  // the block's column sum as an exact-ish hi + lo pair: planes y and gridDim.y + y
     double t = 0.0;
 #pragma unroll
@@ -348,6 +371,36 @@ __global__ __launch_bounds__(256) void k_wide_dz2(const float* __restrict__ dout
     const float hi = (float)t;
     part_db2[(size_t)blockIdx.y * H + n0 + tid] = hi;
     part_db2[(size_t)(gridDim.y + blockIdx.y) * H + n0 + tid] = (float)(t - (double)hi);
+  }
+}
+
+// The value net's head out[m] = b3 + sum_n H2[m][n] W3[n] (one output: a GEMV, HBM-bound on H2's
+// M x H floats), fp32 FMAs on the unsplit operands; one wave per row at a time, VH_RPW rows a wave,
+// the lane partials added by a fixed-order wave reduction.  (As a split GEMM with N = 1 on 128-wide
+// tiles it took ~250 µs at c5 for 0.5 GB.)
+constexpr int VH_RPW = 8;
+__global__ __launch_bounds__(256) void k_wide_vhead(const float* __restrict__ h2, const float* __restrict__ w3,
+                                                    const float* __restrict__ b3, float* __restrict__ out, int M, int H) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool v4 = (H & 255) == 0;
+  for (int i = 0; i < VH_RPW; ++i) {
+    const int m = (blockIdx.x * 4 + w) * VH_RPW + i;
+    if (m >= M) break;
+    const float* r = h2 + (size_t)m * H;
+    float acc = 0.f;
+    if (v4) {
+      for (int n = 4 * l; n < H; n += 256) {
+        const float4 a = *reinterpret_cast<const float4*>(r + n), b = *reinterpret_cast<const float4*>(w3 + n);
+        acc = fmaf(a.x, b.x, acc);
+        acc = fmaf(a.y, b.y, acc);
+        acc = fmaf(a.z, b.z, acc);
+        acc = fmaf(a.w, b.w, acc);
+      }
+    } else {
+      for (int n = l; n < H; n += 64) acc = fmaf(r[n], w3[n], acc);
+    }
+    acc = wave_sum_f(acc);
+    if (l == 0) out[m] = b3[0] + acc;
   }
 }
 
@@ -423,6 +476,11 @@ int forward_net(const rlks_mlp_desc* d, const Net& P, const WideNet& n, const fl
     a.M = M; a.N = H; a.K = H; a.epi = PS_TANH_BIAS; a.C = n.h2; a.ldc = H; a.bias = P.b2; a.cmax = sl + SL_H2;
     if (int rc = launch_gemm_ps(a, s)) return rc;
   }
+  if (An == 1) {
+    hipLaunchKernelGGL(k_wide_vhead, dim3(cdiv(M, 4 * VH_RPW)), dim3(256), 0, s, n.h2, P.w3, P.b3, n.out, M, H);
+    RLKS_LAUNCHED();
+    return RLKS_OK;
+  }
   return gemm(n.h2, H, 0, P.w3, H, 1, n.out, An, M, An, H, GEMM_BIAS, P.b3, nullptr, 0, sl + SL_H2, sl + SL_W3,
               nullptr, s);
 }
@@ -472,15 +530,18 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     if (int rc = forward_net(d, P, n, mb, stride, M, net, w.xh, w.xl, xsl, net == 1, s)) return rc;
     if (net == 0)
       hipLaunchKernelGGL(k_wide_loss_pi, dim3(w.blocks), dim3(64 * LOSS_PI_WAVES), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
-                         n.dout, n.part_stat, sl + SL_DOUT);
+                         n.dout, n.part_stat, sl + SL_DOUT, sl + SL_DSUM);
     else
       hipLaunchKernelGGL(k_wide_loss_vf, dim3(w.blocks), dim3(LOSS_ROWS), 0, s, n.out, mb, stride, M, D, A, *co, dyn,
                          n.dout, n.part_stat, sl + SL_DOUT);
     RLKS_LAUNCHED();
-    // head: dW3 = dout^T H2, db3 = colsum(dout)
-    if (int rc = gemm(n.dout, An, 1, n.h2, H, 0, g + o[4], H, An, H, M, GEMM_STORE, nullptr, nullptr, 0,
-                      sl + SL_DOUT, sl + SL_H2, nullptr, s, w.part))
+    // head: dW3 = dout^T H2 (value net: a dout-weighted column sum of H2, HBM-bound), db3 = colsum(dout)
+    if (An == 1) {
+      if (int rc = launch_colsum(n.h2, M, H, H, g + o[4], 0, w.part, s, n.dout)) return rc;
+    } else if (int rc = gemm(n.dout, An, 1, n.h2, H, 0, g + o[4], H, An, H, M, GEMM_STORE, nullptr, nullptr, 0,
+                             sl + SL_DOUT, sl + SL_H2, nullptr, s, w.part)) {
       return rc;
+    }
     if (net == 0) {
       if (int rc = launch_colsum(n.dout, M, An, An, g + o[5], 0, w.part, s)) return rc;
     } else {
@@ -490,12 +551,12 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
     // dZ2 = (dout W3) (1 - H2^2); dW2 = dZ2^T H1; db2
     RLKS_REQUIRE(H % 8 == 0, RLKS_ERR_UNSUPPORTED, "wide path: hidden width must be a multiple of 8");
     const int dz_blocks = (int)cdiv(M, DZ_ROWS * DZ_RT);
-    hipLaunchKernelGGL(k_wide_dz2, dim3(cdiv(H, DZ_COLS), dz_blocks), dim3(256), 0, s, n.dout, P.w3, n.h2, w.dza, M, H,
-                       An, sl + SL_DZ2, w.part);
+    // (the value net's sum_a |dout| is |dout|: its max slot)
+    hipLaunchKernelGGL(k_wide_dz2, dim3(cdiv(H, DZ_COLS), dz_blocks), dim3(256), 0, s, n.dout, P.w3, n.h2, w.dzh, w.dzl,
+                       M, H, An, sl + (net == 0 ? SL_DSUM : SL_DOUT), sl + SL_W3, sl + SL_DZ2, w.part);
     RLKS_LAUNCHED();
     // db2 from the dZ2 kernel's per-block column sums (before dW2's split-K reuses the partial buffer)
     if (int rc = launch_split_reduce(w.part, 2 * dz_blocks, 1, H, g + o[3], H, 0, s)) return rc;  // hi + lo planes
-    if (int rc = launch_split_planes(w.dza, M, H, H, sl + SL_DZ2, 0, w.dzh, w.dzl, H, s)) return rc;
     {  // dW2[n][k] = sum_m dZ2[m][n] H1[m][k]: both operands K-major planes, split over the rows
       PsArgs a{};
       a.a = ps_op(w.dzh, w.dzl, H, 1, H, sl + SL_DZ2);
