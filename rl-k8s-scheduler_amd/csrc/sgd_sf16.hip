@@ -604,7 +604,7 @@ constexpr int f1b_lds_bytes() {
 // which is the same loss and gradient with A - 1 head rows instead of A (at 2 actions: half of the
 // head, of dZ2's products and of the dW3 reduce-scatter, the epilogue's largest part).  AH: head rows.
 template <int A_, int NET, int KD, int W>
-__device__ __forceinline__ void f1a_body(const SfArgs& g) {
+__device__ __forceinline__ void f1a_body(const SfArgs& g, int grp) {
   constexpr int NTHR = 64 * W;
   constexpr int AH = NET == 0 ? A_ - 1 : 1;
   const SfNet& N = g.n[NET];
@@ -620,7 +620,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   // Prologue: every global load of the first group goes out before any result is used (the W2
   // half-chunk and W1a planes by LDS DMA, the tile's X rows, b2 and W3 into registers), so the
   // workgroup waits for one memory round trip instead of four in a row
-  int tile = blockIdx.x * W + w;
+  int tile = grp * W + w;
   if (!dcheck(tile < g.M / 16, DC_SGD_TILE, tile)) tile = g.M / 16 - 1;
   const int row0 = tile * 16;
   FA_STAMP(0);
@@ -836,7 +836,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   FA_STAMP(6);
   // ---- workgroup sums (fixed wave order) -> this block's partials
   __syncthreads();
-  const int blk = blockIdx.x;
+  const int blk = grp;
   for (int e = tid; e < A_ * HID; e += NTHR) {
     const int a = e >> 8, n = e & (HID - 1);
     float s = 0.f;
@@ -870,17 +870,33 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g) {
   }
 }
 
+// workgroup -> (net, tile group) for F1a / F1b launched as one row of G x nets workgroups.  Both
+// nets in one launch: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one), so the
+// nets alternate in runs of 8 -- each XCD, and so each CU, gets workgroups of both nets, whose
+// different epilogue lengths keep a CU's co-resident workgroups from running their epilogues in
+// phase (the policy net's is longer).  G not a multiple of 8, or !MIX: net-major.  Measured
+// (profiles/r05_mix): c4 F1a 72.7 -> 69.9 µs, F1b 62.4 -> 58.2; at 8 actions F1b 76.5 -> 71.3 but
+// F1a 91.8 -> 101.7, so F1a keeps the net-major order above 4 actions.
+template <int W, bool MIX>
+__device__ __forceinline__ int2 f1_net_group(const SfArgs& g) {
+  const int G = g.M / (16 * W), b = blockIdx.x;
+  if ((int)gridDim.x <= G) return make_int2(0, b);
+  if (MIX && (G & 7) == 0) return make_int2((b >> 3) & 1, ((b >> 4) << 3) | (b & 7));
+  return make_int2(b / G, b % G);
+}
+
 template <int A_, int KD, int W>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_fwd(SfArgs g) {
-  if (blockIdx.y + g.net0 == 0) f1a_body<A_, 0, KD, W>(g);
-  else f1a_body<1, 1, KD, W>(g);
+  const int2 ng = f1_net_group<W, (A_ <= 4)>(g);
+  if (ng.x + g.net0 == 0) f1a_body<A_, 0, KD, W>(g, ng.y);
+  else f1a_body<1, 1, KD, W>(g, ng.y);
 }
 
 // F1a's dW3 / db3 / stats partials per net: one per F1 workgroup
 int sf_f1a_parts(int M, int A) { return M / (16 * SF_F1_W); }
 
 template <int NET, int KD, int ND, int W>
-__device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1 (rows d of dW1a^T)
+__device__ __forceinline__ void f1b_body(const SfArgs& g, int grp) {  // ND = obs_dim + 1 (rows d of dW1a^T)
   constexpr int NTHR = 64 * W;
   constexpr int DT = KD / 16;                      // 16-row d-tiles of dW1a^T
   constexpr int SLOT = W * 16 * 16 * DT;           // floats per k-tile: [W][16 k][16 DT d]
@@ -894,9 +910,9 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1
 
   // w wave-uniform (readfirstlane): tile bases stay in SGPRs, stores use a 32-bit lane offset
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
-  int tile = blockIdx.x * W + w;
+  int tile = grp * W + w;
   if (!dcheck(tile < g.M / 16, DC_SGD_TILE, tile)) tile = g.M / 16 - 1;
-  const int row0 = tile * 16, blk = blockIdx.x;
+  const int row0 = tile * 16, blk = grp;
   const int D = g.D, stride = g.x_stride;
 
   hc_dma<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
@@ -1023,8 +1039,9 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g) {  // ND = obs_dim + 1
 
 template <int KD, int ND, int W>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_bwd(SfArgs g) {
-  if (blockIdx.y + g.net0 == 0) f1b_body<0, KD, ND, W>(g);
-  else f1b_body<1, KD, ND, W>(g);
+  const int2 ng = f1_net_group<W, true>(g);
+  if (ng.x + g.net0 == 0) f1b_body<0, KD, ND, W>(g, ng.y);
+  else f1b_body<1, KD, ND, W>(g, ng.y);
 }
 
 // ----------------------------------------------------------------------------- F2
@@ -1499,7 +1516,7 @@ template <int A_, int KD>
 static int launch_f1_net(SfArgs a, int net0, int nets, hipStream_t s, int halves) {
   constexpr int W = SF_F1_W;
   a.net0 = net0;
-  const dim3 grid(a.M / (16 * W), nets);
+  const dim3 grid(a.M / (16 * W) * nets);  // (f1_net_group)
   if (halves & 1) {  // pi's LDS (A_ >= 1) covers the value net's
     hipLaunchKernelGGL((k_sf_fwd<A_, KD, W>), grid, dim3(64 * W), (f1a_lds_bytes<A_, KD, W>()), s, a);
     RLKS_LAUNCHED();
