@@ -139,7 +139,8 @@ def parse():
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--precision", default="auto", choices=("auto", "sf16", "fp32"), help="SGD-step matrix arithmetic")
+    ap.add_argument("--precision", default="auto", choices=("auto", "sf16", "fp32", "f16"),
+                    help="SGD-step matrix arithmetic (f16: one-product throughput mode, below fp32: a secondary line)")
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                     help="weak: per-GPU work fixed as N grows; strong: whole-job work fixed (8x the per-GPU config)")
     ap.add_argument("--dry-run", action="store_true",
@@ -255,7 +256,7 @@ def kernel_timing(algo, torch, config="c2", reps=20):
     if algo.precision == "wide":
         phases = ()  # generic-width path: one sequence of GEMM launches, timed as a whole below
         peak, peak_name = SF16_PEAK_TFLOPS, "frac_sf16_mfma"
-    elif algo.precision == "sf16":
+    elif algo.precision in ("sf16", "f16"):
         phase(_lib.RLKS_PHASE_ALL)()  # weight splits + dZ2 in place for the per-phase timings
         # F1 = k_sf_fwd (F1a) + k_sf_bwd (F1b): each timed alone, and the pair
         f1 = (("k_sf_fwd", _lib.RLKS_PHASE_F1A), ("k_sf_bwd", _lib.RLKS_PHASE_F1B),
@@ -446,7 +447,7 @@ def cpu_threads() -> int:
     return max(1, min(n, int(omp))) if omp.isdigit() else max(1, n)
 
 
-def mfma_calibration(torch, sf16_tflops):
+def mfma_calibration(torch, sf16_tflops, products=3):
     """what this chip's f16 MFMA pipes sustain on random operands, measured live in this process after
     the timed region (librlks_calib.so: one wave per SIMD on every CU, eight independent accumulators,
     back-to-back issue), for the two shapes the SGD kernels use, against the dominant kernel's f16
@@ -467,9 +468,9 @@ def mfma_calibration(torch, sf16_tflops):
         rc = lib.rlks_calib_mfma_f16(shape, cus, 10000, 5, rnd.data_ptr(), out.data_ptr(), s.cuda_stream, C.byref(tf))
         res[name + "_tflops"] = tf.value if rc == 0 else None
     sustained = res["mfma_f32_16x16x32_f16_tflops"]
-    res["kernel_f16_mfma_tflops"] = 3 * sf16_tflops
-    res["frac_of_sustained_16x16x32"] = 3 * sf16_tflops / sustained if sustained else None
-    res["sf16_ceiling_sustained_tflops"] = sustained / 3 if sustained else None
+    res["kernel_f16_mfma_tflops"] = products * sf16_tflops
+    res["frac_of_sustained_16x16x32"] = products * sf16_tflops / sustained if sustained else None
+    res["sf16_ceiling_sustained_tflops"] = sustained / products if sustained else None
     return res
 
 
@@ -610,17 +611,18 @@ def main():
             cands = [k for k in kernels if k in ROOFLINE_KERNELS]
             dom = max(cands, key=lambda k: kernels[k]["ms"])
             k = kernels[dom]
-            peak = FP32_MFMA_PEAK_TFLOPS if algo.precision == "fp32" else SF16_PEAK_TFLOPS
+            peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16": F16_MFMA_PEAK_TFLOPS}.get(algo.precision, SF16_PEAK_TFLOPS)
             roofline = {"bound": "mfma", "kernel": dom, "achieved": k["tflops"], "peak": peak,
                         "unit": "TFLOP/s", "frac": k["tflops"] / peak, "traffic": None,
                         "flop_per_launch": flops_per_row(dom, algo.D, algo.H, algo.A) * algo.mb,
                         "avg_launch_ms": k["ms"],
                         "peak_basis": ("fp32 MFMA dense peak" if algo.precision == "fp32" else
+                                       "2.5 PF dense f16 MFMA (one product per FLOP)" if algo.precision == "f16" else
                                        "split-fp16: 2.5 PF dense f16 MFMA / 3 products per fp32-accurate FLOP")}
             if dom == "wide_grad":
                 roofline["note"] = "generic-width path: the whole SGD-step gradient (a sequence of split-fp16 GEMM launches)"
             if algo.precision != "fp32" and not args.no_kernel_timing:
-                roofline["calibration"] = mfma_calibration(torch, k["tflops"])
+                roofline["calibration"] = mfma_calibration(torch, k["tflops"], 1 if algo.precision == "f16" else 3)
             pmc = pmc_traffic()
             ab = algo_bytes_per_launch(dom, algo.mb, algo.D, algo.H, algo.A)
             roofline["algorithmic_bytes_per_launch"] = ab
@@ -654,7 +656,8 @@ def main():
             "metric": METRIC,
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
-            "dtype": "fp32" if algo.precision == "fp32" else "fp32 (split-fp16 MFMA, fp32-accurate)", "data": "synthetic (env-generated rollouts, random-init FCNet)",
+            "dtype": {"fp32": "fp32", "f16": "fp16 operands, fp32 accumulation (throughput mode, below the reference's fp32)"}.get(
+                algo.precision, "fp32 (split-fp16 MFMA, fp32-accurate)"), "data": "synthetic (env-generated rollouts, random-init FCNet)",
             "config": {"workload": preset["text"], "name": args.config,
                        "envs_per_gpu": envs, "rollout_steps": args.rollout, "minibatch_per_gpu": algo.mb,
                        "epochs": args.epochs, "global_batch": algo.samples * world, "global_envs": envs * world,

@@ -78,8 +78,11 @@ typedef struct rlks_mlp_desc {
 enum {
   RLKS_PRECISION_FP32 = 0,
   RLKS_PRECISION_SF16 = 1,
-  RLKS_PRECISION_WIDE = 2  /* generic split-fp16 GEMM path (wide_mlp.hip): any width, node envs;
+  RLKS_PRECISION_WIDE = 2, /* generic split-fp16 GEMM path (wide_mlp.hip): any width, node envs;
                               chosen automatically when the fused 256-unit kernels do not fit */
+  RLKS_PRECISION_F16 = 3   /* throughput mode: the split-fp16 SGD kernels with one product (fp16
+                              operands hi x hi, fp32 accumulation) instead of three -- below the
+                              reference's fp32, a secondary figure only; rollouts as RLKS_PRECISION_SF16 */
 };
 
 /* One split-fp16 GEMM (fp32 in / fp32 out, fp32-accurate): C = epi(op(A) op(B)), op = transpose

@@ -567,13 +567,18 @@ static int sf_prep(const rlks_mlp_desc* d, const SfWs& w, const float* params, h
 constexpr int SF_ROLL_FUSED_MAX_LANES = 16384;
 
 static bool is_wide(const rlks_mlp_desc* d) { return d->precision == RLKS_PRECISION_WIDE || wide_needed(d); }
+// the split-fp16 fused kernels (fp32-accurate, or the one-product throughput mode)
+static bool is_sf(const rlks_mlp_desc* d) {
+  return d->precision == RLKS_PRECISION_SF16 || d->precision == RLKS_PRECISION_F16;
+}
 
 // the fused kernels (mlp_fwd / mlp_bwd / sgd_sf16 / rollout_sf16) cover hidden 256, obs < 32 and
 // 2 / 4 / 8 actions; everything else runs on the generic-width path (wide_mlp.hip)
 static int check_desc(const rlks_mlp_desc* d) {
   RLKS_REQUIRE(d, RLKS_ERR_ARG, "null mlp desc");
   RLKS_REQUIRE(d->precision == RLKS_PRECISION_FP32 || d->precision == RLKS_PRECISION_SF16 ||
-                   d->precision == RLKS_PRECISION_WIDE, RLKS_ERR_ARG, "unknown precision");
+                   d->precision == RLKS_PRECISION_WIDE || d->precision == RLKS_PRECISION_F16, RLKS_ERR_ARG,
+               "unknown precision");
   RLKS_REQUIRE(d->obs_dim > 0 && d->hidden > 0 && d->hidden % 32 == 0 && d->hidden <= 8192 && d->n_actions > 0 &&
                    d->n_actions <= 64, RLKS_ERR_UNSUPPORTED,
                "MLP: hidden must be a multiple of 32 (<= 8192), 1 <= n_actions <= 64");
@@ -779,7 +784,7 @@ int rlks_ppo_workspace_bytes(const rlks_mlp_desc* d, int rows, int64_t* bytes) {
     *bytes = wide_ws_layout(d->obs_dim, d->hidden, d->n_actions, rows, nullptr).bytes;
     return RLKS_OK;
   }
-  if (d->precision == RLKS_PRECISION_SF16) {
+  if (is_sf(d)) {
     RLKS_REQUIRE(bytes && rows > 0 && rows % 256 == 0, RLKS_ERR_ARG,
                  "rlks_ppo_workspace_bytes: split-fp16 rows must be a positive multiple of 256");
     *bytes = sf_ws_layout(d->obs_dim, d->n_actions, rows, nullptr).bytes;
@@ -793,7 +798,7 @@ int rlks_ppo_workspace_bytes(const rlks_mlp_desc* d, int rows, int64_t* bytes) {
 
 int rlks_debug_sf_handoff(const rlks_mlp_desc* d, int rows, void* ws, void** out) {
   if (int rc = check_desc(d)) return rc;
-  RLKS_REQUIRE(out && ws && rows > 0 && rows % 256 == 0 && d->precision == RLKS_PRECISION_SF16 && !is_wide(d),
+  RLKS_REQUIRE(out && ws && rows > 0 && rows % 256 == 0 && is_sf(d) && !is_wide(d),
                RLKS_ERR_ARG, "rlks_debug_sf_handoff: split-fp16 descriptor, rows % 256 == 0");
   const SfWs w = sf_ws_layout(d->obs_dim, d->n_actions, rows, (char*)ws);
   for (int net = 0; net < 2; ++net) {
@@ -847,6 +852,7 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
   SfArgs a{};
   a.x = mb; a.x_stride = mb_stride(D, A); a.M = M; a.D = D; a.A_pi = A;
   a.tiles_per_split = w.tiles_per_split; a.co = *co; a.dyn = dyn;
+  a.products = d->precision == RLKS_PRECISION_F16 ? 1 : 3;
   for (int net = 0; net < 2; ++net) {
     a.n[net] = w.n[net];
     const NetPtrs P = net_ptrs_host(params, L, net);
@@ -930,7 +936,7 @@ int rlks_ppo_grad_phases(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, cons
     (void)phases;
     return wide_grad(d, co, params, dyn, mb, M, grad, stats, w, (hipStream_t)stream);
   }
-  if (d->precision == RLKS_PRECISION_SF16) {
+  if (is_sf(d)) {
     RLKS_REQUIRE(co && params && dyn && mb && grad && workspace, RLKS_ERR_ARG, "rlks_ppo_grad: null argument");
     return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, phases, (hipStream_t)stream);
   }
@@ -1027,7 +1033,7 @@ int rlks_ppo_sgd_step(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, float* 
   if (int rc = check_desc(d)) return rc;
   RLKS_REQUIRE(co && params && dyn && mb && grad && adam_m && adam_v && workspace && step >= 1, RLKS_ERR_ARG,
                "rlks_ppo_sgd_step: bad argument");
-  if (d->precision != RLKS_PRECISION_SF16 || is_wide(d)) {  // unfused: gradient, then Adam
+  if (!is_sf(d) || is_wide(d)) {  // unfused: gradient, then Adam
     if (int rc = rlks_ppo_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, stream)) return rc;
     return rlks_adam_step(params, grad, adam_m, adam_v, n_params, lr, beta1, beta2, eps, step, stream);
   }
@@ -1045,7 +1051,7 @@ static int next_gather(const rlks_mlp_desc* d, const rlks_gather_next* x, NextGa
   GatherArgs g;
   if (int rc = gather_args(d, x->T, x->N, x->perm_seed, x->epoch, x->groups, x->group0, x->row0, x->rows, x->mb_dev, g))
     return rc;
-  fused = d->precision == RLKS_PRECISION_SF16 && !is_wide(d) && x->groups <= NEXT_GROUPS;
+  fused = is_sf(d) && !is_wide(d) && x->groups <= NEXT_GROUPS;
   n = NextGather{};
   for (int k = 0; k < x->groups && k < NEXT_GROUPS; ++k) n.perm[k] = g.perm[k];
   n.row0g = g.row0g;
@@ -1097,7 +1103,7 @@ int rlks_ppo_grad_step(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const 
   if (int rc = check_desc(d)) return rc;
   RLKS_REQUIRE(co && params && dyn && mb && grad && workspace && step >= 1, RLKS_ERR_ARG,
                "rlks_ppo_grad_step: bad argument");
-  if (d->precision != RLKS_PRECISION_SF16 || is_wide(d))
+  if (!is_sf(d) || is_wide(d))
     return rlks_ppo_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, stream);
   FusedAdam fa{nullptr, nullptr, nullptr, AdamCo{}, step, prev_fused ? 1 : 0, false};
   return sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, (hipStream_t)stream,
@@ -1133,7 +1139,7 @@ int rlks_ppo_grad_step_part(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, c
   RLKS_REQUIRE(part == 1 || part == 2, RLKS_ERR_ARG, "rlks_ppo_grad_step_part: part must be 1 or 2");
   RLKS_REQUIRE(co && params && dyn && mb && grad && workspace && step >= 1, RLKS_ERR_ARG,
                "rlks_ppo_grad_step_part: bad argument");
-  if (d->precision != RLKS_PRECISION_SF16 || is_wide(d)) {  // no split form: everything in part 1
+  if (!is_sf(d) || is_wide(d)) {  // no split form: everything in part 1
     if (part == 2) return x ? gather_after(d, x, stream) : RLKS_OK;
     return rlks_ppo_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, stream);
   }
@@ -1154,7 +1160,7 @@ int rlks_ppo_adam_apply(const rlks_mlp_desc* d, float* params, const float* grad
   if (int rc = check_desc(d)) return rc;
   RLKS_REQUIRE(params && grad && adam_m && adam_v && workspace && step >= 1, RLKS_ERR_ARG,
                "rlks_ppo_adam_apply: bad argument");
-  if (d->precision != RLKS_PRECISION_SF16 || is_wide(d))
+  if (!is_sf(d) || is_wide(d))
     return rlks_adam_step(params, grad, adam_m, adam_v, n_params, lr, beta1, beta2, eps, step, stream);
   RLKS_REQUIRE(rows > 0 && rows % 256 == 0, RLKS_ERR_ARG, "rlks_ppo_adam_apply: rows as in rlks_ppo_grad_step");
   const int D = d->obs_dim, A = d->n_actions, H = HID;
@@ -1248,7 +1254,7 @@ int rlks_rollout_ws(rlks_env* env, const rlks_mlp_desc* d, const float* params, 
     RLKS_REQUIRE(ws_bytes >= w.bytes, RLKS_ERR_ARG, "rlks_rollout_ws: workspace too small");
     return wide_rollout(env, d, params, b, explore, w, (hipStream_t)stream);
   }
-  if (d->precision != RLKS_PRECISION_SF16) return rlks_rollout(env, d, params, b, explore, stream);
+  if (!is_sf(d)) return rlks_rollout(env, d, params, b, explore, stream);
   RLKS_REQUIRE(env && params && b && b->T > 0 && b->N > 0 && workspace, RLKS_ERR_ARG, "rlks_rollout_ws: bad argument");
   rlks_env_cfg cfg;
   rlks_env_config(env, &cfg);

@@ -49,6 +49,7 @@ struct SfArgs {
   int x_stride, M, D, A_pi;
   int tiles_per_split;
   int net0;  // F1: first net of the grid (blockIdx.y + net0)
+  int products;  // MFMA products per split product: 1 = RLKS_PRECISION_F16 (hi hi), else 3 (fp32-accurate)
   rlks_ppo_coeffs co;
   const float* dyn;
 };

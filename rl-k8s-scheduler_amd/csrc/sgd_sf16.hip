@@ -56,6 +56,11 @@ __device__ __forceinline__ f32x16 mma3(h8 ah, h8 al, h8 bh, h8 bl, f32x16 c) {
   c = mma(ah, bl, c);
   return mma(ah, bh, c);
 }
+template <int P>
+__device__ __forceinline__ f32x16 mmaP(h8 ah, h8 al, h8 bh, h8 bl, f32x16 c) {
+  if constexpr (P == 1) return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+  else return mma3(ah, al, bh, bl, c);
+}
 
 __device__ __forceinline__ void split1(float x, _Float16& hi, _Float16& lo) {
   hi = (_Float16)x;
@@ -440,6 +445,13 @@ __device__ __forceinline__ f4 mm16x3(h8 ah, h8 al, h8 bh, h8 bl, f4 c) {
   return mm16(ah, bh, c);
 }
 __device__ __forceinline__ f4 mk16(h4 a, h4 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0); }
+// P products per split-fp16 product: 3 (lo hi + hi lo + hi hi: fp32-accurate, the default) or 1 (hi hi:
+// the fp16 throughput mode, RLKS_PRECISION_F16 -- fp16 operands, fp32 accumulation)
+template <int P>
+__device__ __forceinline__ f4 mmP(h8 ah, h8 al, h8 bh, h8 bl, f4 c) {
+  if constexpr (P == 1) return mm16(ah, bh, c);
+  else return mm16x3(ah, al, bh, bl, c);
+}
 __device__ __forceinline__ f4 mk16x3(h4 ah, h4 al, h4 bh, h4 bl, f4 c) {
   c = mk16(al, bh, c);
   c = mk16(ah, bl, c);
@@ -603,7 +615,7 @@ constexpr int f1b_lds_bytes() {
 //   dW3[A-1] = -sum_{a < A-1} dW3[a]
 // which is the same loss and gradient with A - 1 head rows instead of A (at 2 actions: half of the
 // head, of dZ2's products and of the dW3 reduce-scatter, the epilogue's largest part).  AH: head rows.
-template <int A_, int NET, int KD, int W>
+template <int A_, int NET, int KD, int W, int P>
 __device__ __forceinline__ void f1a_body(const SfArgs& g, int grp) {
   constexpr int NTHR = 64 * W;
   constexpr int AH = NET == 0 ? A_ - 1 : 1;
@@ -681,7 +693,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g, int grp) {
         for (int b = 0; b < 2; ++b) {
           h8 wh, wl;
           w1_frag<KD>(sW1, 2 * t + b, c, gq, wh, wl);
-          z[b] = mm16x3(wh, wl, xh, xl, f4zero());
+          z[b] = mmP<P>(wh, wl, xh, xl, f4zero());
         }
         float hv[8];  // 2^14 tanh = 2^14 - 2^15 r (the split's fixed H1 scale folded in)
 #pragma unroll
@@ -697,7 +709,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g, int grp) {
         h8 nh, nl;
         if (j < 7) hc_frag(buf, j + 1, c, gq, nh, nl);
         __builtin_amdgcn_sched_barrier(0);
-        acc[8 * ph + j] = mm16x3(ch, cl, bh, bl, acc[8 * ph + j]);
+        acc[8 * ph + j] = mmP<P>(ch, cl, bh, bl, acc[8 * ph + j]);
         __builtin_amdgcn_sched_barrier(0);
         if (j < 7) { ch = nh; cl = nl; }
       }
@@ -885,17 +897,17 @@ __device__ __forceinline__ int2 f1_net_group(const SfArgs& g) {
   return make_int2(b / G, b % G);
 }
 
-template <int A_, int KD, int W>
+template <int A_, int KD, int W, int P>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_fwd(SfArgs g) {
   const int2 ng = f1_net_group<W, (A_ <= 4)>(g);
-  if (ng.x + g.net0 == 0) f1a_body<A_, 0, KD, W>(g, ng.y);
-  else f1a_body<1, 1, KD, W>(g, ng.y);
+  if (ng.x + g.net0 == 0) f1a_body<A_, 0, KD, W, P>(g, ng.y);
+  else f1a_body<1, 1, KD, W, P>(g, ng.y);
 }
 
 // F1a's dW3 / db3 / stats partials per net: one per F1 workgroup
 int sf_f1a_parts(int M, int A) { return M / (16 * SF_F1_W); }
 
-template <int NET, int KD, int ND, int W>
+template <int NET, int KD, int ND, int W, int P>
 __device__ __forceinline__ void f1b_body(const SfArgs& g, int grp) {  // ND = obs_dim + 1 (rows d of dW1a^T)
   constexpr int NTHR = 64 * W;
   constexpr int DT = KD / 16;                      // 16-row d-tiles of dW1a^T
@@ -950,7 +962,7 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g, int grp) {  // ND = ob
         h8 nh, nl;
         if (j < 7) hc_frag(buf, j + 1, c, gq, nh, nl);
         __builtin_amdgcn_sched_barrier(0);
-        acc[8 * ph + j] = mm16x3(ah, al, ch, cl, acc[8 * ph + j]);
+        acc[8 * ph + j] = mmP<P>(ah, al, ch, cl, acc[8 * ph + j]);
         __builtin_amdgcn_sched_barrier(0);
         if (j < 7) { ch = nh; cl = nl; }
       }
@@ -975,7 +987,7 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g, int grp) {  // ND = ob
   for (int kt = 0; kt < 16; ++kt) {
     const _Float16* q = w1b + kt * 16 * KD;
     const h8 wh = *reinterpret_cast<const h8*>(q), wl = *reinterpret_cast<const h8*>(q + HID * KD);
-    const f4 z = mm16x3(xh, xl, wh, wl, f4zero());  // Z1 rows m = 4g + i, column k = 16 kt + c
+    const f4 z = mmP<P>(xh, xl, wh, wl, f4zero());  // Z1 rows m = 4g + i, column k = 16 kt + c
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float r = tanh_r(z[i] * k_z1);
@@ -1010,8 +1022,9 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g, int grp) {  // ND = ob
     }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      const f4 dh = mk16(xtl[dt], zh, mk16(xth[dt], zh, f4zero()));  // rows d = 16 dt + 4g + i, column k
-      const f4 dl2 = mk16(xth[dt], zl, f4zero());
+      const f4 dh = P == 1 ? mk16(xth[dt], zh, f4zero())
+                           : mk16(xtl[dt], zh, mk16(xth[dt], zh, f4zero()));  // rows d = 16 dt + 4g + i, column k
+      const f4 dl2 = P == 1 ? f4zero() : mk16(xth[dt], zl, f4zero());
       const float4 v = {fmaf(dl2[0], u1l, dh[0] * u1), fmaf(dl2[1], u1l, dh[1] * u1), fmaf(dl2[2], u1l, dh[2] * u1),
                         fmaf(dl2[3], u1l, dh[3] * u1)};
       // row k = c of the wave's slot: 16-byte quad gq at gq ^ ((c >> 1) & 3), so that the 8 lanes of a
@@ -1037,11 +1050,11 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g, int grp) {  // ND = ob
   }
 }
 
-template <int KD, int ND, int W>
+template <int KD, int ND, int W, int P>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_bwd(SfArgs g) {
   const int2 ng = f1_net_group<W, true>(g);
-  if (ng.x + g.net0 == 0) f1b_body<0, KD, ND, W>(g, ng.y);
-  else f1b_body<1, KD, ND, W>(g, ng.y);
+  if (ng.x + g.net0 == 0) f1b_body<0, KD, ND, W, P>(g, ng.y);
+  else f1b_body<1, KD, ND, W, P>(g, ng.y);
 }
 
 // ----------------------------------------------------------------------------- F2
@@ -1091,7 +1104,7 @@ constexpr int F2_MAX_TILES = 2 * 256;  // 16-row tiles per F2 workgroup (tiles_p
 // placed ping-pong: per chunk c, phase 1 = {waves 0-3: MFMAs of c, 4-7: production}, phase 2 =
 // {0-3: production, 4-7: MFMAs of c}, a barrier after each, so that each SIMD's VALU work runs
 // beside its partner wave's MFMAs.
-template <int KD>
+template <int KD, int P>
 __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
   const SfNet& N = g.n[blockIdx.y];
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1163,7 +1176,7 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
         const _Float16* pb = b + bbase + s * HID * 16 + 32 * 16 * j;
         const h8 bh = *reinterpret_cast<const h8*>(pb), bl = *reinterpret_cast<const h8*>(pb + F2_BPLANE);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i][j] = mma3(ah[i], al[i], bh, bl, acc[i][j]);
+        for (int i = 0; i < 2; ++i) acc[i][j] = mmaP<P>(ah[i], al[i], bh, bl, acc[i][j]);
       }
     }
   };
@@ -1251,8 +1264,10 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
         xh[j] = a;
         xl[j] = b;
       }
-      z = __builtin_amdgcn_mfma_f32_32x32x8f16(xl, wh[kb], z, 0, 0, 0);
-      z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wl[kb], z, 0, 0, 0);
+      if constexpr (P != 1) {
+        z = __builtin_amdgcn_mfma_f32_32x32x8f16(xl, wh[kb], z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wl[kb], z, 0, 0, 0);
+      }
       z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wh[kb], z, 0, 0, 0);
     }
     // rows of tile 2t + (q >> 3): H1 split at 2^(14 + E - e_T) (<= 2^14)
@@ -1512,20 +1527,25 @@ int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
   return RLKS_OK;
 }
 
-template <int A_, int KD>
-static int launch_f1_net(SfArgs a, int net0, int nets, hipStream_t s, int halves) {
+template <int A_, int KD, int P>
+static int launch_f1_net_p(SfArgs a, int net0, int nets, hipStream_t s, int halves) {
   constexpr int W = SF_F1_W;
   a.net0 = net0;
   const dim3 grid(a.M / (16 * W) * nets);  // (f1_net_group)
   if (halves & 1) {  // pi's LDS (A_ >= 1) covers the value net's
-    hipLaunchKernelGGL((k_sf_fwd<A_, KD, W>), grid, dim3(64 * W), (f1a_lds_bytes<A_, KD, W>()), s, a);
+    hipLaunchKernelGGL((k_sf_fwd<A_, KD, W, P>), grid, dim3(64 * W), (f1a_lds_bytes<A_, KD, W>()), s, a);
     RLKS_LAUNCHED();
   }
   if (halves & 2) {
-    hipLaunchKernelGGL((k_sf_bwd<KD, 3 * A_ + 1, W>), grid, dim3(64 * W), f1b_lds_bytes<KD>(), s, a);
+    hipLaunchKernelGGL((k_sf_bwd<KD, 3 * A_ + 1, W, P>), grid, dim3(64 * W), f1b_lds_bytes<KD>(), s, a);
     RLKS_LAUNCHED();
   }
   return RLKS_OK;
+}
+template <int A_, int KD>
+static int launch_f1_net(const SfArgs& a, int net0, int nets, hipStream_t s, int halves) {
+  return a.products == 1 ? launch_f1_net_p<A_, KD, 1>(a, net0, nets, s, halves)
+                         : launch_f1_net_p<A_, KD, 3>(a, net0, nets, s, halves);
 }
 
 // obs_dim = 3 x clusters: C = 2, 4, 8 -> D = 6, 12, 24 (D + 1 <= 8, 16, 32)
@@ -1545,8 +1565,14 @@ int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int 
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {
   RLKS_REQUIRE(a.tiles_per_split <= F2_MAX_TILES / 2, RLKS_ERR_ARG, "split-fp16 F2: too many row chunks per split");
   const size_t lds = (size_t)2 * F2_BUF * sizeof(_Float16) + 2 * F2_MAX_TILES * sizeof(int);  // 140 KB
-  if (sf_kd(a.D) == 16) hipLaunchKernelGGL(k_sf_dw2<16>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
-  else hipLaunchKernelGGL(k_sf_dw2<32>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+  const bool p1 = a.products == 1;
+  if (sf_kd(a.D) == 16) {
+    if (p1) hipLaunchKernelGGL((k_sf_dw2<16, 1>), dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+    else hipLaunchKernelGGL((k_sf_dw2<16, 3>), dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+  } else {
+    if (p1) hipLaunchKernelGGL((k_sf_dw2<32, 1>), dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+    else hipLaunchKernelGGL((k_sf_dw2<32, 3>), dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+  }
   RLKS_LAUNCHED();
   return RLKS_OK;
 }

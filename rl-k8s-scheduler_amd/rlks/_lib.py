@@ -22,7 +22,7 @@ RLKS_DYN_ADV_MEAN, RLKS_DYN_ADV_INVSTD, RLKS_DYN_KL_COEFF, RLKS_DYN_INV_COUNT = 
 RLKS_STAT_SIZE = 8
 RLKS_PHASE_FWD, RLKS_PHASE_DW2, RLKS_PHASE_DH1, RLKS_PHASE_REDUCE, RLKS_PHASE_ALL = 1, 2, 4, 8, 15
 RLKS_PHASE_FWD_PI, RLKS_PHASE_FWD_VF, RLKS_PHASE_PREP, RLKS_PHASE_F1A, RLKS_PHASE_F1B = 16, 32, 64, 128, 256
-RLKS_PRECISION_FP32, RLKS_PRECISION_SF16, RLKS_PRECISION_WIDE = 0, 1, 2
+RLKS_PRECISION_FP32, RLKS_PRECISION_SF16, RLKS_PRECISION_WIDE, RLKS_PRECISION_F16 = 0, 1, 2, 3
 RLKS_STAT_POLICY_LOSS, RLKS_STAT_VF_LOSS, RLKS_STAT_KL, RLKS_STAT_ENTROPY, RLKS_STAT_ROWS = 0, 1, 2, 3, 4
 RLKS_EPLOG_CAP = 128
 

@@ -100,7 +100,9 @@ class PPOConfig:
         # MFMA (fp32-accurate, 16x the fp32 matrix rate; minibatch rows per rank % 256 == 0),
         # "fp32" = fp32 MFMA; "auto" = sf16 where the minibatch allows it.  Policies the fused
         # kernels do not cover (hidden != 256, obs > 31, actions not 2 / 4 / 8) always run the
-        # generic-width split-fp16 path ("wide")
+        # generic-width split-fp16 path ("wide").  "f16": the split-fp16 kernels with one product
+        # (fp16 operands, fp32 accumulation) -- a throughput mode below the reference's fp32, never
+        # chosen by "auto"
         self.sgd_precision = "auto"
 
     # ---- builder methods (names as in RLlib)
@@ -280,11 +282,11 @@ class PPO:
                 prec = "wide"
             elif prec == "auto":
                 prec = "sf16" if self.mb % 256 == 0 else "fp32"
-            if prec not in ("sf16", "fp32", "wide") or (prec == "sf16" and self.mb % 256):
+            if prec not in ("sf16", "f16", "fp32", "wide") or (prec in ("sf16", "f16") and self.mb % 256):
                 raise ValueError(f"sgd_precision {cfg.sgd_precision!r} with {self.mb} minibatch rows per rank")
             self.precision = prec
             self.params.desc.precision = {"sf16": _lib.RLKS_PRECISION_SF16, "fp32": _lib.RLKS_PRECISION_FP32,
-                                          "wide": _lib.RLKS_PRECISION_WIDE}[prec]
+                                          "wide": _lib.RLKS_PRECISION_WIDE, "f16": _lib.RLKS_PRECISION_F16}[prec]
             P = self.params.padded
             f32 = dict(dtype=torch.float32, device=self.device)
             self.adam_m = torch.zeros(P, **f32)
@@ -343,7 +345,7 @@ class PPO:
         off = self.params.offsets
         g = self.grad
         self._buckets = ([g[off[2]:self.params.padded]], [g[off[0]:off[2]]])
-        self._overlap = bool(cfg.overlap_allreduce) and self.world > 1 and self.precision == "sf16"
+        self._overlap = bool(cfg.overlap_allreduce) and self.world > 1 and self.precision in ("sf16", "f16")
         self.sample_calls = 0   # compute_actions / compute_single_action draws so far (Philox counter)
         self.iteration = 0
         self.timesteps_total = 0

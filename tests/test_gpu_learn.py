@@ -145,6 +145,47 @@ def _minibatch(rows, rng, D=6, A=2, p=None, d=None):
 
 
 @pytest.mark.parametrize("A", [2, 8])
+def test_f16_throughput_mode_gradient(A):
+    """RLKS_PRECISION_F16 (the split-fp16 SGD kernels with one product: fp16 operands hi x hi, fp32
+    accumulation): a throughput mode below the reference's fp32, never chosen by "auto".  Its gradient
+    is within 5e-3 of the fp64 oracle per tensor (norm-wise: fp16's 2^-11 operand rounding), and it is
+    not the fp32-accurate result (the mode really drops the lo products)."""
+    from rlks import _lib
+
+    d = _dev()
+    rows, D = 4096, 3 * A
+    p = _params(d, seed=rows + A, D=D, A=A)
+    rng = np.random.default_rng(rows)
+    mb = _minibatch(rows, rng, D=D, A=A, p=p, d=d)
+    dyn = torch.tensor([0.3, 0.7, 0.2, 1.0 / rows, 0, 0, 0, 0], dtype=torch.float32, device=d)
+    co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.01)
+    mbt = torch.from_numpy(mb).to(d)
+    grads = {}
+    for prec in (_lib.RLKS_PRECISION_F16, _lib.RLKS_PRECISION_SF16):
+        p.desc.precision = prec
+        wsb = C.c_int64()
+        _lib.call("rlks_ppo_workspace_bytes", C.byref(p.desc), rows, C.byref(wsb))
+        ws = torch.empty(wsb.value, dtype=torch.uint8, device=d)
+        grad = torch.zeros(p.padded, device=d)
+        _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
+                  rows, grad.data_ptr(), None, ws.data_ptr(), ws.numel(), None)
+        grads[prec] = grad.cpu().numpy().astype(np.float64)
+    eg, _ = oracle.ppo_loss_grad(p.flat.cpu().numpy(), p.offsets, D, 256, A, mb, entropy_coeff=0.01, kl_coeff=0.2,
+                                 adv_mean=0.3, adv_inv_std=0.7)
+    g16, gsf = grads[_lib.RLKS_PRECISION_F16], grads[_lib.RLKS_PRECISION_SF16]
+    assert np.isfinite(g16).all()
+    worst = 0.0
+    for i, shp in enumerate(p.shapes):
+        o, n = p.offsets[i], int(np.prod(shp))
+        a, b = g16[o:o + n], eg[o:o + n]
+        r = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+        worst = max(worst, r)
+        assert r <= 5e-3, (i, r)
+        assert np.linalg.norm(gsf[o:o + n] - b) <= 1e-5 * np.linalg.norm(b) + 1e-12, i
+    assert worst > 1e-6, worst  # (the one-product mode is not the fp32-accurate kernel)
+
+
+@pytest.mark.parametrize("A", [2, 8])
 def test_sf16_grad_tile_dynamic_range(A):
     """split-fp16 gradient with every other 16-row tile 'quiet': its rows' dlogits / dvalue 2^-20 of the
     others' (old logits = the current ones, standardised advantage and value error scaled by 2^-20),
