@@ -1323,49 +1323,45 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
   __syncthreads();
   F2_STAMP(0);
   if constexpr (KD > 16) {
-  // KD = 32 (8 actions): one loop for both halves: [MFMAs of chunk ci | barrier | production of chunk ci + 1 + off |
-  // barrier], the second half (off = 1) one phase behind after a production of chunk 1 of its own, so
-  // that each SIMD still pairs one wave's MFMAs with its partner's production.  (Two loops, the second
-  // half's starting with its production, compiled to different code -- the first half's MFMA phase
-  // opened with s_waitcnt vmcnt(0) on its prefetches -- and the second half's production ran at half
-  // the first half's speed: profiles/r05_f2.)  c3 F2 88 -> 80 µs (the two-loop form also spilled
-  // 10 registers here); at KD = 16 the two loops stay (c4: 66-68 vs 69-71 µs, same box)  The production runs at the last chunks too, redoing
-  // one into the idle buffer uncounted: unconditional, so that the prefetches stay where they are.
-  const int off = first ? 0 : 1;
-  if (!first) {
-    produce(sm + F2_BUF, 1 < nk);
-    load_x(min(t0 + 2, t1 - 1));
-    __builtin_amdgcn_sched_barrier(0);
-    load_dz(min(t0 + 2, t1 - 1));
-    F2_STAMP(2);
-  }
-  if (!first) {
-    phase_barrier();
-    F2_STAMP(3);
-  }
-  for (int ci = 0; ci < nk; ++ci) {
-    mfma_chunk(sm + (ci & 1) * F2_BUF);
-    F2_STAMP(1);
-    phase_barrier();
-    F2_STAMP(3);
-    const int cn = ci + 1 + off;  // the chunk this production makes
-    produce(sm + (cn & 1) * F2_BUF, cn < nk);
-    load_x(min(t0 + cn + 1, t1 - 1));  // (before the dZ2 pieces: a spill reload for these
-    __builtin_amdgcn_sched_barrier(0);  // addresses would otherwise wait for them)
-    load_dz(min(t0 + cn + 1, t1 - 1));
-    F2_STAMP(2);
-    phase_barrier();
-    F2_STAMP(3);
-  }
-  if (first) {  // the second half's extra phase
-    phase_barrier();
-    F2_STAMP(3);
-  }
-  } else {
-  // (one loop per half, so that the phases' state stays in registers; the production runs at the last
-  // chunk too, redoing it into the idle buffer uncounted: unconditional, so that the compiler keeps
-  // the prefetches where they are)
-  if (first) {
+    // KD = 32 (8 actions): one loop for both halves, [MFMAs of chunk ci | barrier | production of chunk
+    // ci + 1 + off | barrier], the second half (off = 1) one phase behind after a production of chunk 1
+    // of its own, so that each SIMD still pairs one wave's MFMAs with its partner's production.  (With a
+    // loop per half the two compiled to different code and the second half's production ran at half the
+    // first half's speed, profiles/r05_f2; here this form also avoids that instance's 10 spilled
+    // registers: c3 F2 86.5 -> 84.8 µs.  At KD = 16 the two loops stay: c4 66-68 vs 69-71 µs.)  The
+    // production runs at the last chunks too, redoing one into the idle buffer uncounted.
+    const int off = first ? 0 : 1;
+    if (!first) {
+      produce(sm + F2_BUF, 1 < nk);
+      load_x(min(t0 + 2, t1 - 1));
+      __builtin_amdgcn_sched_barrier(0);
+      load_dz(min(t0 + 2, t1 - 1));
+      F2_STAMP(2);
+      phase_barrier();
+      F2_STAMP(3);
+    }
+    for (int ci = 0; ci < nk; ++ci) {
+      mfma_chunk(sm + (ci & 1) * F2_BUF);
+      F2_STAMP(1);
+      phase_barrier();
+      F2_STAMP(3);
+      const int cn = ci + 1 + off;  // the chunk this production makes
+      produce(sm + (cn & 1) * F2_BUF, cn < nk);
+      load_x(min(t0 + cn + 1, t1 - 1));  // (before the dZ2 pieces: a spill reload for these
+      __builtin_amdgcn_sched_barrier(0);  // addresses would otherwise wait for them)
+      load_dz(min(t0 + cn + 1, t1 - 1));
+      F2_STAMP(2);
+      phase_barrier();
+      F2_STAMP(3);
+    }
+    if (first) {  // the second half's extra phase
+      phase_barrier();
+      F2_STAMP(3);
+    }
+  } else if (first) {
+    // (one loop per half, so that the phases' state stays in registers; the production runs at the last
+    // chunk too, redoing it into the idle buffer uncounted: unconditional, so that the compiler keeps
+    // the prefetches where they are)
     for (int ci = 0; ci < nk; ++ci) {
       mfma_chunk(sm + (ci & 1) * F2_BUF);
       F2_STAMP(1);
@@ -1382,8 +1378,8 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
   } else {
     for (int ci = 0; ci < nk; ++ci) {
       produce(sm + ((ci + 1) & 1) * F2_BUF, ci + 1 < nk);
-      load_x(min(t0 + ci + 2, t1 - 1));  // (before the dZ2 pieces: a spill reload for these
-      __builtin_amdgcn_sched_barrier(0);  // addresses would otherwise wait for them)
+      load_x(min(t0 + ci + 2, t1 - 1));
+      __builtin_amdgcn_sched_barrier(0);
       load_dz(min(t0 + ci + 2, t1 - 1));
       F2_STAMP(2);
       phase_barrier();
@@ -1393,7 +1389,6 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
       phase_barrier();
       F2_STAMP(3);
     }
-  }
   }
 #undef F2_STAMP
 
