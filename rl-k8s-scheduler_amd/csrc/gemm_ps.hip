@@ -177,33 +177,43 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   float* const Cout = split ? g.part + (size_t)blockIdx.z * g.M * g.N : g.C;
   const int ldc = split ? g.N : g.ldc;
   float cmax = 0.f;
+  // the wave's 64 x 64 block from uniform base pointers (SGPRs) and 32-bit per-lane offsets: with a
+  // 64-bit address per element the unrolled epilogue spilled (10-16 registers); -1.3% on the c5
+  // gradient (profiles/r05_gemm).  Without the bounds branches it hoisted its loads and spilled more
+  const int mw = m0 + wm * 64, nw = n0 + wn * 64;
+  float* const cw = Cout + (size_t)mw * ldc + nw;
+  _Float16* const hw = EPI == PS_TANH_BIAS_PLANES ? g.c_hi + (size_t)mw * ldc + nw : nullptr;
+  _Float16* const lw = EPI == PS_TANH_BIAS_PLANES ? g.c_lo + (size_t)mw * ldc + nw : nullptr;
+  const _Float16* const ahw = EPI == PS_DTANH ? g.aux_hi + (size_t)mw * g.ldaux + nw : nullptr;
+  const _Float16* const alw = EPI == PS_DTANH ? g.aux_lo + (size_t)mw * g.ldaux + nw : nullptr;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 64 + 32 * j + r;
+    const int nl = 32 * j + r, n = nw + nl;
     const bool nok = n < g.N;
     const float bias = (EPI == PS_TANH_BIAS || EPI == PS_TANH_BIAS_PLANES) && nok ? g.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int m = m0 + wm * 64 + 32 * i + acc_row(q, l);
-        if (!nok || m >= g.M) continue;
+        const int ml = 32 * i + acc_row(q, l);  // C row mw + ml, column n
+        if (!nok || mw + ml >= g.M) continue;
+        const int off = ml * ldc + nl;
         float v = acc[i][j][q] * unscale;
         if (EPI == PS_TANH_BIAS || EPI == PS_TANH_BIAS_PLANES)
           v = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f((v + bias) * 2.885390081777927f) + 1.f), 1.f);
         if (EPI == PS_TANH_BIAS_PLANES) {  // H1 for the pre-split GEMMs: fp16 planes at 2^14
           const float hs = v * 16384.f;
           const _Float16 hh = (_Float16)hs;
-          g.c_hi[(size_t)m * ldc + n] = hh;
-          g.c_lo[(size_t)m * ldc + n] = (_Float16)(hs - (float)hh);
+          hw[off] = hh;
+          lw[off] = (_Float16)(hs - (float)hh);
           continue;
         }
         if (EPI == PS_DTANH) {  // G = (hi + lo) 2^-14 from the aux planes
-          const size_t ai = (size_t)m * g.ldaux + n;
-          const float gg = ((float)g.aux_hi[ai] + (float)g.aux_lo[ai]) * (1.f / 16384.f);
+          const int ai = ml * g.ldaux + nl;
+          const float gg = ((float)ahw[ai] + (float)alw[ai]) * (1.f / 16384.f);
           v *= 1.f - gg * gg;
         }
-        Cout[(size_t)m * ldc + n] = v;
+        cw[off] = v;
         cmax = fmaxf(cmax, fabsf(v));
       }
   }
