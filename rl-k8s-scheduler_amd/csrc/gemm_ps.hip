@@ -194,27 +194,43 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int ml = 32 * i + acc_row(q, l);  // C row mw + ml, column n
-        if (!nok || mw + ml >= g.M) continue;
-        const int off = ml * ldc + nl;
-        float v = acc[i][j][q] * unscale;
-        if (EPI == PS_TANH_BIAS || EPI == PS_TANH_BIAS_PLANES)
-          v = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f((v + bias) * 2.885390081777927f) + 1.f), 1.f);
-        if (EPI == PS_TANH_BIAS_PLANES) {  // H1 for the pre-split GEMMs: fp16 planes at 2^14
-          const float hs = v * 16384.f;
-          const _Float16 hh = (_Float16)hs;
-          hw[off] = hh;
-          lw[off] = (_Float16)(hs - (float)hh);
-          continue;
+      for (int qb = 0; qb < 16; qb += 8) {
+        // dZ1: the batch's 8 aux (hi, lo) pairs loaded up front from clamped (always in-bounds)
+        // addresses, so that their latencies overlap instead of each load waiting behind its
+        // element's bounds branch (219 of dZ1's 1,900 µs at c5, profiles/r05_gemm)
+        _Float16 gh[8], gl[8];
+        if (EPI == PS_DTANH) {
+          const int nc = min(n, g.N - 1) - nw;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int mc = min(mw + 32 * i + acc_row(qb + t, l), g.M - 1) - mw;
+            gh[t] = ahw[mc * g.ldaux + nc];
+            gl[t] = alw[mc * g.ldaux + nc];
+          }
         }
-        if (EPI == PS_DTANH) {  // G = (hi + lo) 2^-14 from the aux planes
-          const int ai = ml * g.ldaux + nl;
-          const float gg = ((float)ahw[ai] + (float)alw[ai]) * (1.f / 16384.f);
-          v *= 1.f - gg * gg;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int ml = 32 * i + acc_row(qb + t, l);  // C row mw + ml, column n
+          if (!nok || mw + ml >= g.M) continue;
+          const int off = ml * ldc + nl;
+          float v = acc[i][j][qb + t] * unscale;
+          if (EPI == PS_TANH_BIAS || EPI == PS_TANH_BIAS_PLANES)
+            v = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f((v + bias) * 2.885390081777927f) + 1.f), 1.f);
+          if (EPI == PS_TANH_BIAS_PLANES) {  // H1 for the pre-split GEMMs: fp16 planes at 2^14
+            const float hs = v * 16384.f;
+            const _Float16 hh = (_Float16)hs;
+            hw[off] = hh;
+            lw[off] = (_Float16)(hs - (float)hh);
+            continue;
+          }
+          if (EPI == PS_DTANH) {  // G = (hi + lo) 2^-14 from the aux planes
+            const float gg = ((float)gh[t] + (float)gl[t]) * (1.f / 16384.f);
+            v *= 1.f - gg * gg;
+          }
+          cw[off] = v;
+          cmax = fmaxf(cmax, fabsf(v));
         }
-        cw[off] = v;
-        cmax = fmaxf(cmax, fabsf(v));
+        if (EPI == PS_DTANH) __builtin_amdgcn_sched_barrier(0);  // one batch's loads in flight at a time
       }
   }
   if (g.cmax && !split) {

@@ -5,7 +5,7 @@ LOG=$1; TO=$2; CMD=$3
 for i in $(seq 1 30); do
   timeout $((TO + 900)) /usr/local/graft/bin/gpurun --timeout $TO -- "$CMD" > $LOG 2>&1
   rc=$?
-  if grep -q "status=transient" $LOG && grep -q "nothing was charged\|no free box" $LOG; then
+  if grep -q "status=transient" $LOG && grep -q "nothing was charged\|no free box\|backing off\|stopped responding while being prepared" $LOG; then
     echo "retry $i (rc=$rc)" >> $LOG.retries; sleep 150; continue
   fi
   break
