@@ -250,16 +250,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   float* const Cout = split ? g.part + (size_t)blockIdx.z * g.M * g.N : g.C;
   const int ldc = split ? g.N : g.ldc;
   float cmax = 0.f;
+  // the wave's 64 x 64 block from uniform base pointers and 32-bit per-lane offsets (gemm_ps.hip)
+  const int mw = m0 + wm * 64, nw = n0 + wn * 64;
+  float* const cw = Cout + (size_t)mw * ldc + nw;
+  const float* const cin = g.C + (size_t)mw * g.ldc + nw;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 64 + 32 * j + r;
+    const int nl = 32 * j + r, n = nw + nl;
     const bool nok = n < g.N;
     const float bias = (EPI == GEMM_TANH_BIAS || EPI == GEMM_BIAS || EPI == GEMM_TANH_BIAS_PLANES) && nok ? g.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int m = m0 + wm * 64 + 32 * i + acc_row(q, l);
+        const int ml = 32 * i + acc_row(q, l), m = mw + ml;
         if (!nok || m >= g.M) continue;
         float v = acc[i][j][q] * unscale;
         if (EPI == GEMM_TANH_BIAS_PLANES) {  // H1 for the pre-split GEMMs: fp16 planes at 2^14
@@ -275,8 +279,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           const float gg = g.aux[(size_t)m * g.ldaux + n];
           v *= 1.f - gg * gg;
         }
-        if (g.accumulate && !split) v += g.C[(size_t)m * g.ldc + n];
-        Cout[(size_t)m * ldc + n] = v;
+        if (g.accumulate && !split) v += cin[ml * g.ldc + nl];
+        cw[ml * ldc + nl] = v;
         cmax = fmaxf(cmax, fabsf(v));
       }
   }
