@@ -60,6 +60,7 @@ def flops_per_row(name, D=6, H=256, A=2):
         # split-fp16 F1 (sgd_sf16.hip) as two kernels: forward + head backward (F1a), dH1 = dZ2 W2 +
         # dW1 = dZ1^T X (F1b); f1_total is the pair
         "f1_total": sum(fwd(An) + head(An) + 2 * H * H + 2 * D * H for An in (A, 1)),
+        "k_sf_f1": sum(fwd(An) + head(An) + 2 * H * H + 2 * D * H for An in (A, 1)),  # fused F1 = F1a + F1b
         "k_sf_fwd": sum(fwd(An) + head(An) for An in (A, 1)),
         "k_sf_bwd": 2 * (2 * H * H + 2 * D * H),
         "k_sf_dw2": 2 * 2 * H * H,                  # dW2 = dZ2^T H1, both nets
@@ -105,7 +106,8 @@ def env_setup(name):
                          init_occupancy=0.5)
 
 
-ROOFLINE_KERNELS = ("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "wide_grad")
+ROOFLINE_KERNELS = ("k_fwd_head_pi", "k_fwd_head_vf", "k_dw2", "k_dh1", "k_sf_f1", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2",
+                    "wide_grad")
 
 
 def algo_bytes_per_launch(name, rows, D=6, H=256, A=2):
@@ -116,7 +118,7 @@ def algo_bytes_per_launch(name, rows, D=6, H=256, A=2):
     gradient partials and the weights (< 0.5 MB) are not algorithmic: they are the overhead
     traffic_over_algorithmic exposes."""
     rec = (D + A + 4 + 3) // 4 * 4 * 4
-    per_row = {"k_sf_fwd": rec, "k_sf_bwd": 4 * D, "k_sf_dw2": 4 * D}.get(name)
+    per_row = {"k_sf_f1": rec, "k_sf_fwd": rec, "k_sf_bwd": 4 * D, "k_sf_dw2": 4 * D}.get(name)
     return None if per_row is None else per_row * rows
 
 
@@ -177,22 +179,38 @@ def _free_port():
     return port
 
 
+def visible_gpus():
+    """GPUs this process may use, counted without any HIP call (the launcher parent must stay
+    HIP-free: torch.cuda.device_count() falls back to hipGetDeviceCount, which initialises HIP, when
+    amdsmi is unavailable).  A *_VISIBLE_DEVICES list, if set, is the count; otherwise the KFD topology's
+    GPU nodes (gpu_id != 0) in sysfs.  None when neither says: the ranks then check for themselves."""
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() != ""])
+    nodes = Path("/sys/class/kfd/kfd/topology/nodes")
+    try:
+        ids = [(d / "gpu_id").read_text().strip() for d in nodes.iterdir() if (d / "gpu_id").exists()]
+    except OSError:
+        return None
+    n = sum(1 for i in ids if i not in ("", "0"))
+    return n if ids else None
+
+
 def launch_ranks(n, argv, timeout=None):
     """`bench.py --gpus N` with no torch.distributed launcher around it: start N fresh child
     processes of this script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
     MASTER_PORT set (the contract's torch.distributed.run environment), and return the worst exit
-    status.  This process makes no HIP call (a child is started, never exec'd: see the GPU box's
-    rules); it only counts devices, which does not initialise the GPU on this image.  When a rank
-    fails, the others are stopped (they would wait at the next collective forever)."""
+    status.  This process makes no HIP call and does not import torch (a child is started, never
+    exec'd: see the GPU box's rules); it counts devices from sysfs (visible_gpus).  When a rank fails,
+    the others are stopped at once (they would wait at the next collective until RCCL's watchdog)."""
     import subprocess
 
     backend = os.environ.get("RLKS_DIST_BACKEND", "nccl")
     if "--dry-run" not in argv and backend == "nccl":
-        import torch
-
-        have = torch.cuda.device_count()
-        if n > have:
-            raise SystemExit(f"bench.py --gpus {n}: only {have} HIP device(s) visible (RCCL needs one GPU per rank; "
+        have = visible_gpus()
+        if have is not None and n > have:
+            raise SystemExit(f"bench.py --gpus {n}: only {have} GPU(s) visible (RCCL needs one GPU per rank; "
                              "RLKS_DIST_BACKEND=gloo rehearses several ranks on fewer GPUs)")
     port = os.environ.get("MASTER_PORT") or str(_free_port())
     procs = []
@@ -204,10 +222,16 @@ def launch_ranks(n, argv, timeout=None):
     t0 = time.monotonic()
     worst = 0
     try:
-        while any(p.poll() is None for p in procs):
-            failed = [p.returncode for p in procs if p.returncode not in (None, 0)]
-            if failed or (timeout is not None and time.monotonic() - t0 > timeout):
-                worst = failed[0] if failed else 124
+        while True:
+            codes = [p.poll() for p in procs]  # every process polled in every pass (a list, not a generator)
+            failed = [c for c in codes if c not in (None, 0)]
+            if failed:
+                worst = failed[0]
+                break
+            if all(c is not None for c in codes):
+                break
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                worst = 124
                 break
             time.sleep(0.2)
     finally:
@@ -278,6 +302,21 @@ def kernel_timing(algo, torch, config="c2", reps=20):
     if "f1_total" in out:
         tf = flops_per_row("f1_total", D, H, A) * algo.mb / (out["f1_total"]["ms"] * 1e-3) / 1e12
         out["f1_total"].update({"tflops": tf, peak_name: tf / peak})
+    if algo.precision in ("sf16", "f16"):
+        # in-pipeline: every kernel of full gradients launched back to back as the SGD step runs them,
+        # HIP events between the launches (rlks_ppo_grad_profile): the durations rocprofv3 sees, which
+        # choose the roofline kernel (isolated repeats of one phase above are diagnostics only)
+        ms4 = (C.c_double * 4)()
+        _lib.call("rlks_ppo_grad_profile", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(), algo.dyn.data_ptr(),
+                  algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, algo.ws.data_ptr(), algo.ws.numel(), reps,
+                  ms4, s.cuda_stream)
+        f1 = "k_sf_fwd+k_sf_bwd" if os.environ.get("RLKS_F1_SPLIT") else "k_sf_f1"
+        pipe = {"k_sf_prep": ms4[0], f1: ms4[1], "k_sf_dw2": ms4[2], "k_reduce": ms4[3]}
+        rec = {"ms": pipe, "method": f"{reps} full gradients, HIP events between the launches"}
+        for name, fl in ((f1, flops_per_row("k_sf_f1", D, H, A)), ("k_sf_dw2", flops_per_row("k_sf_dw2", D, H, A))):
+            tf = fl * algo.mb / (pipe[name] * 1e-3) / 1e12
+            rec[name] = {"ms": pipe[name], "tflops": tf, peak_name: tf / peak}
+        out["pipeline"] = rec
     ms = timed(lambda: _lib.call("rlks_ppo_grad", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(),
                                  algo.dyn.data_ptr(), algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None,
                                  algo.ws.data_ptr(), algo.ws.numel(), s.cuda_stream), n=reps if H <= 256 else 3)
@@ -493,6 +532,9 @@ def dry_run(args, world, rank):
 
     if world > 1:
         dist.init_process_group("gloo")
+    fail = os.environ.get("RLKS_DRYRUN_FAIL_RANK")
+    if fail is not None and int(fail) == rank:  # launcher test: this rank dies while the others wait
+        sys.exit(3)
     preset = CONFIGS[args.config]
     envs, mb = shard_sizes(args, preset, world)
     for _ in range(args.warmup):
@@ -607,14 +649,20 @@ def main():
         roofline = None
         if kernels:
             # the dominant kernel as rocprofv3 --stats ranks them: largest share of GPU time (each
-            # runs once per SGD step, so: the longest launch)
-            cands = [k for k in kernels if k in ROOFLINE_KERNELS]
-            dom = max(cands, key=lambda k: kernels[k]["ms"])
-            k = kernels[dom]
+            # runs once per SGD step, so: the longest launch), timed in the pipeline where there is one
+            if "pipeline" in kernels:
+                pk = {n: v for n, v in kernels["pipeline"].items() if isinstance(v, dict) and "tflops" in v}
+                dom = max(pk, key=lambda n: pk[n]["ms"])
+                k = pk[dom]
+            else:
+                cands = [k for k in kernels if k in ROOFLINE_KERNELS]
+                dom = max(cands, key=lambda k: kernels[k]["ms"])
+                k = kernels[dom]
             peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16": F16_MFMA_PEAK_TFLOPS}.get(algo.precision, SF16_PEAK_TFLOPS)
             roofline = {"bound": "mfma", "kernel": dom, "achieved": k["tflops"], "peak": peak,
                         "unit": "TFLOP/s", "frac": k["tflops"] / peak, "traffic": None,
-                        "flop_per_launch": flops_per_row(dom, algo.D, algo.H, algo.A) * algo.mb,
+                        "flop_per_launch": flops_per_row(dom if dom in ROOFLINE_KERNELS else "k_sf_f1", algo.D, algo.H,
+                                                         algo.A) * algo.mb,
                         "avg_launch_ms": k["ms"],
                         "peak_basis": ("fp32 MFMA dense peak" if algo.precision == "fp32" else
                                        "2.5 PF dense f16 MFMA (one product per FLOP)" if algo.precision == "f16" else
@@ -631,11 +679,24 @@ def main():
                 roofline["traffic_source"] = pmc["source"]
                 if ab:
                     roofline["traffic_over_algorithmic"] = roofline["traffic"] / ab
+            if "pipeline" in kernels:  # the step's MFMA kernels side by side
+                side = {}
+                for n, v in kernels["pipeline"].items():
+                    if not (isinstance(v, dict) and "tflops" in v):
+                        continue
+                    e = {"avg_launch_ms": v["ms"], "achieved": v["tflops"], "frac": v["tflops"] / peak,
+                         "algorithmic_bytes_per_launch": algo_bytes_per_launch(n, algo.mb, algo.D, algo.H, algo.A)}
+                    if pmc and args.config in ("c2", "c4") and n in pmc:
+                        e["traffic"] = pmc[n]["hbm_bytes_per_launch"]
+                    side[n] = e
+                roofline["kernels"] = side
             if pmc and args.config in ("c2", "c4") and algo.precision == "sf16":
                 # the whole SGD step against its compulsory bytes: the minibatch records read once, the
                 # parameters read by the weight split, and Adam (p, m, v read + written, the gradient
                 # written and read): everything else is a hand-off between the step's own kernels
-                step = [k for k in ("k_sf_split", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce") if k in pmc]
+                step = [k for k in ("k_sf_split", "k_sf_f1", "k_sf_dw2", "k_reduce") if k in pmc]
+                if "k_sf_f1" not in pmc or os.environ.get("RLKS_F1_SPLIT"):
+                    step = [k for k in ("k_sf_split", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce") if k in pmc]
                 moved = sum(pmc[k]["hbm_bytes_per_launch"] for k in step)
                 P = algo.params.padded
                 comp = algo.mb * algo.stride * 4 + P * 4 + (6 + 2) * P * 4

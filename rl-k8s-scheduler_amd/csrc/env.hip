@@ -586,7 +586,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
   __shared__ int s_n, s_reset;
   const int tid = threadIdx.x;
   const int cm = (1 << cs) - 1;
-  const int env0 = blockIdx.x * (PB >> cs);
+  const int env0 = v.lane0 + blockIdx.x * (PB >> cs);  // (a lane range: node_rollout's halves)
   const int C = v.C, N = v.nodes, D = 3 * C;
   // ---- A: loads
   int t[NP], ep[NP], a[NP];
@@ -599,7 +599,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
     const int p = tid + j * NT, c = p & cm, lane = env0 + (p >> cs);
     t[j] = ep[j] = a[j] = used0[j] = 0;
     ocost[j] = olat[j] = rcost[j] = rlat[j] = eret[j] = 0.0;
-    if (lane < v.N && c < C) {
+    if (lane < v.lane_end && c < C) {
       t[j] = v.step[lane];
       ep[j] = v.episode[lane];
       a[j] = actions[lane];
@@ -624,7 +624,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     const int p = tid + j * NT, c = p & cm, el = p >> cs, lane = env0 + el;
-    if (lane < v.N && c < C) {
+    if (lane < v.lane_end && c < C) {
       if (!dcheck(a[j] >= 0 && a[j] < C, DC_NODE_ACTION, a[j])) a[j] = 0;
       if (t[j] < v.T) {
         if (c == 0) {
@@ -684,7 +684,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     const int p = tid + j * NT, c = p & cm, el = p >> cs, lane = env0 + el;
-    if (!(lane < v.N && c < C)) continue;
+    if (!(lane < v.lane_end && c < C)) continue;
     if (t[j] >= v.T) {  // iloc[t] out of bounds before any change
       if (c == 0) {
         ++n_over;
@@ -958,6 +958,23 @@ __global__ void k_mt_draws(uint32_t* __restrict__ mt, double* __restrict__ out, 
   for (int i = 0; i < n; ++i) out[i] = mt_random(mt, 1, 0);
 }
 
+// the trusted node step (rlks_env_step with status / truncated / step / final obs null) over the lanes
+// [lane0, lane_end) only, for node_rollout's two halves; false: this env has no lane-range step (C >
+// NODE_WL_MAX_C or no nodes), use rlks_env_step
+bool node_step_range(rlks_env* e, int lane0, int lane_end, const int32_t* actions, float* obs, float* rew32,
+                     uint8_t* term, hipStream_t s) {
+  const int C = e->cfg.n_clouds;
+  if (e->cfg.nodes_per_cluster <= 0 || C > NODE_WL_MAX_C) return false;
+  int cs = 0;
+  while ((1 << cs) < C) ++cs;
+  EnvView v = view(e);
+  v.lane0 = lane0;
+  v.lane_end = lane_end;
+  const dim3 gridw(cdiv(lane_end - lane0, (NODE_WL_NP * 64 * NODE_WL_W) >> cs)), blkw(64 * NODE_WL_W);
+  hipLaunchKernelGGL((k_node_step_wl<NODE_WL_NP, NODE_WL_W>), gridw, blkw, 0, s, v, e->d_cost, e->d_lat, actions, obs,
+                     nullptr, rew32, term, nullptr, nullptr, nullptr, nullptr, cs);
+  return hipGetLastError() == hipSuccess;
+}
 }  // namespace rlks
 
 using namespace rlks;
@@ -1113,6 +1130,9 @@ int rlks_env_destroy(rlks_env* e) {
   if (e->d_free) (void)hipFree(e->d_free);
   if (e->d_chunk) (void)hipFree(e->d_chunk);
   if (e->d_used_cpu) (void)hipFree(e->d_used_cpu);
+  if (e->side) (void)hipStreamDestroy(e->side);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   delete e;
   return RLKS_OK;
 }

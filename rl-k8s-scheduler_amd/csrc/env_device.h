@@ -45,6 +45,10 @@ struct rlks_env {
   long long* d_eplog_key;
   unsigned* d_eplog_n;
   double* d_epstat;  // [ceil(n_envs / EPS_LANES)][2] partial (sum, count) of rlks_env_episode_stats
+  // node rollouts in two lane halves (ppo.hip node_rollout): the second half's stream and the fork /
+  // join events, created on first use
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace rlks {
@@ -54,6 +58,8 @@ constexpr int MAX_TABLE_BYTES = 128 * 1024;  // LDS budget for the staged tables
 
 struct EnvView {
   int N, T, C, max_steps, noise_mode, autoreset, env_offset, track_returns;
+  int lane0, lane_end;  // the lanes a node step / sample launch covers: [lane0, lane_end) (view(): all N);
+                        // N stays the stride of the per-lane arrays
   uint32_t k0, k1;
   double cpu_lo, span, w_cost, w_lat, scale;
   int32_t* step;
@@ -80,9 +86,12 @@ struct EnvView {
   unsigned* eplog_n;
 };
 
+bool node_step_range(rlks_env* e, int lane0, int lane_end, const int32_t* actions, float* obs, float* rew32,
+                     uint8_t* term, hipStream_t s);  // (env.hip)
+
 inline EnvView view(const rlks_env* e) {
   EnvView v;
-  v.N = e->cfg.n_envs; v.T = e->cfg.n_rows; v.C = e->cfg.n_clouds; v.max_steps = e->cfg.max_steps;
+  v.N = e->cfg.n_envs; v.lane0 = 0; v.lane_end = e->cfg.n_envs; v.T = e->cfg.n_rows; v.C = e->cfg.n_clouds; v.max_steps = e->cfg.max_steps;
   v.noise_mode = e->cfg.noise_mode; v.autoreset = e->cfg.autoreset; v.env_offset = e->cfg.env_offset;
   v.track_returns = e->cfg.skip_returns ? 0 : 1;
   v.k0 = (uint32_t)e->cfg.seed; v.k1 = (uint32_t)(e->cfg.seed >> 32);

@@ -480,14 +480,14 @@ struct SfWs {
   float* pmax_roll[2];  // the rollout's weight-max slots (the SGD steps' pmax keeps its parity state)
   int64_t bytes, weight_bytes;
   int blocks, splits, tiles_per_split;
-  int fa_parts;  // F1a's dW3 / db3 / stats partials per net (sf_f1a_parts <= blocks)
+  int fa_parts;  // F1's dW3 / db3 / stats partials per net (the split kernels' count: the allocation)
 };
 
 static SfWs sf_ws_layout(int D, int A, int M, char* base) {
   SfWs w{};
   const int KD = sf_kd(D), tiles = M / 32;  // F2's 32-row tiles
   w.blocks = M / (16 * SF_F1_W);  // F1 workgroups of SF_F1_W x 16 rows
-  w.fa_parts = sf_f1a_parts(M, A);
+  w.fa_parts = sf_f1_parts(M, false);
   w.splits = 1;
   constexpr int F2_MAX_SPLITS = 128;  // F2 row splits per net (one 512-thread workgroup each)
   while (w.splits * 2 <= F2_MAX_SPLITS && tiles % (w.splits * 2) == 0) w.splits *= 2;
@@ -607,13 +607,14 @@ static int node_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* para
     }
     r.M = N; r.D = D;
   }
-  auto forward = [&](const float* x, float* logits, float* values) -> int {
+  auto forward = [&](const float* x, float* logits, float* values, int M = -1, hipStream_t fs = nullptr) -> int {
     if (w) {  // 16-row tiles of both nets (sgd_sf16.hip k_sf_fwd16)
       SfFwdArgs a = r;
       a.x = x;
+      a.M = M < 0 ? N : M;
       a.out[0] = logits;
       a.out[1] = values;
-      return launch_sf_fwd16(a, A, s);
+      return launch_sf_fwd16(a, A, fs ? fs : s);
     }
     for (int net = 0; net < 2; ++net) {
       float* out = net == 0 ? logits : values;
@@ -626,6 +627,43 @@ static int node_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* para
     return RLKS_OK;
   };
   const EnvView v = view(env);
+  // Two lane halves on two streams: each half runs forward -> sample -> node step
+  // on its own stream, so one half's latency-bound node step runs beside the other half's MFMA-bound
+  // forward instead of after it.  Same launches per lane, Philox counters per lane: the same rollout bit
+  // for bit (RLKS_NODE_ONE_STREAM: the single-stream order, A/B).
+  const int half = (N / 2) / 128 * 128;
+  if (w && N >= 8192 && env->cfg.nodes_per_cluster > 0 && env->cfg.n_clouds <= 64 && !getenv("RLKS_NODE_ONE_STREAM")) {
+    if (!env->side) {
+      RLKS_HIP(hipStreamCreateWithFlags(&env->side, hipStreamNonBlocking));
+      RLKS_HIP(hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));
+      RLKS_HIP(hipEventCreateWithFlags(&env->ev_join, hipEventDisableTiming));
+    }
+    RLKS_HIP(hipEventRecord(env->ev_fork, s));
+    RLKS_HIP(hipStreamWaitEvent(env->side, env->ev_fork, 0));
+    const int lo[2] = {0, half}, hi[2] = {half, N};
+    const hipStream_t hs[2] = {s, env->side};
+    for (int t = 0; t < b->T; ++t) {
+      const size_t tN = (size_t)t * N;
+      for (int h = 0; h < 2; ++h) {
+        const size_t o = tN + lo[h];
+        if (int rc = forward(b->obs + o * D, b->logits + o * A, b->values + o, hi[h] - lo[h], hs[h])) return rc;
+        EnvView vh = v;
+        vh.lane0 = lo[h];
+        vh.lane_end = hi[h];
+        if (int rc = launch_sample(vh, b->logits + tN * A, A, explore, b->actions + tN, b->logp + tN, hs[h])) return rc;
+        if (!node_step_range(env, lo[h], hi[h], b->actions + tN, b->obs + (tN + N) * D, b->rewards + tN,
+                             b->dones + tN, hs[h]))
+          return fail(RLKS_ERR_HIP, "node_rollout: lane-range node step");
+      }
+    }
+    for (int h = 0; h < 2; ++h) {
+      const size_t o = (size_t)b->T * N + lo[h];
+      if (int rc = forward(b->obs + o * D, nullptr, b->values + o, hi[h] - lo[h], hs[h])) return rc;
+    }
+    RLKS_HIP(hipEventRecord(env->ev_join, env->side));
+    RLKS_HIP(hipStreamWaitEvent(s, env->ev_join, 0));
+    return RLKS_OK;
+  }
   for (int t = 0; t < b->T; ++t) {
     const size_t tN = (size_t)t * N;
     if (int rc = forward(b->obs + tN * D, b->logits + tN * A, b->values + tN)) return rc;
@@ -831,6 +869,13 @@ struct FusedAdam {
                       // all-reduce follows; rlks_ppo_adam_apply then applies Adam)
 };
 
+// in-pipeline kernel timing (rlks_ppo_grad_profile): events recorded between sf_grad's launches while
+// a profile runs (null otherwise: one pointer test per mark)
+static hipEvent_t* g_prof_ev = nullptr;
+static void prof_mark(int i, hipStream_t s) {
+  if (g_prof_ev) (void)hipEventRecord(g_prof_ev[i], s);
+}
+
 // part: 0 = the whole gradient; 1 = the weight split, F1a, F2 and the reduce of W2 / b2 / W3 / b3 and
 // the stats; 2 = F1b and the reduce of W1 / b1 (rlks_ppo_grad_step_part: the caller all-reduces part
 // 1's buckets while part 2 runs)
@@ -844,11 +889,13 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
   const Layout L = make_layout(D, H, A);
   const bool f_pi = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_PI), f_vf = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_VF);
   if (part == 2) phases &= ~(RLKS_PHASE_PREP | RLKS_PHASE_DW2);
+  prof_mark(0, s);
   if ((phases & (RLKS_PHASE_FWD | RLKS_PHASE_PREP)) && part != 2) {
     const int parity = fa ? ((fa->step - 1) & 1) : 0;
     if (int rc = sf_prep(d, w, params, s, false, parity, fa && fa->prev_fused, fa ? (unsigned)fa->step : 0u))
       return rc;
   }
+  prof_mark(1, s);
   SfArgs a{};
   a.x = mb; a.x_stride = mb_stride(D, A); a.M = M; a.D = D; a.A_pi = A;
   a.tiles_per_split = w.tiles_per_split; a.co = *co; a.dyn = dyn;
@@ -865,28 +912,32 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
   if (!(f_pi || f_vf) && (phases & (RLKS_PHASE_F1A | RLKS_PHASE_F1B)))
     if (int rc = launch_sf_f1(a, 0, 2, A, s, (phases & RLKS_PHASE_F1A ? 1 : 0) | (phases & RLKS_PHASE_F1B ? 2 : 0)))
       return rc;
+  prof_mark(2, s);
   if (phases & RLKS_PHASE_DW2)
     if (int rc = launch_sf_dw2(a, w.splits, s)) return rc;
+  prof_mark(3, s);
   if (!(phases & RLKS_PHASE_REDUCE)) return RLKS_OK;
+  // F1's partial count: the fused kernel (whole gradient, one rank) has half the split kernels' workgroups
+  const int f1p = sf_f1_parts(M, part == 0 && sf_f1_fused());
   Reducer R;
   for (int net = 0; net < 2; ++net) {
     const int An = net == 0 ? A : 1;
     const int64_t* o = L.off + 6 * net;
     const SfNet& n = w.n[net];
     if (part != 1) {
-      R.add(n.part_w1, grad + o[0], nullptr, (int64_t)H * D, w.blocks, H * D, 2 * net + 1);
-      R.add(n.part_b1, grad + o[1], nullptr, H, w.blocks, H, 2 * net + 1);
+      R.add(n.part_w1, grad + o[0], nullptr, (int64_t)H * D, f1p, H * D, 2 * net + 1);
+      R.add(n.part_b1, grad + o[1], nullptr, H, f1p, H, 2 * net + 1);
     }
     if (part != 2) {
       R.add(n.part_w2, grad + o[2], nullptr, SF_W2_PSTRIDE, w.splits, H * H, 2 * net);
       R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
-      R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, w.fa_parts, An * H);
-      if (net == 0) R.add(n.part_b3, grad + o[5], nullptr, An, w.fa_parts, An);
-      else R.add(n.part_b3, grad + o[5], nullptr, 1, 2 * w.fa_parts, 1);  // every hi and lo, in f64
+      R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, f1p, An * H);
+      if (net == 0) R.add(n.part_b3, grad + o[5], nullptr, An, f1p, An);
+      else R.add(n.part_b3, grad + o[5], nullptr, 1, 2 * f1p, 1);  // every hi and lo, in f64
     }
   }
   if (stats && part != 2) {  // per-block columns [policy loss, vf loss, kl, entropy] -> RLKS_STAT_* directly
-    const int tiles = w.fa_parts;
+    const int tiles = f1p;
     R.add(w.n[0].part_stat + 0, nullptr, stats + RLKS_STAT_POLICY_LOSS, 4, tiles, 1);
     R.add(w.n[1].part_stat + 1, nullptr, stats + RLKS_STAT_VF_LOSS, 4, tiles, 1);
     R.add(w.n[0].part_stat + 2, nullptr, stats + RLKS_STAT_KL, 4, tiles, 1);
@@ -922,6 +973,7 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
   }
   RLKS_LAUNCHED();
+  prof_mark(4, s);
   return RLKS_OK;
 }
 
@@ -1008,6 +1060,40 @@ int rlks_ppo_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float
                   const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes,
                   void* stream) {
   return rlks_ppo_grad_phases(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, stream);
+}
+
+int rlks_ppo_grad_profile(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
+                          const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes,
+                          int reps, double* ms_out, void* stream) {
+  if (int rc = check_desc(d)) return rc;
+  RLKS_REQUIRE(is_sf(d) && !is_wide(d) && reps > 0 && ms_out && co && params && dyn && mb && grad && workspace,
+               RLKS_ERR_ARG, "rlks_ppo_grad_profile: split-fp16 descriptor, reps > 0");
+  hipStream_t s = (hipStream_t)stream;
+  constexpr int NE = 5;
+  hipEvent_t ev[2][NE];
+  for (int b = 0; b < 2; ++b)
+    for (int i = 0; i < NE; ++i)
+      if (hipEventCreate(&ev[b][i]) != hipSuccess) return fail(RLKS_ERR_HIP, "rlks_ppo_grad_profile: event");
+  for (int k = 0; k < NE - 1; ++k) ms_out[k] = 0.0;
+  int rc = RLKS_OK;
+  // one untimed pass, then reps timed ones, each read back before its events are reused
+  rc = sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, s);
+  for (int r = 0; r < reps && rc == RLKS_OK; ++r) {
+    g_prof_ev = ev[r & 1];
+    rc = sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, s);
+    g_prof_ev = nullptr;
+    if (rc) break;
+    (void)hipEventSynchronize(ev[r & 1][NE - 1]);
+    for (int k = 0; k < NE - 1; ++k) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, ev[r & 1][k], ev[r & 1][k + 1]);
+      ms_out[k] += ms / reps;
+    }
+  }
+  g_prof_ev = nullptr;
+  for (int b = 0; b < 2; ++b)
+    for (int i = 0; i < NE; ++i) (void)hipEventDestroy(ev[b][i]);
+  return rc;
 }
 
 static AdamCo adam_co(float lr, float beta1, float beta2, float eps, int step) {

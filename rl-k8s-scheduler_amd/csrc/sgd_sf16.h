@@ -4,7 +4,9 @@
 #include "mlp_common.h"
 
 namespace rlks {
-constexpr int SF_F1_W = 8;          // waves per F1 workgroup (two workgroups per CU); 16 rows each
+constexpr int SF_F1_W = 8;    // waves per F1a / F1b workgroup (two workgroups per CU); 16 rows each
+constexpr int SF_F1F_W = 16;  // waves per fused-F1 (k_sf_f1) workgroup: one workgroup per CU (sgd_sf16.hip)
+constexpr int SF_FWD_W = 8;   // waves per rollout-forward (k_sf_fwd16) workgroup (two per CU)
 constexpr int SF_PMAX = 1024;       // weight-max entries per (parity, kind)
 constexpr int SF_W2_PSTRIDE = 256 * 256;  // floats between F2's dW2 partials (padding them apart: no gain)
 }  // namespace rlks
@@ -94,7 +96,10 @@ int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
 // halves: 1 = F1a (k_sf_fwd), 2 = F1b (k_sf_bwd), 3 = both
 int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int halves = 3);  // needs M % 256 == 0
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
-// F1a's partials of dW3 / db3 / stats per net (one per F1 workgroup)
-int sf_f1a_parts(int M, int A);
+// F1's partials per net (one per F1 workgroup): dW1 / db1, and dW3 / db3 / stats; the workspace holds
+// the split kernels' count (the larger), the fused kernel writes half as many
+int sf_f1_parts(int M, bool fused);
+// whether launch_sf_f1(..., halves = 3) runs the fused kernel (RLKS_F1_SPLIT unset)
+bool sf_f1_fused();
 
 }  // namespace rlks

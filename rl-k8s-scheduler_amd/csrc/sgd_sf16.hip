@@ -480,6 +480,18 @@ __device__ __forceinline__ void hc_dma(const _Float16* hi, const _Float16* lo, i
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
   }
 }
+// the same copy as hc_dma through registers (global load -> ds_write): diagnostic builds only
+template <int W>
+__device__ __forceinline__ void hc_stage(const _Float16* hi, const _Float16* lo, int r0, int col, _Float16* buf, int w,
+                                         int l) {
+#pragma unroll
+  for (int i = 0; i < 16 / W; ++i) {
+    const int blk = (16 / W) * w + i, arr = blk >> 3, sig = (blk & 7) * 64 + l;
+    const int r = sig >> 2, q = (sig & 3) ^ sw16(r);
+    const _Float16* src = (arr ? lo : hi) + (r0 + r) * HID + col + 8 * q;
+    *reinterpret_cast<v4u*>(buf + arr * H16 + (blk & 7) * 512 + l * 8) = *reinterpret_cast<const v4u*>(src);
+  }
+}
 // (hi, lo) fragment of image row 16 j + c, piece g
 __device__ __forceinline__ void hc_frag(const _Float16* buf, int j, int c, int g, h8& fh, h8& fl) {
   const int off = (16 * j + c) * 32 + 8 * (g ^ sw16(c));
@@ -529,10 +541,22 @@ __device__ __forceinline__ void w1_frag(const _Float16* sW1, int kt, int c, int 
 // sum over the four 16-lane rows of a wave (lanes c, c + 16, c + 32, c + 48): every lane gets the
 // same bits
 __device__ __forceinline__ float sum_rows4(float v) {
+#if defined(RLKS_SUMROWS_SHFL)
+  v += __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+#elif defined(RLKS_SUMROWS_NOP)
+  float a = v, b = v;
+  asm volatile("s_nop 4\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 4" : "+v"(a), "+v"(b));
+  v = a + b;
+  a = v; b = v;
+  asm volatile("s_nop 4\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 4" : "+v"(a), "+v"(b));
+  return a + b;
+#else
   auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
   p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+#endif
 }
 // reduce-scatter of 16 per-lane values over the 16 lanes of a row: lane c of the row ends with the
 // row total of v[c] (DPP row_ror:8, row_half_mirror, quad_perm xor 2, xor 1; 43 VALU)
@@ -615,8 +639,8 @@ constexpr int f1b_lds_bytes() {
 //   dW3[A-1] = -sum_{a < A-1} dW3[a]
 // which is the same loss and gradient with A - 1 head rows instead of A (at 2 actions: half of the
 // head, of dZ2's products and of the dW3 reduce-scatter, the epilogue's largest part).  AH: head rows.
-template <int A_, int NET, int KD, int W, int P>
-__device__ __forceinline__ void f1a_body(const SfArgs& g, int grp) {
+template <int A_, int NET, int KD, int W, int P, bool OPQ = false>
+__device__ __forceinline__ int f1a_body(const SfArgs& g, int grp) {
   constexpr int NTHR = 64 * W;
   constexpr int AH = NET == 0 ? A_ - 1 : 1;
   const SfNet& N = g.n[NET];
@@ -628,7 +652,9 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g, int grp) {
   float* sW3 = sB2 + HID;
 
   // w wave-uniform (readfirstlane): tile bases stay in SGPRs, stores use a 32-bit lane offset
-  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
+  int tid = threadIdx.x;
+  if constexpr (OPQ) asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(tid));
+  const int l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
   // Prologue: every global load of the first group goes out before any result is used (the W2
   // half-chunk and W1a planes by LDS DMA, the tile's X rows, b2 and W3 into registers), so the
   // workgroup waits for one memory round trip instead of four in a row
@@ -880,6 +906,7 @@ __device__ __forceinline__ void f1a_body(const SfArgs& g, int grp) {
       vf_b3_part(vx, g.co.vf_loss_coeff, load_dyn(g).inv_count, N.part_b3 + (size_t)blk * 2);
     }
   }
+  return edz;  // (wave-uniform: the fused F1 hands it to f1b_body in a register)
 }
 
 // workgroup -> (net, tile group) for F1a / F1b launched as one row of G x nets workgroups.  Both
@@ -904,11 +931,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   else f1a_body<1, 1, KD, W, P>(g, ng.y);
 }
 
-// F1a's dW3 / db3 / stats partials per net: one per F1 workgroup
-int sf_f1a_parts(int M, int A) { return M / (16 * SF_F1_W); }
+int sf_f1_parts(int M, bool fused) { return M / (16 * (fused ? SF_F1F_W : SF_F1_W)); }
+bool sf_f1_fused() { return getenv("RLKS_F1_SPLIT") == nullptr; }
 
-template <int NET, int KD, int ND, int W, int P>
-__device__ __forceinline__ void f1b_body(const SfArgs& g, int grp) {  // ND = obs_dim + 1 (rows d of dW1a^T)
+// FUSED (k_sf_f1: right after f1a_body in the same workgroup): the tile's dZ2 exponent arrives in a
+// register (edz_in), and the W1a planes F1a staged are still in LDS when its epilogue slots stopped
+// short of them (W1_KEPT)
+template <int NET, int KD, int ND, int W, int P, bool FUSED = false, bool W1_KEPT = false>
+__device__ __forceinline__ void f1b_body(const SfArgs& g, int grp, int edz_in = 0) {  // ND = obs_dim + 1 (rows d of dW1a^T)
   constexpr int NTHR = 64 * W;
   constexpr int DT = KD / 16;                      // 16-row d-tiles of dW1a^T
   constexpr int SLOT = W * 16 * 16 * DT;           // floats per k-tile: [W][16 k][16 DT d]
@@ -920,16 +950,24 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g, int grp) {  // ND = ob
   _Float16* sW1 = sCh + 4 * H16;                      // [2 hi/lo][HID][KD]
   float* sEp = lds;                                   // epilogue slots (the chunk buffers)
 
-  // w wave-uniform (readfirstlane): tile bases stay in SGPRs, stores use a 32-bit lane offset
-  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
+  // w wave-uniform (readfirstlane): tile bases stay in SGPRs, stores use a 32-bit lane offset.  FUSED:
+  // the lane index through an opaque copy, so that the compiler derives F1b's lane offsets afresh
+  // instead of keeping F1a's alive across its epilogue (which spilled)
+  int tid = threadIdx.x;
+  if constexpr (FUSED) asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(tid));
+  const int l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
   int tile = grp * W + w;
   if (!dcheck(tile < g.M / 16, DC_SGD_TILE, tile)) tile = g.M / 16 - 1;
   const int row0 = tile * 16, blk = grp;
   const int D = g.D, stride = g.x_stride;
 
+#ifdef RLKS_F1_NODMA
+  if constexpr (FUSED) hc_stage<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
+  else
+#endif
   hc_dma<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
-  w1_stage<KD, NTHR>(N, sW1, tid);
-  const int edz = N.tile_edz[tile];
+  if constexpr (!W1_KEPT) w1_stage<KD, NTHR>(N, sW1, tid);
+  const int edz = FUSED ? edz_in : N.tile_edz[tile];
   const _Float16* dzp = N.dz2s + (size_t)tile * (16 * HID * 2) + l * 8;  // split by F1a at 2^edz
   h8 dh = *reinterpret_cast<const h8*>(dzp), dl = *reinterpret_cast<const h8*>(dzp + 512);
   vm_drain();
@@ -945,6 +983,10 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g, int grp) {  // ND = ob
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
       const int st = 2 * s + ph;
+#ifdef RLKS_F1_NODMA
+      if (FUSED && st < 15) hc_stage<W>(N.w2th, N.w2tl, 128 * (ph ^ 1), 32 * (s + ph), sCh + (ph ^ 1) * 2 * H16, w, l);
+      else
+#endif
       if (st < 15) hc_dma<W>(N.w2th, N.w2tl, 128 * (ph ^ 1), 32 * (s + ph), sCh + (ph ^ 1) * 2 * H16, w, l);
       if (ph == 0) {
         ah = dh;
@@ -1055,6 +1097,56 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   const int2 ng = f1_net_group<W, true>(g);
   if (ng.x + g.net0 == 0) f1b_body<0, KD, ND, W, P>(g, ng.y);
   else f1b_body<1, KD, ND, W, P>(g, ng.y);
+}
+
+// F1 fused: F1a then F1b on the same 16-row tiles in one workgroup.  The dZ2 hand-off is still
+// written for F2, but F1b reads each lane's own fragments back right after they were written (from the
+// XCD's L2, not HBM), the tile exponent stays in a register, the W1a planes stay in LDS (up to 4
+// actions), and there is one launch boundary (and its drain) less per SGD step.  A workgroup's F1b
+// loop (MFMA-dense) then runs beside its co-resident workgroup's F1a epilogue (VALU-heavy) whenever
+// the two drift out of phase, which the separate kernels never allowed.
+template <int A_, int KD, int W>
+constexpr bool f1_w1_kept() {  // F1a's epilogue slots end before the W1a planes (sW1 = 4 H16 halves in)
+#ifdef RLKS_F1_RESTAGE
+  return false;
+#endif
+  return W * (A_ - 1 > 1 ? A_ - 1 : 1) * HID * 4 + W * (A_ + 4) * 4 <= 4 * H16 * 2;
+}
+template <int A_, int KD, int W>
+constexpr int f1_lds_bytes() {
+#ifdef RLKS_F1_ONEWG
+  return 96 * 1024;
+#endif
+  return f1a_lds_bytes<A_, KD, W>() > f1b_lds_bytes<KD>() ? f1a_lds_bytes<A_, KD, W>() : f1b_lds_bytes<KD>();
+}
+#ifdef RLKS_F1_OPQ
+constexpr bool F1_OPQ = true;
+#else
+constexpr bool F1_OPQ = false;
+#endif
+template <int A_, int KD, int W, int P>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_f1(SfArgs g) {
+  const int2 ng = f1_net_group<W, (A_ <= 4)>(g);
+  // F1b's loads of the X rows are the ones F1a made: an opaque copy of the row pointer keeps the
+  // compiler from carrying F1a's values across the epilogue in registers (which spilled)
+  SfArgs g2 = g;
+  if (ng.x + g.net0 == 0) {
+    const int edz = f1a_body<A_, 0, KD, W, P, F1_OPQ>(g, ng.y);
+    __syncthreads();  // epilogue slots read; the dZ2 stores complete (the fence waits for them)
+#ifdef RLKS_F1_FENCE
+    __threadfence();
+#endif
+    asm volatile("" : "+s"(g2.x));
+    f1b_body<0, KD, 3 * A_ + 1, W, P, true, f1_w1_kept<A_, KD, W>()>(g2, ng.y, edz);
+  } else {
+    const int edz = f1a_body<1, 1, KD, W, P, F1_OPQ>(g, ng.y);
+    __syncthreads();
+#ifdef RLKS_F1_FENCE
+    __threadfence();
+#endif
+    asm volatile("" : "+s"(g2.x));
+    f1b_body<1, KD, 3 * A_ + 1, W, P, true, f1_w1_kept<1, KD, W>()>(g2, ng.y, edz);
+  }
 }
 
 // ----------------------------------------------------------------------------- F2
@@ -1568,6 +1660,13 @@ static int launch_f1_net_p(SfArgs a, int net0, int nets, hipStream_t s, int halv
   constexpr int W = SF_F1_W;
   a.net0 = net0;
   const dim3 grid(a.M / (16 * W) * nets);  // (f1_net_group)
+  if (halves == 3 && sf_f1_fused()) {  // one fused kernel (RLKS_F1_SPLIT: the two, A/B)
+    constexpr int WF = SF_F1F_W;
+    hipLaunchKernelGGL((k_sf_f1<A_, KD, WF, P>), dim3(a.M / (16 * WF) * nets), dim3(64 * WF), (f1_lds_bytes<A_, KD, WF>()), s,
+                       a);
+    RLKS_LAUNCHED();
+    return RLKS_OK;
+  }
   if (halves & 1) {  // pi's LDS (A_ >= 1) covers the value net's
     hipLaunchKernelGGL((k_sf_fwd<A_, KD, W, P>), grid, dim3(64 * W), (f1a_lds_bytes<A_, KD, W>()), s, a);
     RLKS_LAUNCHED();
@@ -1616,7 +1715,7 @@ int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {
 
 template <int A_, int KD>
 static int launch_fwd16_t(const SfFwdArgs& a, int net0, int nets, hipStream_t s) {
-  constexpr int W = SF_F1_W;
+  constexpr int W = SF_FWD_W;
   SfFwdArgs b = a;
   b.net0 = net0;
   hipLaunchKernelGGL((k_sf_fwd16<A_, KD, W>), dim3((a.M + 16 * W - 1) / (16 * W), nets), dim3(64 * W),

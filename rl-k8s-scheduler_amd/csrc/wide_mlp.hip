@@ -242,8 +242,8 @@ __global__ void k_wide_stats(const float* __restrict__ ps_pi, const float* __res
 // fused rollout kernels): action and its log-probability
 __global__ void k_wide_sample(EnvView v, const float* __restrict__ logits, int A, int explore,
                               int32_t* __restrict__ actions, float* __restrict__ logp) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= v.N) return;
+  const int m = v.lane0 + blockIdx.x * blockDim.x + threadIdx.x;  // (a lane range: node_rollout's halves)
+  if (m >= v.lane_end) return;
   const float* lg = logits + (size_t)m * A;
   float mx = lg[0];
   int amax = 0;
@@ -404,6 +404,108 @@ __global__ __launch_bounds__(256) void k_wide_vhead(const float* __restrict__ h2
   }
 }
 
+// The policy net's head out[m][a] = b3[a] + sum_n H2[m][n] W3[a][n] (A <= 32 NT actions, K = hidden):
+// a split-fp16 GEMM with whole H2 rows streamed straight into the MFMA operands (VERDICT r05 item 6:
+// the generic GEMM's 128-row tiles fetched 128-byte row pieces from 128 DRAM pages per chunk, 1.8 TB/s).
+// One wave per 32 rows, v_mfma_f32_32x32x16_f16: A = 32 rows x 16 k of H2 (lane: row l & 31, k = 8
+// (l >> 5) + 0..7: two float4 of its row), split at the fixed scale 2^14 (|tanh| < 1, like H1 in F1);
+// B = W3^T (lane: action 32 t + (l & 31), the same 8 k) from L2, split at the W3 slot's power of two.
+// Each k step is 3 MFMAs per action tile; H2 is read once (HBM-bound: 4 B x H per row).
+constexpr int PH_KU = 4;  // H2 k steps of 16 in flight per wave (a ring)
+__device__ __forceinline__ int ph_exp(float mx) {  // mx 2^e in [2^14, 2^15) (gemm_sf16.hip's operand scale)
+  if (!(mx > 0.f) || !(mx <= 3.4e38f)) return 0;
+  int e;
+  (void)frexpf(mx, &e);
+  return min(max(15 - e, -120), 120);
+}
+template <int NT>
+__global__ __launch_bounds__(256) void k_wide_phead(const float* __restrict__ h2, const float* __restrict__ w3,
+                                                    const float* __restrict__ b3, const unsigned* __restrict__ w3max,
+                                                    float* __restrict__ out, int M, int H, int A) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, r = l & 31, kg = l >> 5;
+  const int m0 = (blockIdx.x * 4 + w) * 32;
+  if (m0 >= M) return;
+  const float* hrow = h2 + (size_t)min(m0 + r, M - 1) * H + 8 * kg;
+  const int ew = ph_exp(__uint_as_float(*w3max));
+  const float sw = ldexpf(1.f, ew);
+  const float* wrow[NT];
+  float wsc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int a = 32 * t + r;
+    wrow[t] = w3 + (size_t)min(a, A - 1) * H + 8 * kg;
+    wsc[t] = a < A ? sw : 0.f;
+  }
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+  auto split8 = [](const float4& a, const float4& b, float sc, h8& hi, h8& lo) {
+    const float x[8] = {a.x * sc, a.y * sc, a.z * sc, a.w * sc, b.x * sc, b.y * sc, b.z * sc, b.w * sc};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const _Float16 h = (_Float16)x[j];
+      hi[j] = h;
+      lo[j] = (_Float16)(x[j] - (float)h);
+    }
+  };
+  // H2: a ring of PH_KU k steps in flight (the step u + PH_KU load is issued when step u is consumed;
+  // past the end the address is clamped and the data unused); W3: one step ahead
+  float4 xr[PH_KU][2], wc[NT][2];
+#pragma unroll
+  for (int u = 0; u < PH_KU; ++u) {
+    xr[u][0] = *reinterpret_cast<const float4*>(hrow + 16 * u);
+    xr[u][1] = *reinterpret_cast<const float4*>(hrow + 16 * u + 4);
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    wc[t][0] = *reinterpret_cast<const float4*>(wrow[t]);
+    wc[t][1] = *reinterpret_cast<const float4*>(wrow[t] + 4);
+  }
+  for (int k0 = 0; k0 < H; k0 += 16 * PH_KU) {
+#pragma unroll
+    for (int u = 0; u < PH_KU; ++u) {
+      const float4 x0 = xr[u][0], x1 = xr[u][1];
+      float4 w[NT][2];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) { w[t][0] = wc[t][0]; w[t][1] = wc[t][1]; }
+      const int kx = min(k0 + 16 * (u + PH_KU), H - 16), kw = min(k0 + 16 * (u + 1), H - 16);
+      xr[u][0] = *reinterpret_cast<const float4*>(hrow + kx);
+      xr[u][1] = *reinterpret_cast<const float4*>(hrow + kx + 4);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        wc[t][0] = *reinterpret_cast<const float4*>(wrow[t] + kw);
+        wc[t][1] = *reinterpret_cast<const float4*>(wrow[t] + kw + 4);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      h8 xh, xl;
+      split8(x0, x1, 16384.f, xh, xl);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        h8 bh, bl;
+        split8(w[t][0], w[t][1], wsc[t], bh, bl);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, bh, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, bl, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, bh, acc[t], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  const float un = ldexpf(1.f, -14 - ew);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int a = 32 * t + r;
+    if (a >= A) continue;
+    const float bb = b3[a];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int m = m0 + acc_row(q, l);
+      if (m < M) out[(size_t)m * A + a] = fmaf(acc[t][q], un, bb);
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- host
 namespace {
 
@@ -478,6 +580,14 @@ int forward_net(const rlks_mlp_desc* d, const Net& P, const WideNet& n, const fl
   }
   if (An == 1) {
     hipLaunchKernelGGL(k_wide_vhead, dim3(cdiv(M, 4 * VH_RPW)), dim3(256), 0, s, n.h2, P.w3, P.b3, n.out, M, H);
+    RLKS_LAUNCHED();
+    return RLKS_OK;
+  }
+  if (An <= 64 && H % (16 * PH_KU) == 0 && !getenv("RLKS_WIDE_HEAD_GEMM")) {  // (RLKS_WIDE_HEAD_GEMM: the generic GEMM, A/B)
+    if (An <= 32)
+      hipLaunchKernelGGL(k_wide_phead<1>, dim3(cdiv(M, 128)), dim3(256), 0, s, n.h2, P.w3, P.b3, sl + SL_W3, n.out, M, H, An);
+    else
+      hipLaunchKernelGGL(k_wide_phead<2>, dim3(cdiv(M, 128)), dim3(256), 0, s, n.h2, P.w3, P.b3, sl + SL_W3, n.out, M, H, An);
     RLKS_LAUNCHED();
     return RLKS_OK;
   }
@@ -600,7 +710,8 @@ int wide_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* pa
 
 int launch_sample(const EnvView& v, const float* logits, int A, int explore, int32_t* actions, float* logp,
                   hipStream_t s) {
-  hipLaunchKernelGGL(k_wide_sample, dim3(cdiv(v.N, 256)), dim3(256), 0, s, v, logits, A, explore, actions, logp);
+  hipLaunchKernelGGL(k_wide_sample, dim3(cdiv(v.lane_end - v.lane0, 256)), dim3(256), 0, s, v, logits, A, explore,
+                     actions, logp);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }

@@ -128,6 +128,7 @@ SIGNATURES = {
     "rlks_ppo_workspace_bytes": [C.POINTER(MlpDesc), _I, C.POINTER(_I64)],
     "rlks_ppo_grad": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _P],
     "rlks_ppo_grad_phases": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _I, _P],
+    "rlks_ppo_grad_profile": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _I, _P, _P],
     "rlks_adam_step": [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _I, _P],
     "rlks_ppo_sgd_step": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _P, _I64, _F, _F, _F,
                           _F, _I, _I, _P, _I64, _P],

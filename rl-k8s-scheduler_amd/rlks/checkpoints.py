@@ -69,9 +69,10 @@ def run_experiment(config, *, name: str = "FINAL_PPO_AWS_AZURE", stop_iterations
     """train_final.py's Tune run on one trial: train() until `stop_iterations`, save every
     `checkpoint_frequency` iterations and at the end, keep the `num_to_keep` newest checkpoints.
     Layout: <storage>/<name>/PPO_<env>_00000/checkpoint_<iteration:06d>.  Returns the last result,
-    the trial directory and the kept checkpoints (oldest first).  `reporter` is installed as the
-    algorithm's own (PPO.train() reports through it), unless the algorithm already has one
-    (PPOConfig.metrics_json_lines / RLKS_METRICS_JSONL): every iteration is reported once."""
+    the trial directory and the kept checkpoints (oldest first).  `reporter` receives every
+    iteration once; if the algorithm already has a reporter of its own (PPOConfig.metrics_json_lines /
+    RLKS_METRICS_JSONL), both receive it (a fan-out).  The algorithm's previous reporter is restored
+    when the run ends."""
     from .ppo import PPO
 
     root = Path(storage_path) if storage_path is not None else results_root()
@@ -79,8 +80,27 @@ def run_experiment(config, *, name: str = "FINAL_PPO_AWS_AZURE", stop_iterations
     trial = root / name / f"PPO_{env}_00000"
     trial.mkdir(parents=True, exist_ok=True)
     algo = algo if algo is not None else PPO(config=config, **ppo_kw)
-    if reporter is not None and getattr(algo, "reporter", None) is None:
-        algo.reporter = reporter
+    prev = getattr(algo, "reporter", None)
+    if reporter is not None:
+        algo.reporter = reporter if prev is None else FanOut(prev, reporter)
+    try:
+        return _run(algo, trial, stop_iterations, checkpoint_frequency, num_to_keep, checkpoint_at_end)
+    finally:
+        algo.reporter = prev
+
+
+class FanOut:
+    """several reporters as one: each report() goes to all of them, in order"""
+
+    def __init__(self, *reporters):
+        self.reporters = reporters
+
+    def report(self, result, algo):
+        for r in self.reporters:
+            r.report(result, algo)
+
+
+def _run(algo, trial, stop_iterations, checkpoint_frequency, num_to_keep, checkpoint_at_end):
     kept: list[Path] = []
     result = None
 

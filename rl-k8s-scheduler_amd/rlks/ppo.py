@@ -730,7 +730,13 @@ class PPO:
             ddp.group().barrier()
         return str(path)
 
-    def restore(self, checkpoint_path):
+    def restore(self, checkpoint_path, reset_optimizer=False):
+        """load a checkpoint written by save().  Adam moments are saved per tensor (round 5 on); an
+        older checkpoint's flat moments load only when it recorded the parameter layout they were
+        written in (param_offsets equal to this policy's).  A flat buffer without that record cannot
+        be placed safely (the flat layout order changed in round 4) and raises ValueError, unless
+        reset_optimizer=True: then the weights and counters load and the moments restart at zero
+        (with a warning), as a fresh Adam would."""
         import torch
 
         path = Path(checkpoint_path)
@@ -754,11 +760,18 @@ class PPO:
                 self.params.join(buf, per)
             elif meta.get("param_offsets") == list(self.params.offsets):
                 buf.copy_(tensors[k].to(self.device))  # a flat buffer saved with this very layout
+            elif reset_optimizer:
+                import warnings
+
+                warnings.warn(f"checkpoint {path}: Adam moments saved without their parameter layout; "
+                              "reset_optimizer=True: they restart at zero", RuntimeWarning, stacklevel=2)
+                buf.zero_()
             else:
                 # an older checkpoint: raw flat moments with no record of the storage order they were
                 # written in; copying them could land one tensor's moments on another silently
                 raise ValueError(f"checkpoint {path}: Adam moments saved as a flat buffer without their parameter "
-                                 "layout; cannot restore them safely")
+                                 "layout; cannot restore them safely (restore(..., reset_optimizer=True) loads the "
+                                 "weights and restarts Adam)")
         self.adam_step = int(meta["adam_step"])
         self.dyn[_lib.RLKS_DYN_KL_COEFF] = float(meta["kl_coeff"])
         self.iteration = int(meta["iteration"])

@@ -31,7 +31,9 @@ def _band(ref32):
     return [np.asarray(r, np.float64).ravel() for r in (ref32 if isinstance(ref32, (list, tuple)) else [ref32])]
 
 
-def rel_errors(x, ref64, ref32, floor=1e-6):
+def rel_errors(x, ref64, ref32, floor=1e-6, single=False):
+    """relative errors of x and of the fp32 band (element-wise worst evaluation) over the kept
+    elements; single=True also returns those of the band's first (plain) evaluation alone"""
     x, ref64 = (np.asarray(a, np.float64).ravel() for a in (x, ref64))
     band = _band(ref32)
     assert all(x.shape == ref64.shape == r.shape for r in band), (x.shape, ref64.shape, [r.shape for r in band])
@@ -39,7 +41,10 @@ def rel_errors(x, ref64, ref32, floor=1e-6):
     keep = np.abs(ref64) > floor * np.abs(ref64).max()
     den = np.abs(ref64[keep])
     e32 = np.max([np.abs(r - ref64)[keep] for r in band], axis=0) / den
-    return np.abs(x - ref64)[keep] / den, e32
+    e = np.abs(x - ref64)[keep] / den
+    if single:
+        return e, e32, np.abs(band[0] - ref64)[keep] / den
+    return e, e32
 
 
 def assert_pcts(e, e32, factor=4.0, what="", max_factor=None, floor=ULP2):
@@ -64,13 +69,14 @@ def grad_close_as_fp32(g, g64, g32, offsets, shapes, factor=4.0, floor=1e-6, sca
     """the gradient form of test_sf16_gradient_per_element.  g32: the fp32 band (or one evaluation).
 
     Pooled over all parameter tensors (the floor relative to each tensor's own max): the relative
-    error |g - g64| / |g64| no worse than the fp32 references' by `factor` at p50 / p99 / p99.9.
+    error |g - g64| / |g64| no worse than one plain fp32 evaluation's by `factor` at p50 / p99 and
+    than the fp32 band's at p99.9.
 
     Bias tensors, each on its own and unscaled (a bias gradient is a plain sum over the minibatch
     rows, so a coherent error shows there first: VERDICT r04 item 1): the relative error at p99
     within `tensor_factor` and at the maximum within `tensor_max_factor` of the fp32 references',
-    allowing only the result's own rounding to fp32 (2^-24: a one-element tensor such as the value
-    head's bias is a lottery below that for the fp32 references as well).
+    allowing the result's own rounding to fp32 (2^-24) only for tensors of fewer than 100 elements
+    (the value head's one-element bias is a lottery below that for the fp32 references as well).
 
     Weight tensors: every element against its own cancellation scale s (oracle.ppo_loss_grad(...,
     scale=True): the sum over the minibatch rows of the absolute per-row terms of that element):
@@ -78,12 +84,13 @@ def grad_close_as_fp32(g, g64, g32, offsets, shapes, factor=4.0, floor=1e-6, sca
     fp32 references', not asked to beat 2^-22 of it (the split representation's own error per row
     term).  Without `scale` the weight tensors take the bias tensors' unscaled form."""
     band = _band(g32)
-    es, e32s = [], []
+    es, e32s, e1s = [], [], []
     for i, shp in enumerate(shapes):
         o, n = offsets[i], int(np.prod(shp))
-        e, e32 = rel_errors(g[o:o + n], g64[o:o + n], [r[o:o + n] for r in band], floor)
+        e, e32, e1 = rel_errors(g[o:o + n], g64[o:o + n], [r[o:o + n] for r in band], floor, single=True)
         es.append(e)
         e32s.append(e32)
+        e1s.append(e1)
         if scale is not None and i not in BIAS:
             s = np.asarray(scale[o:o + n], np.float64)
             keep = s > 0
@@ -91,18 +98,21 @@ def grad_close_as_fp32(g, g64, g32, offsets, shapes, factor=4.0, floor=1e-6, sca
             es_ = np.abs(np.asarray(g[o:o + n], np.float64)[keep] - ref) / s[keep]
             e32_ = np.max([np.abs(r[o:o + n][keep] - ref) for r in band], axis=0) / s[keep]
             fl, kind = ULP2, " (scaled)"
-        else:  # (floor: the result's own rounding to fp32, half an ulp, which no fp32 output can beat)
-            es_, e32_, fl, kind = e, e32, ULP_OUT, ""
+        else:  # floor, only for a tensor of < 100 elements (the value head's one-element bias): the
+            # result's own rounding to fp32, half an ulp, which no fp32 output can beat there
+            es_, e32_, fl, kind = e, e32, (ULP_OUT if n < 100 else 0.0), ""
         if es_.size:
             assert es_.max() <= tensor_max_factor * e32_.max() + fl, \
                 f"tensor {i} max: {es_.max():.3e} vs fp32 {e32_.max():.3e}{kind}"
             if es_.size >= 100 or i in BIAS:
                 a, b = np.percentile(es_, 99), np.percentile(e32_, 99)
                 assert a <= tensor_factor * b + fl, f"tensor {i} p99: {a:.3e} vs fp32 {b:.3e}{kind}"
-    e, e32 = np.concatenate(es), np.concatenate(e32s)
+    # pooled: p50 / p99 against the single plain fp32 evaluation (over ~10^5 elements its percentiles
+    # are not luck: ADVICE r05), p99.9 against the band
+    e, e32, e1 = np.concatenate(es), np.concatenate(e32s), np.concatenate(e1s)
     for q in QS[:-1]:
-        a, b = np.percentile(e, q), np.percentile(e32, q)
-        assert a <= factor * b, f"pooled p{q}: {a:.3e} vs fp32 {b:.3e}"
+        a, b = np.percentile(e, q), np.percentile(e1 if q < 99.9 else e32, q)
+        assert a <= factor * b, f"pooled p{q}: {a:.3e} vs fp32 {b:.3e}{'' if q < 99.9 else ' (band)'}"
 
 
 def log_softmax(lo, dtype):

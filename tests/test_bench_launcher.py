@@ -58,3 +58,39 @@ def test_world_size_must_match_gpus():
 def test_strong_scaling_rejects_an_uneven_split():
     r = _bench("--dry-run", "--gpus", "3", "--scaling", "strong", "--steps", "1")
     assert r.returncode != 0 and "do not split over 3 ranks" in r.stderr
+
+
+def test_launcher_stops_the_others_when_a_later_rank_fails():
+    """every rank is polled in every pass, so rank 1 failing while rank 0 blocks at the
+    barrier ends the job promptly with rank 1's status (not at RCCL's watchdog, or never)."""
+    import time
+
+    t0 = time.monotonic()
+    r = _bench("--dry-run", "--gpus", "2", "--steps", "1", "--warmup", "0", env_extra={"RLKS_DRYRUN_FAIL_RANK": "1"},
+               timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert time.monotonic() - t0 < 60
+
+
+def test_launcher_parent_stays_hip_free():
+    """the launcher parent counts GPUs from sysfs and never initialises HIP (nor
+    imports torch) before it starts the ranks."""
+    code = ("import sys; sys.argv = ['bench.py']; import bench; "
+            "n = bench.visible_gpus(); "
+            "rc = bench.launch_ranks(2, ['--dry-run', '--gpus', '2', '--steps', '1', '--warmup', '0']); "
+            "assert rc == 0, rc; "
+            "assert 'torch' not in sys.modules, 'launcher parent imported torch'; "
+            "print('ok', n)")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["RLKS_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_visible_gpus_honours_the_visible_devices_list(monkeypatch):
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    assert bench.visible_gpus() == 3

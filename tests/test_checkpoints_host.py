@@ -88,3 +88,46 @@ def test_per_tensor_state_survives_a_layout_change():
         pass
     else:
         raise AssertionError("a shape mismatch must refuse")
+
+
+def test_run_experiment_fans_out_reporters_and_restores(tmp_path):
+    """a caller's reporter and the algorithm's own both receive every iteration, and the
+    algorithm's own is back in place when run_experiment returns (a fake algorithm: no GPU)"""
+    from rlks.checkpoints import run_experiment
+
+    class Rec:
+        def __init__(self):
+            self.seen = []
+
+        def report(self, result, algo):
+            self.seen.append(result["training_iteration"])
+
+    class FakeAlgo:
+        rank = 0
+
+        def __init__(self):
+            self.iteration = 0
+            self.reporter = Rec()
+
+        def train(self):
+            self.iteration += 1
+            r = {"training_iteration": self.iteration}
+            if self.reporter is not None:
+                self.reporter.report(r, self)
+            return r
+
+        def save(self, d):
+            p = Path(d) / f"checkpoint_{self.iteration:06d}"
+            p.mkdir(parents=True, exist_ok=True)
+            return str(p)
+
+    class Cfg:
+        env = "K8sMultiCloudEnv"
+
+    algo = FakeAlgo()
+    own, mine = algo.reporter, Rec()
+    out = run_experiment(Cfg(), stop_iterations=3, checkpoint_frequency=2, num_to_keep=5, storage_path=tmp_path,
+                         reporter=mine, algo=algo)
+    assert own.seen == [1, 2, 3] and mine.seen == [1, 2, 3]
+    assert algo.reporter is own
+    assert [Path(p).name for p in out["checkpoints"]] == ["checkpoint_000002", "checkpoint_000003"]

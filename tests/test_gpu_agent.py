@@ -531,3 +531,29 @@ def test_restore_warns_without_env_state(tmp_path):
     assert meta["state"]["env_state_saved"] is False
     with pytest.warns(RuntimeWarning, match="exact continuation"):
         PPO.from_checkpoint(path, device=d)
+
+
+def test_restore_of_flat_moments_without_layout(tmp_path):
+    """a checkpoint whose Adam moments are one flat buffer with no record of the layout
+    (written before round 5) is refused with a clear error, and restore(..., reset_optimizer=True)
+    loads its weights and restarts the moments at zero"""
+    from rlks.ppo import PPO
+
+    d = _dev()
+    a = PPO(config=_cfg(256, 8, 1024, epochs=1, seed=3), device=d)
+    a.train()
+    path = Path(a.save(tmp_path))
+    t = torch.load(path / "state.pt", weights_only=True)
+    flat = {k: v for k, v in t.items() if not (k.startswith("adam_m/") or k.startswith("adam_v/"))}
+    flat["adam_m"], flat["adam_v"] = a.adam_m.cpu().clone(), a.adam_v.cpu().clone()
+    torch.save(flat, path / "state.pt")
+    meta = json.loads((path / "algorithm_state.json").read_text())
+    meta["state"].pop("param_offsets", None)
+    (path / "algorithm_state.json").write_text(json.dumps(meta))
+    b = PPO(config=_cfg(256, 8, 1024, epochs=1, seed=3), device=d)
+    with pytest.raises(ValueError, match="parameter layout"):
+        b.restore(path)
+    with pytest.warns(RuntimeWarning, match="restart at zero"):
+        b.restore(path, reset_optimizer=True)
+    assert torch.equal(b.params.flat, a.params.flat)
+    assert float(b.adam_m.abs().sum()) == 0.0 and b.adam_step == a.adam_step

@@ -657,3 +657,41 @@ def test_ppo_iteration_parity_and_surface(tmp_path):
     algo2 = PPO.from_checkpoint(path, device=d)
     assert torch.equal(algo2.params.flat, algo.params.flat) and algo2.iteration == algo.iteration
     assert algo2.compute_single_action(np.full(6, 0.5, np.float32), explore=False) == a0
+
+
+@pytest.mark.parametrize("A", [2, 4, 8])
+def test_fused_f1_is_bit_identical_to_split_kernels(A, monkeypatch):
+    """the one-rank SGD step runs F1a + F1b as one kernel (k_sf_f1, 16-wave
+    workgroups).  Same arithmetic as the two kernels (RLKS_F1_SPLIT=1), so the whole gradient is bit
+    for bit theirs, and a rerun is bit for bit the first run, at the c4 minibatch (65,536 rows: every
+    CU runs two rounds of workgroups).  (An 8-wave form with two workgroups per CU was measured
+    non-deterministic in a few tiles a step: DESIGN.md §15.)"""
+    from rlks import _lib
+
+    d = _dev()
+    rows, D = 65536, 3 * A
+    p = _params(d, seed=rows + A, D=D, A=A)
+    p.desc.precision = _lib.RLKS_PRECISION_SF16
+    mb = _minibatch(rows, np.random.default_rng(rows + 1), D=D, A=A, p=p, d=d)
+    mbt = torch.from_numpy(mb).to(d)
+    dyn = torch.tensor([0.3, 0.7, 0.2, 1.0 / rows, 0, 0, 0, 0], dtype=torch.float32, device=d)
+    co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.01)
+    wsb = C.c_int64()
+    _lib.call("rlks_ppo_workspace_bytes", C.byref(p.desc), rows, C.byref(wsb))
+    ws = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
+
+    def grad():
+        g = torch.zeros(p.padded, device=d)
+        st = torch.zeros(8, dtype=torch.float64, device=d)
+        _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
+                  rows, g.data_ptr(), st.data_ptr(), ws.data_ptr(), ws.numel(), None)
+        torch.cuda.synchronize()
+        return g.cpu().numpy(), st.cpu().numpy()
+
+    monkeypatch.setenv("RLKS_F1_SPLIT", "1")
+    gs, ss = grad()
+    monkeypatch.delenv("RLKS_F1_SPLIT")
+    runs = [grad() for _ in range(3)]
+    for gf, sf in runs:
+        np.testing.assert_array_equal(gf.view(np.uint32), gs.view(np.uint32))
+        np.testing.assert_array_equal(sf.view(np.uint64), ss.view(np.uint64))

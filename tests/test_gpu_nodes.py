@@ -270,3 +270,38 @@ def test_node_rollout_full_c3_size():
         close_as_fp32(b["values"][t][rows], ev, fv, what=f"values[{t}]")
         if t < T:
             close_as_fp32(b["logits"][t][rows], el, fl, what=f"logits[{t}]")
+
+
+def test_node_rollout_two_streams_equal_one_stream(monkeypatch):
+    """node_rollout runs its lanes in two halves on two streams (one half's node
+    step beside the other half's forward).  With a lane count whose halves are ragged (12,000 lanes:
+    5,888 + 6,112) the rollout buffers and the env state equal the single-stream order's bit for bit,
+    and both replay in the C oracle"""
+    from rlks.env import NodeSpec
+    from rlks.ppo import PPO, PPOConfig
+    from rlks.tables import synthetic_table
+
+    d = _dev()
+    N, T, C = 12000, 16, 8
+    tab = synthetic_table(C, 100, seed=5)
+    spec = NodeSpec(C, 64, arrival_rate=1.5, depart_prob=0.03, init_occupancy=0.5)
+    out = []
+    for one in (True, False):
+        if one:
+            monkeypatch.setenv("RLKS_NODE_ONE_STREAM", "1")
+        else:
+            monkeypatch.delenv("RLKS_NODE_ONE_STREAM", raising=False)
+        cfg = (PPOConfig().framework("torch")
+               .training(train_batch_size=N * T, sgd_minibatch_size=N * T // 4, num_sgd_iter=1, lr=3e-4)
+               .debugging(seed=21))
+        cfg.num_envs, cfg.table, cfg.nodes = N, tab, spec
+        cfg.rollout_fragment_length = T
+        algo = PPO(config=cfg, device=d)
+        algo.rollout(explore=True)
+        algo.rollout(explore=True)  # the second one starts from the carried observations
+        torch.cuda.synchronize()
+        out.append(({k: v.cpu().numpy() for k, v in algo.buf.items()}, algo.env.save_state().cpu().numpy()))
+    (b1, s1), (b2, s2) = out
+    for k in b1:
+        np.testing.assert_array_equal(b1[k].view(np.uint8), b2[k].view(np.uint8), err_msg=k)
+    np.testing.assert_array_equal(s1, s2)

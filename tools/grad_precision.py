@@ -6,7 +6,8 @@ three fp32 evaluations; the diagnostic behind tests/parity.py's bias-tensor chec
   RLKS_LIB=<variant .so> python3 tools/grad_precision.py [--quick] [--json out.json]
 
 For every parameter tensor: the unscaled relative error |g - g64| / |g64| over the elements with
-|g64| > 1e-6 max|g64| at the maximum and p99, the fp32 reference's, and their ratios; and the
+|g64| > 1e-6 max|g64| at the maximum and p99, the fp32 reference's, and their ratios (against the band
+and, beside it, against a single plain fp32 evaluation: VERDICT r05 item 7); and the
 cancellation-scaled maximum (|g - g64| / sum_rows |terms|).  Test infrastructure (imports the
 oracle); never part of the product path."""
 import argparse
@@ -82,6 +83,7 @@ def run_case(path, rows, D, H, A, seed_off=0):
         keep = np.abs(b) > 1e-6 * np.abs(b).max()
         e = np.abs(a - b)[keep] / np.abs(b[keep])
         e32 = np.max([np.abs(r - b)[keep] for r in c], axis=0) / np.abs(b[keep])
+        e1 = np.abs(c[0] - b)[keep] / np.abs(b[keep])  # one plain fp32 evaluation (the band's first)
         ks = s > 0
         es = np.abs(a - b)[ks] / s[ks]
         es32 = np.max([np.abs(r - b)[ks] for r in c], axis=0) / s[ks]
@@ -89,10 +91,14 @@ def run_case(path, rows, D, H, A, seed_off=0):
                "rel_max": float(e.max()), "rel_max_fp32": float(e32.max()),
                "rel_p99": float(np.percentile(e, 99)), "rel_p99_fp32": float(np.percentile(e32, 99)),
                "rel_p50": float(np.percentile(e, 50)), "rel_p50_fp32": float(np.percentile(e32, 50)),
+               "rel_max_fp32_single": float(e1.max()), "rel_p99_fp32_single": float(np.percentile(e1, 99)),
+               "rel_p50_fp32_single": float(np.percentile(e1, 50)),
                "scaled_max": float(es.max()), "scaled_max_fp32": float(es32.max())}
         rec["max_ratio"] = rec["rel_max"] / max(rec["rel_max_fp32"], 1e-30)
         rec["p99_ratio"] = rec["rel_p99"] / max(rec["rel_p99_fp32"], 1e-30)
         rec["scaled_ratio"] = rec["scaled_max"] / max(rec["scaled_max_fp32"], 1e-30)
+        rec["max_ratio_single"] = rec["rel_max"] / max(rec["rel_max_fp32_single"], 1e-30)
+        rec["p99_ratio_single"] = rec["rel_p99"] / max(rec["rel_p99_fp32_single"], 1e-30)
         out.append(rec)
     return out
 
@@ -116,7 +122,8 @@ def main():
                 flag = " <" if (r["name"].split(".")[1].startswith("b") and (r["max_ratio"] > 8 or r["p99_ratio"] > 4)) else ""
                 print(f"  {r['tensor']:2d} {r['name']:6s} max {r['rel_max']:.2e}/{r['rel_max_fp32']:.2e}={r['max_ratio']:6.2f}"
                       f"  p99 {r['rel_p99']:.2e}/{r['rel_p99_fp32']:.2e}={r['p99_ratio']:5.2f}"
-                      f"  p50 {r['rel_p50']:.1e}/{r['rel_p50_fp32']:.1e}  scaled {r['scaled_ratio']:5.2f}{flag}", flush=True)
+                      f"  p50 {r['rel_p50']:.1e}/{r['rel_p50_fp32']:.1e}  scaled {r['scaled_ratio']:5.2f}"
+                      f"  | one fp32: max x{r['max_ratio_single']:6.2f} p99 x{r['p99_ratio_single']:5.2f}{flag}", flush=True)
     if args.json:
         Path(args.json).parent.mkdir(parents=True, exist_ok=True)
         Path(args.json).write_text(json.dumps(res, indent=1))

@@ -9,7 +9,7 @@ import json
 import sys
 
 # bench.py kernel name -> rocprofv3 kernel-name prefix
-NAMES = {"k_sf_fwd": "rlks::k_sf_fwd", "k_sf_split": "rlks::k_sf_split", "k_sf_bwd": "rlks::k_sf_bwd<", "k_sf_dw2": "rlks::k_sf_dw2", "k_reduce": "rlks::k_reduce",
+NAMES = {"k_sf_f1": "rlks::k_sf_f1<", "k_sf_fwd": "rlks::k_sf_fwd<", "k_sf_split": "rlks::k_sf_split", "k_sf_bwd": "rlks::k_sf_bwd<", "k_sf_dw2": "rlks::k_sf_dw2", "k_reduce": "rlks::k_reduce",
          "k_gather_packed": "rlks::k_gather_packed",
          "k_gae": "rlks::k_gae", "k_fwd_head_pi": "rlks::k_fwd_head<2, 0, 4, 2, 1", "k_dw2": "rlks::k_dw2",
          "k_dh1": "rlks::k_dh1", "k_node_step": "rlks::k_node_step"}
