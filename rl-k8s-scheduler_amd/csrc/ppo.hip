@@ -627,12 +627,14 @@ static int node_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* para
     return RLKS_OK;
   };
   const EnvView v = view(env);
-  // Two lane halves on two streams: each half runs forward -> sample -> node step
-  // on its own stream, so one half's latency-bound node step runs beside the other half's MFMA-bound
-  // forward instead of after it.  Same launches per lane, Philox counters per lane: the same rollout bit
-  // for bit (RLKS_NODE_ONE_STREAM: the single-stream order, A/B).
+  // Two lane halves on two streams (opt-in: RLKS_NODE_TWO_STREAMS=1): each half runs
+  // forward -> sample -> node step on its own stream, so that one half's latency-bound node step could
+  // run beside the other half's forward.  Same launches per lane, Philox counters per lane: the same
+  // rollout bit for bit.  Measured at c3 (profiles/r06_node): 12.9-13.0 ms a rollout against 12.7 ms in
+  // one stream -- the half-size forward keeps every CU's wave slots (4 waves per SIMD at 128
+  // registers), so the node step finds none free beside it and the split only adds its overheads.
   const int half = (N / 2) / 128 * 128;
-  if (w && N >= 8192 && env->cfg.nodes_per_cluster > 0 && env->cfg.n_clouds <= 64 && !getenv("RLKS_NODE_ONE_STREAM")) {
+  if (w && N >= 8192 && env->cfg.nodes_per_cluster > 0 && env->cfg.n_clouds <= 64 && getenv("RLKS_NODE_TWO_STREAMS")) {
     if (!env->side) {
       RLKS_HIP(hipStreamCreateWithFlags(&env->side, hipStreamNonBlocking));
       RLKS_HIP(hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));
@@ -905,9 +907,14 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     const NetPtrs P = net_ptrs_host(params, L, net);
     a.n[net].b2 = P.b2; a.n[net].w3 = P.w3; a.n[net].b3 = P.b3;
   }
-  // F1 (forward, loss, dZ2, dH1 -> dW1 / db1, dW3 / db3) per net; F2 (dW2, db2) for both
+  // F1 (forward, loss, dZ2, dH1 -> dW1 / db1, dW3 / db3) per net; F2 (dW2, db2) for both.  One fused
+  // kernel for a whole one-rank gradient (rlks_ppo_grad, the fused-Adam SGD step); the multi-rank step
+  // keeps the two kernels in both its forms (one bucket, or F1b overlapping the all-reduce: part 1 / 2),
+  // so that those two stay bit-identical to each other
+  const bool fused_f1 = part == 0 && !(fa && !fa->apply) && sf_f1_fused();
   if (f_pi || f_vf)
-    if (int rc = launch_sf_f1(a, f_pi ? 0 : 1, (f_pi && f_vf) ? 2 : 1, A, s, part == 0 ? 3 : part)) return rc;
+    if (int rc = launch_sf_f1(a, f_pi ? 0 : 1, (f_pi && f_vf) ? 2 : 1, A, s, fused_f1 ? SF_F1_FUSED : part == 0 ? 3 : part))
+      return rc;
   // split F1 halves alone, both nets (profiling: each reads what a full F1 left in the workspace)
   if (!(f_pi || f_vf) && (phases & (RLKS_PHASE_F1A | RLKS_PHASE_F1B)))
     if (int rc = launch_sf_f1(a, 0, 2, A, s, (phases & RLKS_PHASE_F1A ? 1 : 0) | (phases & RLKS_PHASE_F1B ? 2 : 0)))
@@ -917,8 +924,8 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     if (int rc = launch_sf_dw2(a, w.splits, s)) return rc;
   prof_mark(3, s);
   if (!(phases & RLKS_PHASE_REDUCE)) return RLKS_OK;
-  // F1's partial count: the fused kernel (whole gradient, one rank) has half the split kernels' workgroups
-  const int f1p = sf_f1_parts(M, part == 0 && sf_f1_fused());
+  // F1's partial count: the fused kernel has half the split kernels' workgroups
+  const int f1p = sf_f1_parts(M, fused_f1);
   Reducer R;
   for (int net = 0; net < 2; ++net) {
     const int An = net == 0 ? A : 1;

@@ -93,13 +93,14 @@ int launch_sf_fwd16(const SfFwdArgs& a, int A, hipStream_t s);
 
 int sf_kd(int D);
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
-// halves: 1 = F1a (k_sf_fwd), 2 = F1b (k_sf_bwd), 3 = both
+// halves: 1 = F1a (k_sf_fwd), 2 = F1b (k_sf_bwd), 3 = both, SF_F1_FUSED = the fused kernel (k_sf_f1)
+constexpr int SF_F1_FUSED = 7;
 int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int halves = 3);  // needs M % 256 == 0
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
 // F1's partials per net (one per F1 workgroup): dW1 / db1, and dW3 / db3 / stats; the workspace holds
 // the split kernels' count (the larger), the fused kernel writes half as many
 int sf_f1_parts(int M, bool fused);
-// whether launch_sf_f1(..., halves = 3) runs the fused kernel (RLKS_F1_SPLIT unset)
+// whether a one-rank gradient runs the fused kernel (RLKS_F1_SPLIT unset)
 bool sf_f1_fused();
 
 }  // namespace rlks

@@ -1660,7 +1660,7 @@ static int launch_f1_net_p(SfArgs a, int net0, int nets, hipStream_t s, int halv
   constexpr int W = SF_F1_W;
   a.net0 = net0;
   const dim3 grid(a.M / (16 * W) * nets);  // (f1_net_group)
-  if (halves == 3 && sf_f1_fused()) {  // one fused kernel (RLKS_F1_SPLIT: the two, A/B)
+  if (halves == SF_F1_FUSED) {  // one fused kernel
     constexpr int WF = SF_F1F_W;
     hipLaunchKernelGGL((k_sf_f1<A_, KD, WF, P>), dim3(a.M / (16 * WF) * nets), dim3(64 * WF), (f1_lds_bytes<A_, KD, WF>()), s,
                        a);

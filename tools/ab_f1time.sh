@@ -11,7 +11,7 @@ d=[json.loads(l) for l in open('$O/$n.txt') if l.startswith('{')][-1]
 k=d['kernels']; p=k.get('pipeline',{}).get('ms',{})
 print('$n', round(d['value']/1e6,3), 'grad', round(k['sgd_grad_total']['ms']*1e3,1), 'pipeline', {a:round(b*1e3,1) for a,b in p.items()})"
 }
-for i in 1 2; do
+for i in 1 2 3; do
   run split RLKS_F1_SPLIT=1 && run fused RLKS_X=0 || exit 1
   for L in "$@"; do run $L RLKS_LIB=$PWD/rl-k8s-scheduler_amd/rlks/$L || exit 1; done
 done
