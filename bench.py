@@ -306,15 +306,17 @@ def kernel_timing(algo, torch, config="c2", reps=20):
         # in-pipeline: every kernel of full gradients launched back to back as the SGD step runs them,
         # HIP events between the launches (rlks_ppo_grad_profile): the durations rocprofv3 sees, which
         # choose the roofline kernel (isolated repeats of one phase above are diagnostics only)
-        ms4 = (C.c_double * 4)()
+        ms5 = (C.c_double * 5)()
         _lib.call("rlks_ppo_grad_profile", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(), algo.dyn.data_ptr(),
                   algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, algo.ws.data_ptr(), algo.ws.numel(), reps,
-                  ms4, s.cuda_stream)
-        f1 = "k_sf_fwd+k_sf_bwd" if os.environ.get("RLKS_F1_SPLIT") else "k_sf_f1"
-        pipe = {"k_sf_prep": ms4[0], f1: ms4[1], "k_sf_dw2": ms4[2], "k_reduce": ms4[3]}
+                  ms5, s.cuda_stream)
+        fused = bool(os.environ.get("RLKS_F1_FUSED"))
+        f1 = ("k_sf_f1",) if fused else ("k_sf_fwd", "k_sf_bwd")
+        pipe = {"k_sf_prep": ms5[0], f1[0]: ms5[1], **({} if fused else {"k_sf_bwd": ms5[2]}),
+                "k_sf_dw2": ms5[3], "k_reduce": ms5[4]}
         rec = {"ms": pipe, "method": f"{reps} full gradients, HIP events between the launches"}
-        for name, fl in ((f1, flops_per_row("k_sf_f1", D, H, A)), ("k_sf_dw2", flops_per_row("k_sf_dw2", D, H, A))):
-            tf = fl * algo.mb / (pipe[name] * 1e-3) / 1e12
+        for name in (*f1, "k_sf_dw2"):
+            tf = flops_per_row(name, D, H, A) * algo.mb / (pipe[name] * 1e-3) / 1e12
             rec[name] = {"ms": pipe[name], "tflops": tf, peak_name: tf / peak}
         out["pipeline"] = rec
     ms = timed(lambda: _lib.call("rlks_ppo_grad", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(),
@@ -694,9 +696,9 @@ def main():
                 # the whole SGD step against its compulsory bytes: the minibatch records read once, the
                 # parameters read by the weight split, and Adam (p, m, v read + written, the gradient
                 # written and read): everything else is a hand-off between the step's own kernels
-                step = [k for k in ("k_sf_split", "k_sf_f1", "k_sf_dw2", "k_reduce") if k in pmc]
-                if "k_sf_f1" not in pmc or os.environ.get("RLKS_F1_SPLIT"):
-                    step = [k for k in ("k_sf_split", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce") if k in pmc]
+                step = [k for k in ("k_sf_split", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce") if k in pmc]
+                if os.environ.get("RLKS_F1_FUSED") and "k_sf_f1" in pmc:
+                    step = [k for k in ("k_sf_split", "k_sf_f1", "k_sf_dw2", "k_reduce") if k in pmc]
                 moved = sum(pmc[k]["hbm_bytes_per_launch"] for k in step)
                 P = algo.params.padded
                 comp = algo.mb * algo.stride * 4 + P * 4 + (6 + 2) * P * 4

@@ -907,22 +907,30 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     const NetPtrs P = net_ptrs_host(params, L, net);
     a.n[net].b2 = P.b2; a.n[net].w3 = P.w3; a.n[net].b3 = P.b3;
   }
-  // F1 (forward, loss, dZ2, dH1 -> dW1 / db1, dW3 / db3) per net; F2 (dW2, db2) for both.  One fused
-  // kernel for a whole one-rank gradient (rlks_ppo_grad, the fused-Adam SGD step); the multi-rank step
-  // keeps the two kernels in both its forms (one bucket, or F1b overlapping the all-reduce: part 1 / 2),
-  // so that those two stay bit-identical to each other
+  // F1 (forward, loss, dZ2, dH1 -> dW1 / db1, dW3 / db3) per net; F2 (dW2, db2) for both.  F1 is the
+  // two kernels F1a, F1b; RLKS_F1_FUSED=1 runs the fused kernel for a whole one-rank gradient
+  // (rlks_ppo_grad, the fused-Adam SGD step) -- the multi-rank step keeps the two kernels in both its
+  // forms (one bucket, or F1b overlapping the all-reduce: part 1 / 2), so that those stay bit-identical
   const bool fused_f1 = part == 0 && !(fa && !fa->apply) && sf_f1_fused();
-  if (f_pi || f_vf)
-    if (int rc = launch_sf_f1(a, f_pi ? 0 : 1, (f_pi && f_vf) ? 2 : 1, A, s, fused_f1 ? SF_F1_FUSED : part == 0 ? 3 : part))
-      return rc;
+  if (f_pi || f_vf) {
+    const int net0 = f_pi ? 0 : 1, nets = (f_pi && f_vf) ? 2 : 1;
+    if (fused_f1 || part != 0) {
+      if (int rc = launch_sf_f1(a, net0, nets, A, s, fused_f1 ? SF_F1_FUSED : part)) return rc;
+    } else {  // F1a, then F1b (a profiling mark between them)
+      if (int rc = launch_sf_f1(a, net0, nets, A, s, 1)) return rc;
+      prof_mark(2, s);
+      if (int rc = launch_sf_f1(a, net0, nets, A, s, 2)) return rc;
+    }
+  }
   // split F1 halves alone, both nets (profiling: each reads what a full F1 left in the workspace)
   if (!(f_pi || f_vf) && (phases & (RLKS_PHASE_F1A | RLKS_PHASE_F1B)))
     if (int rc = launch_sf_f1(a, 0, 2, A, s, (phases & RLKS_PHASE_F1A ? 1 : 0) | (phases & RLKS_PHASE_F1B ? 2 : 0)))
       return rc;
-  prof_mark(2, s);
+  if (g_prof_ev && fused_f1) prof_mark(2, s);  // (no F1b launch: an empty interval)
+  prof_mark(3, s);
   if (phases & RLKS_PHASE_DW2)
     if (int rc = launch_sf_dw2(a, w.splits, s)) return rc;
-  prof_mark(3, s);
+  prof_mark(4, s);
   if (!(phases & RLKS_PHASE_REDUCE)) return RLKS_OK;
   // F1's partial count: the fused kernel has half the split kernels' workgroups
   const int f1p = sf_f1_parts(M, fused_f1);
@@ -980,7 +988,7 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
   }
   RLKS_LAUNCHED();
-  prof_mark(4, s);
+  prof_mark(5, s);
   return RLKS_OK;
 }
 
@@ -1076,7 +1084,7 @@ int rlks_ppo_grad_profile(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, con
   RLKS_REQUIRE(is_sf(d) && !is_wide(d) && reps > 0 && ms_out && co && params && dyn && mb && grad && workspace,
                RLKS_ERR_ARG, "rlks_ppo_grad_profile: split-fp16 descriptor, reps > 0");
   hipStream_t s = (hipStream_t)stream;
-  constexpr int NE = 5;
+  constexpr int NE = 6;
   hipEvent_t ev[2][NE];
   for (int b = 0; b < 2; ++b)
     for (int i = 0; i < NE; ++i)

@@ -100,7 +100,8 @@ int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
 // F1's partials per net (one per F1 workgroup): dW1 / db1, and dW3 / db3 / stats; the workspace holds
 // the split kernels' count (the larger), the fused kernel writes half as many
 int sf_f1_parts(int M, bool fused);
-// whether a one-rank gradient runs the fused kernel (RLKS_F1_SPLIT unset)
+// whether a one-rank gradient runs the fused kernel (opt-in: RLKS_F1_FUSED set; measured no faster
+// than the two kernels)
 bool sf_f1_fused();
 
 }  // namespace rlks

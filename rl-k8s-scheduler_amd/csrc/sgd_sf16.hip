@@ -932,7 +932,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 }
 
 int sf_f1_parts(int M, bool fused) { return M / (16 * (fused ? SF_F1F_W : SF_F1_W)); }
-bool sf_f1_fused() { return getenv("RLKS_F1_SPLIT") == nullptr; }
+bool sf_f1_fused() { return getenv("RLKS_F1_FUSED") != nullptr; }
 
 // FUSED (k_sf_f1: right after f1a_body in the same workgroup): the tile's dZ2 exponent arrives in a
 // register (edz_in), and the W1a planes F1a staged are still in LDS when its epilogue slots stopped
@@ -1099,12 +1099,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   else f1b_body<1, KD, ND, W, P>(g, ng.y);
 }
 
-// F1 fused: F1a then F1b on the same 16-row tiles in one workgroup.  The dZ2 hand-off is still
-// written for F2, but F1b reads each lane's own fragments back right after they were written (from the
-// XCD's L2, not HBM), the tile exponent stays in a register, the W1a planes stay in LDS (up to 4
-// actions), and there is one launch boundary (and its drain) less per SGD step.  A workgroup's F1b
-// loop (MFMA-dense) then runs beside its co-resident workgroup's F1a epilogue (VALU-heavy) whenever
-// the two drift out of phase, which the separate kernels never allowed.
+// F1 fused (opt-in, RLKS_F1_FUSED=1): F1a then F1b on the same 16-row tiles in one
+// workgroup.  The dZ2 hand-off is still written for F2, but F1b reads each lane's own fragments back
+// right after they were written (from the XCD's L2, not HBM), the tile exponent stays in a register,
+// the W1a planes stay in LDS (up to 4 actions), and there is one launch boundary less per SGD step.
+// Launched with 16-wave workgroups, one per CU (SF_F1F_W): with two 8-wave workgroups per CU in
+// different phases a few policy tiles a step came out different from run to run (cause not isolated).
+// Measured no faster than the two kernels (126-128 µs against 126 µs for the pair at c4).
 template <int A_, int KD, int W>
 constexpr bool f1_w1_kept() {  // F1a's epilogue slots end before the W1a planes (sW1 = 4 H16 halves in)
 #ifdef RLKS_F1_RESTAGE

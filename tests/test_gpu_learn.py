@@ -438,13 +438,15 @@ def test_packed_gather_equals_direct_gather(D, A, T, N, groups):
     assert bool((packed[:, stride:] == 0).all())
 
 
-@pytest.mark.parametrize("A", [2, 8])
-def test_fused_sgd_step_equals_grad_then_adam(A):
+@pytest.mark.parametrize("A,f1", [(2, "split"), (8, "split"), (2, "fused")])
+def test_fused_sgd_step_equals_grad_then_adam(A, f1, monkeypatch):
     """rlks_ppo_sgd_step (Adam inside the gradient reduction, the next step's weight maxima from
     its slots) and the multi-rank pair rlks_ppo_grad_step + rlks_ppo_adam_apply (an all-reduce goes
     between them) give the parameters, Adam moments and gradients of rlks_ppo_grad + rlks_adam_step,
     bit for bit, over consecutive steps -- including a first step that claims prev_fused with no
-    fused predecessor (the device-side tag check falls back to scanning the weights)"""
+    fused predecessor (the device-side tag check falls back to scanning the weights).  f1 = "fused":
+    the one-rank step and rlks_ppo_grad run the fused F1 kernel (RLKS_F1_FUSED=1) while the
+    multi-rank pair always runs the two F1 kernels, so its reference is then rlks_ppo_grad without it"""
     from rlks import _lib
     from rlks.policy import PolicyParams
 
@@ -457,7 +459,9 @@ def test_fused_sgd_step_equals_grad_then_adam(A):
     p_ref = PolicyParams(D, 256, A, device=d, seed=3)
     p_fus = PolicyParams(D, 256, A, device=d, seed=3)
     p_spl = PolicyParams(D, 256, A, device=d, seed=3)
+    p_rs = PolicyParams(D, 256, A, device=d, seed=3)  # the split-kernel reference of the multi-rank pair
     p_ref.desc.precision = p_fus.desc.precision = p_spl.desc.precision = _lib.RLKS_PRECISION_SF16
+    p_rs.desc.precision = _lib.RLKS_PRECISION_SF16
     P = p_ref.padded
     dyn = torch.tensor([0.1, 1.3, 0.2, 1.0 / M, 0, 0, 0, 0], dtype=torch.float32, device=d)
     wsb = C.c_int64()
@@ -465,11 +469,15 @@ def test_fused_sgd_step_equals_grad_then_adam(A):
     ws_ref = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
     ws_fus = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
     ws_spl = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
+    ws_rs = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
     st = {k: torch.zeros(P, device=d) for k in ("m_ref", "v_ref", "g_ref", "m_fus", "v_fus", "g_fus", "m_spl", "v_spl",
-                                                 "g_spl")}
+                                                 "g_spl", "m_rs", "v_rs", "g_rs")}
+    stats_rs = torch.zeros(8, dtype=torch.float64, device=d)
     stats_ref = torch.zeros(8, dtype=torch.float64, device=d)
     stats_fus = torch.zeros(8, dtype=torch.float64, device=d)
     stats_spl = torch.zeros(8, dtype=torch.float64, device=d)
+    if f1 == "fused":
+        monkeypatch.setenv("RLKS_F1_FUSED", "1")
     for step in range(1, 6):
         mb = torch.zeros(M, stride, device=d)
         mb[:, :D] = torch.rand(M, D, generator=g, device=d)
@@ -482,6 +490,14 @@ def test_fused_sgd_step_equals_grad_then_adam(A):
                   st["g_ref"].data_ptr(), stats_ref.data_ptr(), ws_ref.data_ptr(), ws_ref.numel(), None)
         _lib.call("rlks_adam_step", p_ref.flat.data_ptr(), st["g_ref"].data_ptr(), st["m_ref"].data_ptr(),
                   st["v_ref"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, None)
+        monkeypatch.delenv("RLKS_F1_FUSED", raising=False)
+        _lib.call("rlks_ppo_grad", C.byref(desc), C.byref(co), p_rs.flat.data_ptr(), dyn.data_ptr(), mb.data_ptr(), M,
+                  st["g_rs"].data_ptr(), stats_rs.data_ptr(), ws_rs.data_ptr(), ws_rs.numel(), None)
+        torch.cuda.synchronize()
+        if f1 == "fused":
+            monkeypatch.setenv("RLKS_F1_FUSED", "1")
+        _lib.call("rlks_adam_step", p_rs.flat.data_ptr(), st["g_rs"].data_ptr(), st["m_rs"].data_ptr(),
+                  st["v_rs"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, None)
         _lib.call("rlks_ppo_sgd_step", C.byref(desc), C.byref(co), p_fus.flat.data_ptr(), dyn.data_ptr(),
                   mb.data_ptr(), M, st["g_fus"].data_ptr(), stats_fus.data_ptr(), st["m_fus"].data_ptr(),
                   st["v_fus"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, 1, ws_fus.data_ptr(), ws_fus.numel(),
@@ -494,13 +510,13 @@ def test_fused_sgd_step_equals_grad_then_adam(A):
                   st["m_spl"].data_ptr(), st["v_spl"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, ws_spl.data_ptr(),
                   ws_spl.numel(), M, None)
         assert torch.equal(st["g_spl"].view(torch.int32), g_summed.view(torch.int32)), step
-        for sfx in ("fus", "spl"):
+        for ref, sfx in (("ref", "fus"), ("rs", "spl")):
             for k in ("g", "m", "v"):
-                assert torch.equal(st[k + "_ref"].view(torch.int32), st[k + "_" + sfx].view(torch.int32)), (step, k, sfx)
+                assert torch.equal(st[k + "_" + ref].view(torch.int32), st[k + "_" + sfx].view(torch.int32)), (step, k, sfx)
         assert torch.equal(p_ref.flat.view(torch.int32), p_fus.flat.view(torch.int32)), step
-        assert torch.equal(p_ref.flat.view(torch.int32), p_spl.flat.view(torch.int32)), step
+        assert torch.equal(p_rs.flat.view(torch.int32), p_spl.flat.view(torch.int32)), step
         assert torch.equal(stats_ref, stats_fus)
-        assert torch.equal(stats_ref, stats_spl)
+        assert torch.equal(stats_rs, stats_spl)
 
 
 @pytest.mark.parametrize("A,groups", [(2, 1), (4, 2), (2, 16)])
@@ -661,13 +677,12 @@ def test_ppo_iteration_parity_and_surface(tmp_path):
 
 @pytest.mark.parametrize("A", [2, 4, 8])
 def test_fused_f1_is_deterministic_and_matches_split_kernels(A, monkeypatch):
-    """the one-rank SGD step runs F1a + F1b as one kernel (k_sf_f1, 16-wave
-    workgroups, one per CU).  At the c4 minibatch (65,536 rows: two rounds of workgroups) three runs
-    are bit for bit the same, and the gradient equals the two split kernels' (RLKS_F1_SPLIT=1, 8-wave
-    workgroups) up to the order of the workgroup sums (16 waves' slots added in LDS instead of 8 +
-    twice the partials).  (The fused kernel on 8-wave workgroups, two per CU, was measured
-    non-deterministic in a few tiles a step: DESIGN.md §15.)  Parity against the fp64 oracle:
-    test_ppo_grad_matches_oracle, which runs the fused kernel."""
+    """F1a + F1b as one kernel (k_sf_f1, 16-wave workgroups, one per CU; opt-in,
+    RLKS_F1_FUSED=1: measured no faster than the two kernels).  At the c4 minibatch (65,536 rows: two
+    rounds of workgroups) three runs are bit for bit the same, and the gradient equals the two split
+    kernels' (8-wave workgroups, the default) up to the order of the workgroup sums (16 waves' slots
+    added in LDS instead of 8, and half as many partials).  (The fused kernel on 8-wave workgroups, two per CU, was measured
+    non-deterministic in a few tiles a step: DESIGN.md §15.)"""
     from rlks import _lib
     from rlks.policy import TENSOR_NAMES
 
@@ -691,9 +706,8 @@ def test_fused_f1_is_deterministic_and_matches_split_kernels(A, monkeypatch):
         torch.cuda.synchronize()
         return g.cpu().numpy(), st.cpu().numpy()
 
-    monkeypatch.setenv("RLKS_F1_SPLIT", "1")
     gs, ss = grad()
-    monkeypatch.delenv("RLKS_F1_SPLIT")
+    monkeypatch.setenv("RLKS_F1_FUSED", "1")
     runs = [grad() for _ in range(3)]
     for gf, sf in runs[1:]:
         np.testing.assert_array_equal(gf.view(np.uint32), runs[0][0].view(np.uint32))

@@ -1,5 +1,5 @@
 #!/bin/bash
-# timing only: the c4 SGD-step kernels with the fused F1 (default), the two F1 kernels (RLKS_F1_SPLIT=1)
+# timing only: the c4 SGD-step kernels with the two F1 kernels (default), the fused F1 (RLKS_F1_FUSED=1)
 # and the given variant libraries, one box
 O=gpurun_out/f1time; mkdir -p $O
 run() {  # name, env...
@@ -12,6 +12,6 @@ k=d['kernels']; p=k.get('pipeline',{}).get('ms',{})
 print('$n', round(d['value']/1e6,3), 'grad', round(k['sgd_grad_total']['ms']*1e3,1), 'pipeline', {a:round(b*1e3,1) for a,b in p.items()})"
 }
 for i in 1 2 3; do
-  run split RLKS_F1_SPLIT=1 && run fused RLKS_X=0 || exit 1
+  run split RLKS_X=0 && run fused RLKS_F1_FUSED=1 || exit 1
   for L in "$@"; do run $L RLKS_LIB=$PWD/rl-k8s-scheduler_amd/rlks/$L || exit 1; done
 done

@@ -1,5 +1,5 @@
-"""fused F1 (k_sf_f1) vs the two kernels (RLKS_F1_SPLIT=1): same arithmetic, so the gradients must be
-bit-identical.  Prints per tensor the max |fused - split| at several minibatch sizes."""
+"""fused F1 (k_sf_f1, RLKS_F1_FUSED=1) vs the two kernels (the default): the same arithmetic, so with the
+same workgroup size the gradients must be bit-identical.  Prints per tensor the max |fused - split| at several minibatch sizes."""
 import ctypes as C
 import os
 import sys
@@ -43,10 +43,10 @@ def main():
             mbt = torch.from_numpy(mb).to(d)
             dyn = torch.tensor([0.3, 0.7, 0.2, 1.0 / rows, 0, 0, 0, 0], dtype=torch.float32, device=d)
             co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.01)
-            os.environ["RLKS_F1_SPLIT"] = "1"
+            os.environ.pop("RLKS_F1_FUSED", None)
             gs = grad(p, mbt, rows, co, dyn, d)
             srep = float(np.abs(gs - grad(p, mbt, rows, co, dyn, d)).max())
-            os.environ.pop("RLKS_F1_SPLIT")
+            os.environ["RLKS_F1_FUSED"] = "1"
             gf = grad(p, mbt, rows, co, dyn, d)
             gf2 = grad(p, mbt, rows, co, dyn, d)
             out = []

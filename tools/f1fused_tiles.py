@@ -15,6 +15,7 @@ from test_gpu_learn import _minibatch, _params  # noqa: E402
 def main():
     from rlks import _lib
 
+    os.environ["RLKS_F1_FUSED"] = "1"
     d = torch.device("cuda", 0)
     A = int(os.environ.get("F1_A", "2"))
     rows = int(os.environ.get("F1_ROWS", "65536"))

@@ -10,7 +10,7 @@ import json
 import sys
 from collections import defaultdict
 
-KEEP = ("k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce", "k_sf_split", "k_gather")
+KEEP = ("k_sf_f1", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce", "k_sf_split", "k_gather")
 
 
 def short(name):
