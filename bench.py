@@ -306,7 +306,7 @@ def kernel_timing(algo, torch, config="c2", reps=20):
         # in-pipeline: every kernel of full gradients launched back to back as the SGD step runs them,
         # HIP events between the launches (rlks_ppo_grad_profile): the durations rocprofv3 sees, which
         # choose the roofline kernel (isolated repeats of one phase above are diagnostics only)
-        ms5 = (C.c_double * 5)()
+        ms5 = (C.c_double * 6)()
         _lib.call("rlks_ppo_grad_profile", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(), algo.dyn.data_ptr(),
                   algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, algo.ws.data_ptr(), algo.ws.numel(), reps,
                   ms5, s.cuda_stream)
@@ -314,7 +314,9 @@ def kernel_timing(algo, torch, config="c2", reps=20):
         f1 = ("k_sf_f1",) if fused else ("k_sf_fwd", "k_sf_bwd")
         pipe = {"k_sf_prep": ms5[0], f1[0]: ms5[1], **({} if fused else {"k_sf_bwd": ms5[2]}),
                 "k_sf_dw2": ms5[3], "k_reduce": ms5[4]}
-        rec = {"ms": pipe, "method": f"{reps} full gradients, HIP events between the launches"}
+        rec = {"ms": pipe, "event_bracket_ms": ms5[5],
+               "method": f"{reps} full rlks_ppo_grad passes, each kernel launched between its own start / stop "
+                         "events (hipExtLaunchKernelGGL), less the same bracket's time around an empty kernel"}
         for name in (*f1, "k_sf_dw2"):
             tf = flops_per_row(name, D, H, A) * algo.mb / (pipe[name] * 1e-3) / 1e12
             rec[name] = {"ms": pipe[name], "tflops": tf, peak_name: tf / peak}
@@ -653,9 +655,14 @@ def main():
             # the dominant kernel as rocprofv3 --stats ranks them: largest share of GPU time (each
             # runs once per SGD step, so: the longest launch), timed in the pipeline where there is one
             if "pipeline" in kernels:
+                # the kernel: the longest in the pipeline (kernel-bracketing events: they rank the kernels as
+                # rocprofv3 does); its duration: 20 back-to-back launches of it alone (HIP events around the
+                # batch), which matched rocprofv3's in-pipeline average within 1% on the boxes measured
+                # (66.7 vs 66.7 µs, 68.8 vs 69.0 µs; profiles/r06_trace) -- the bracketed figure carries the
+                # bracket's own few µs, reported beside it
                 pk = {n: v for n, v in kernels["pipeline"].items() if isinstance(v, dict) and "tflops" in v}
                 dom = max(pk, key=lambda n: pk[n]["ms"])
-                k = pk[dom]
+                k = kernels[dom] if dom in kernels and "tflops" in kernels[dom] else pk[dom]
             else:
                 cands = [k for k in kernels if k in ROOFLINE_KERNELS]
                 dom = max(cands, key=lambda k: kernels[k]["ms"])
@@ -671,6 +678,11 @@ def main():
                                        "split-fp16: 2.5 PF dense f16 MFMA / 3 products per fp32-accurate FLOP")}
             if dom == "wide_grad":
                 roofline["note"] = "generic-width path: the whole SGD-step gradient (a sequence of split-fp16 GEMM launches)"
+            if "pipeline" in kernels:
+                roofline["avg_launch_ms_method"] = ("20 back-to-back launches of the kernel (HIP events on its stream); "
+                                                    "chosen as the longest kernel of the SGD step in the pipeline")
+                roofline["avg_launch_ms_pipeline"] = kernels["pipeline"]["ms"][dom]
+                roofline["pipeline_event_bracket_ms"] = kernels["pipeline"]["event_bracket_ms"]
             if algo.precision != "fp32" and not args.no_kernel_timing:
                 roofline["calibration"] = mfma_calibration(torch, k["tflops"], 1 if algo.precision == "f16" else 3)
             pmc = pmc_traffic()
@@ -686,7 +698,10 @@ def main():
                 for n, v in kernels["pipeline"].items():
                     if not (isinstance(v, dict) and "tflops" in v):
                         continue
-                    e = {"avg_launch_ms": v["ms"], "achieved": v["tflops"], "frac": v["tflops"] / peak,
+                    iso = kernels.get(n, {})
+                    ms_k = iso.get("ms", v["ms"])
+                    tf_k = iso.get("tflops", v["tflops"])
+                    e = {"avg_launch_ms": ms_k, "avg_launch_ms_pipeline": v["ms"], "achieved": tf_k, "frac": tf_k / peak,
                          "algorithmic_bytes_per_launch": algo_bytes_per_launch(n, algo.mb, algo.D, algo.H, algo.A)}
                     if pmc and args.config in ("c2", "c4") and n in pmc:
                         e["traffic"] = pmc[n]["hbm_bytes_per_launch"]

@@ -280,9 +280,11 @@ int rlks_ppo_grad_phases(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeff
                          void* workspace_dev, int64_t workspace_bytes, int phases, void* stream);
 
 /* In-pipeline kernel timing of the split-fp16 gradient (bench.py roofline): `reps` full rlks_ppo_grad
- * passes with HIP events recorded between the launches on `stream` (after one untimed pass);
- * ms_out[5] = average ms of the weight split, F1a (k_sf_fwd; or the fused k_sf_f1 under
- * RLKS_F1_FUSED), F1b (k_sf_bwd; 0 when fused), F2 (k_sf_dw2) and the reduce. */
+ * passes on `stream` (after one untimed pass), each kernel launched with a start / stop event pair
+ * (hipExtLaunchKernelGGL: the kernel's own duration, as rocprofv3 measures it); ms_out[6] = average ms
+ * of the weight split (k_sf_split), F1a (k_sf_fwd; or the fused k_sf_f1 under RLKS_F1_FUSED), F1b
+ * (k_sf_bwd; 0 when fused), F2 (k_sf_dw2) and the reduce (k_reduce), each less the event bracket's own
+ * cost, which ms_out[5] reports (the same bracket around an empty kernel).  Synchronises the stream. */
 int rlks_ppo_grad_profile(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
                           const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
                           void* workspace_dev, int64_t workspace_bytes, int reps, double* ms_out, void* stream);

@@ -677,6 +677,8 @@ static int node_rollout(rlks_env* env, const rlks_mlp_desc* d, const float* para
   return forward(b->obs + (size_t)b->T * N * D, nullptr, b->values + (size_t)b->T * N);
 }
 
+__global__ void k_empty() {}  // (rlks_ppo_grad_profile: the event bracket's own time)
+
 }  // namespace rlks
 
 using namespace rlks;
@@ -871,13 +873,6 @@ struct FusedAdam {
                       // all-reduce follows; rlks_ppo_adam_apply then applies Adam)
 };
 
-// in-pipeline kernel timing (rlks_ppo_grad_profile): events recorded between sf_grad's launches while
-// a profile runs (null otherwise: one pointer test per mark)
-static hipEvent_t* g_prof_ev = nullptr;
-static void prof_mark(int i, hipStream_t s) {
-  if (g_prof_ev) (void)hipEventRecord(g_prof_ev[i], s);
-}
-
 // part: 0 = the whole gradient; 1 = the weight split, F1a, F2 and the reduce of W2 / b2 / W3 / b3 and
 // the stats; 2 = F1b and the reduce of W1 / b1 (rlks_ppo_grad_step_part: the caller all-reduces part
 // 1's buckets while part 2 runs)
@@ -891,13 +886,11 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
   const Layout L = make_layout(D, H, A);
   const bool f_pi = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_PI), f_vf = phases & (RLKS_PHASE_FWD | RLKS_PHASE_FWD_VF);
   if (part == 2) phases &= ~(RLKS_PHASE_PREP | RLKS_PHASE_DW2);
-  prof_mark(0, s);
   if ((phases & (RLKS_PHASE_FWD | RLKS_PHASE_PREP)) && part != 2) {
     const int parity = fa ? ((fa->step - 1) & 1) : 0;
     if (int rc = sf_prep(d, w, params, s, false, parity, fa && fa->prev_fused, fa ? (unsigned)fa->step : 0u))
       return rc;
   }
-  prof_mark(1, s);
   SfArgs a{};
   a.x = mb; a.x_stride = mb_stride(D, A); a.M = M; a.D = D; a.A_pi = A;
   a.tiles_per_split = w.tiles_per_split; a.co = *co; a.dyn = dyn;
@@ -916,21 +909,16 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     const int net0 = f_pi ? 0 : 1, nets = (f_pi && f_vf) ? 2 : 1;
     if (fused_f1 || part != 0) {
       if (int rc = launch_sf_f1(a, net0, nets, A, s, fused_f1 ? SF_F1_FUSED : part)) return rc;
-    } else {  // F1a, then F1b (a profiling mark between them)
-      if (int rc = launch_sf_f1(a, net0, nets, A, s, 1)) return rc;
-      prof_mark(2, s);
-      if (int rc = launch_sf_f1(a, net0, nets, A, s, 2)) return rc;
+    } else {
+      if (int rc = launch_sf_f1(a, net0, nets, A, s, 3)) return rc;
     }
   }
   // split F1 halves alone, both nets (profiling: each reads what a full F1 left in the workspace)
   if (!(f_pi || f_vf) && (phases & (RLKS_PHASE_F1A | RLKS_PHASE_F1B)))
     if (int rc = launch_sf_f1(a, 0, 2, A, s, (phases & RLKS_PHASE_F1A ? 1 : 0) | (phases & RLKS_PHASE_F1B ? 2 : 0)))
       return rc;
-  if (g_prof_ev && fused_f1) prof_mark(2, s);  // (no F1b launch: an empty interval)
-  prof_mark(3, s);
   if (phases & RLKS_PHASE_DW2)
     if (int rc = launch_sf_dw2(a, w.splits, s)) return rc;
-  prof_mark(4, s);
   if (!(phases & RLKS_PHASE_REDUCE)) return RLKS_OK;
   // F1's partial count: the fused kernel has half the split kernels' workgroups
   const int f1p = sf_f1_parts(M, fused_f1);
@@ -985,10 +973,9 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     else if (stride == 20) hipLaunchKernelGGL((k_reduce_gather<20, 32>), grid, dim3(256), 0, s, R.a, n);
     else hipLaunchKernelGGL((k_reduce_gather<36, 48>), grid, dim3(256), 0, s, R.a, n);
   } else {
-    hipLaunchKernelGGL(k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
+    launch_timed(KEV_REDUCE, k_reduce, dim3(R.blocks), dim3(256), 0, s, R.a);
   }
   RLKS_LAUNCHED();
-  prof_mark(5, s);
   return RLKS_OK;
 }
 
@@ -1084,30 +1071,39 @@ int rlks_ppo_grad_profile(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, con
   RLKS_REQUIRE(is_sf(d) && !is_wide(d) && reps > 0 && ms_out && co && params && dyn && mb && grad && workspace,
                RLKS_ERR_ARG, "rlks_ppo_grad_profile: split-fp16 descriptor, reps > 0");
   hipStream_t s = (hipStream_t)stream;
-  constexpr int NE = 6;
-  hipEvent_t ev[2][NE];
-  for (int b = 0; b < 2; ++b)
-    for (int i = 0; i < NE; ++i)
-      if (hipEventCreate(&ev[b][i]) != hipSuccess) return fail(RLKS_ERR_HIP, "rlks_ppo_grad_profile: event");
-  for (int k = 0; k < NE - 1; ++k) ms_out[k] = 0.0;
-  int rc = RLKS_OK;
-  // one untimed pass, then reps timed ones, each read back before its events are reused
-  rc = sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, s);
+  hipEvent_t ev[2 * KEV_N];
+  for (int i = 0; i < 2 * KEV_N; ++i)
+    if (hipEventCreate(&ev[i]) != hipSuccess) return fail(RLKS_ERR_HIP, "rlks_ppo_grad_profile: event");
+  for (int k = 0; k <= KEV_N; ++k) ms_out[k] = 0.0;
+  // one untimed pass, then reps timed ones, each read back before its events are reused; a kernel
+  // the pass does not launch (F1b under the fused F1) keeps its events unrecorded and reads 0
+  int rc = sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, s);
   for (int r = 0; r < reps && rc == RLKS_OK; ++r) {
-    g_prof_ev = ev[r & 1];
+    g_kernel_events = ev;
     rc = sf_grad(d, co, params, dyn, mb, M, grad, stats, workspace, ws_bytes, RLKS_PHASE_ALL, s);
-    g_prof_ev = nullptr;
+    g_kernel_events = nullptr;
     if (rc) break;
-    (void)hipEventSynchronize(ev[r & 1][NE - 1]);
-    for (int k = 0; k < NE - 1; ++k) {
+    if (hipStreamSynchronize(s) != hipSuccess) { rc = fail(RLKS_ERR_HIP, "rlks_ppo_grad_profile: sync"); break; }
+    for (int k = 0; k < KEV_N; ++k) {
       float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, ev[r & 1][k], ev[r & 1][k + 1]);
-      ms_out[k] += ms / reps;
+      if (hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]) == hipSuccess) ms_out[k] += ms / reps;
     }
   }
-  g_prof_ev = nullptr;
-  for (int b = 0; b < 2; ++b)
-    for (int i = 0; i < NE; ++i) (void)hipEventDestroy(ev[b][i]);
+  g_kernel_events = nullptr;
+  // the event bracket's own cost: the same start / stop pair around an empty kernel (one wave), read
+  // like the others and subtracted from each kernel's figure (ms_out[KEV_N] reports it)
+  double ovh = 0.0;
+  for (int r = 0; r < reps && rc == RLKS_OK; ++r) {
+    hipExtLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0u, s, ev[0], ev[1], 0u);
+    if (hipStreamSynchronize(s) != hipSuccess) { rc = fail(RLKS_ERR_HIP, "rlks_ppo_grad_profile: sync"); break; }
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) ovh += ms / reps;
+  }
+  for (int k = 0; k < KEV_N; ++k)
+    if (ms_out[k] > 0.0) ms_out[k] = ms_out[k] > ovh ? ms_out[k] - ovh : 0.0;
+  ms_out[KEV_N] = ovh;
+  (void)hipGetLastError();  // (an unrecorded event's elapsed-time query)
+  for (int i = 0; i < 2 * KEV_N; ++i) (void)hipEventDestroy(ev[i]);
   return rc;
 }
 

@@ -11,7 +11,23 @@ constexpr int SF_PMAX = 1024;       // weight-max entries per (parity, kind)
 constexpr int SF_W2_PSTRIDE = 256 * 256;  // floats between F2's dW2 partials (padding them apart: no gain)
 }  // namespace rlks
 
+#include <hip/hip_ext.h>
+
 namespace rlks {
+
+// In-pipeline kernel timing (rlks_ppo_grad_profile): while a profile runs, the SGD step's kernels are
+// launched through hipExtLaunchKernelGGL with a start / stop event pair each (the events bracket the
+// kernel itself, as rocprofv3's kernel trace does, not the launch gaps); null otherwise.
+enum { KEV_SPLIT, KEV_F1A, KEV_F1B, KEV_F2, KEV_REDUCE, KEV_N };
+extern hipEvent_t* g_kernel_events;  // [2 KEV_N]: start, stop per kernel
+template <typename K, typename... Args>
+inline void launch_timed(int idx, K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args) {
+  if (g_kernel_events)
+    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, g_kernel_events[2 * idx], g_kernel_events[2 * idx + 1], 0u,
+                          args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+}
 
 struct SfNetW {
   const float *w1, *b1, *w2;

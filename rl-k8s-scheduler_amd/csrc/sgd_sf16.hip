@@ -1646,12 +1646,15 @@ extern "C" int rlks_dbg_f2_stamps(unsigned long long* host) {
 }
 #endif
 
+hipEvent_t* g_kernel_events = nullptr;
+
 int launch_sf_prep(const SfPrepArgs& a, hipStream_t s) {
   if (!a.skip_wmax) {
     hipLaunchKernelGGL(k_sf_wmax, dim3(2, 32), dim3(256), 0, s, a);
     RLKS_LAUNCHED();
   }
-  hipLaunchKernelGGL(k_sf_split, dim3(2, 64), dim3(256), 0, s, a);
+  if (a.write_roll) hipLaunchKernelGGL(k_sf_split, dim3(2, 64), dim3(256), 0, s, a);
+  else launch_timed(KEV_SPLIT, k_sf_split, dim3(2, 64), dim3(256), 0, s, a);
   RLKS_LAUNCHED();
   return RLKS_OK;
 }
@@ -1663,17 +1666,17 @@ static int launch_f1_net_p(SfArgs a, int net0, int nets, hipStream_t s, int halv
   const dim3 grid(a.M / (16 * W) * nets);  // (f1_net_group)
   if (halves == SF_F1_FUSED) {  // one fused kernel
     constexpr int WF = SF_F1F_W;
-    hipLaunchKernelGGL((k_sf_f1<A_, KD, WF, P>), dim3(a.M / (16 * WF) * nets), dim3(64 * WF), (f1_lds_bytes<A_, KD, WF>()), s,
-                       a);
+    launch_timed(KEV_F1A, k_sf_f1<A_, KD, WF, P>, dim3(a.M / (16 * WF) * nets), dim3(64 * WF), f1_lds_bytes<A_, KD, WF>(),
+                 s, a);
     RLKS_LAUNCHED();
     return RLKS_OK;
   }
   if (halves & 1) {  // pi's LDS (A_ >= 1) covers the value net's
-    hipLaunchKernelGGL((k_sf_fwd<A_, KD, W, P>), grid, dim3(64 * W), (f1a_lds_bytes<A_, KD, W>()), s, a);
+    launch_timed(KEV_F1A, k_sf_fwd<A_, KD, W, P>, grid, dim3(64 * W), f1a_lds_bytes<A_, KD, W>(), s, a);
     RLKS_LAUNCHED();
   }
   if (halves & 2) {
-    hipLaunchKernelGGL((k_sf_bwd<KD, 3 * A_ + 1, W, P>), grid, dim3(64 * W), f1b_lds_bytes<KD>(), s, a);
+    launch_timed(KEV_F1B, k_sf_bwd<KD, 3 * A_ + 1, W, P>, grid, dim3(64 * W), f1b_lds_bytes<KD>(), s, a);
     RLKS_LAUNCHED();
   }
   return RLKS_OK;
@@ -1703,11 +1706,11 @@ int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {
   const size_t lds = (size_t)2 * F2_BUF * sizeof(_Float16) + 2 * F2_MAX_TILES * sizeof(int);  // 140 KB
   const bool p1 = a.products == 1;
   if (sf_kd(a.D) == 16) {
-    if (p1) hipLaunchKernelGGL((k_sf_dw2<16, 1>), dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
-    else hipLaunchKernelGGL((k_sf_dw2<16, 3>), dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+    if (p1) launch_timed(KEV_F2, k_sf_dw2<16, 1>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+    else launch_timed(KEV_F2, k_sf_dw2<16, 3>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
   } else {
-    if (p1) hipLaunchKernelGGL((k_sf_dw2<32, 1>), dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
-    else hipLaunchKernelGGL((k_sf_dw2<32, 3>), dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+    if (p1) launch_timed(KEV_F2, k_sf_dw2<32, 1>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+    else launch_timed(KEV_F2, k_sf_dw2<32, 3>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
   }
   RLKS_LAUNCHED();
   return RLKS_OK;

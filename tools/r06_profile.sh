@@ -18,4 +18,4 @@ rows = sorted(csv.DictReader(open(f)), key=lambda r: -float(r['TotalDurationNs']
 for r in rows:
     print(r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1e3, 1), 'us', r['Percentage'])
 PY
-bash tools/pmc_sgd.sh r06_pmc
+[ -n "$NO_PMC" ] || bash tools/pmc_sgd.sh r06_pmc
