@@ -586,7 +586,14 @@ def main():
     import torch
     import torch.distributed as dist
 
-    if world > 1:
+    # RLKS_DDP_FORCE=1 on one rank: a one-rank process group (RCCL) and the multi-rank SGD step with every
+    # collective issued (rlks.distributed.forced): RCCL's all-reduce on hardware with one GPU
+    forced = world == 1 and os.environ.get("RLKS_DDP_FORCE") == "1"
+    if forced:
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or forced:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # RCCL ("nccl") over xGMI, one GPU per rank.  RLKS_DIST_BACKEND=gloo is for rehearsing the
         # multi-rank path with several ranks on fewer GPUs (ranks share devices round-robin).
@@ -616,6 +623,8 @@ def main():
            .debugging(seed=42))
     cfg.num_envs = envs
     cfg.rollout_fragment_length = args.rollout
+    if os.environ.get("RLKS_OVERLAP_ALLREDUCE") is not None:  # multi-rank A/B: 0 = one bucket after the gradient
+        cfg.overlap_allreduce = os.environ["RLKS_OVERLAP_ALLREDUCE"] != "0"
     cfg.table, cfg.nodes = table, nodes
     algo = PPO(config=cfg, device=dev)
 
@@ -642,7 +651,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # multi-rank: one more (untimed) iteration with events around every gradient all-reduce
-    allreduce = algo.profile_allreduce() if world > 1 else None
+    allreduce = algo.profile_allreduce() if algo.multi else None
     kernels = None if args.no_kernel_timing else kernel_timing(algo, torch, args.config)
     # sanity: the policy is learning something finite
     st = algo.stats.cpu().numpy()
@@ -744,7 +753,7 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu, "allreduce": allreduce, "kernels": kernels, "finite": finite,
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if world > 1 or forced:
         dist.barrier()
         dist.destroy_process_group()
     return result

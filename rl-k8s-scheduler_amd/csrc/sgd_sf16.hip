@@ -480,18 +480,6 @@ __device__ __forceinline__ void hc_dma(const _Float16* hi, const _Float16* lo, i
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
   }
 }
-// the same copy as hc_dma through registers (global load -> ds_write): diagnostic builds only
-template <int W>
-__device__ __forceinline__ void hc_stage(const _Float16* hi, const _Float16* lo, int r0, int col, _Float16* buf, int w,
-                                         int l) {
-#pragma unroll
-  for (int i = 0; i < 16 / W; ++i) {
-    const int blk = (16 / W) * w + i, arr = blk >> 3, sig = (blk & 7) * 64 + l;
-    const int r = sig >> 2, q = (sig & 3) ^ sw16(r);
-    const _Float16* src = (arr ? lo : hi) + (r0 + r) * HID + col + 8 * q;
-    *reinterpret_cast<v4u*>(buf + arr * H16 + (blk & 7) * 512 + l * 8) = *reinterpret_cast<const v4u*>(src);
-  }
-}
 // (hi, lo) fragment of image row 16 j + c, piece g
 __device__ __forceinline__ void hc_frag(const _Float16* buf, int j, int c, int g, h8& fh, h8& fl) {
   const int off = (16 * j + c) * 32 + 8 * (g ^ sw16(c));
@@ -541,22 +529,10 @@ __device__ __forceinline__ void w1_frag(const _Float16* sW1, int kt, int c, int 
 // sum over the four 16-lane rows of a wave (lanes c, c + 16, c + 32, c + 48): every lane gets the
 // same bits
 __device__ __forceinline__ float sum_rows4(float v) {
-#if defined(RLKS_SUMROWS_SHFL)
-  v += __shfl_xor(v, 16);
-  return v + __shfl_xor(v, 32);
-#elif defined(RLKS_SUMROWS_NOP)
-  float a = v, b = v;
-  asm volatile("s_nop 4\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 4" : "+v"(a), "+v"(b));
-  v = a + b;
-  a = v; b = v;
-  asm volatile("s_nop 4\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 4" : "+v"(a), "+v"(b));
-  return a + b;
-#else
   auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
   p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(p[0]) + __uint_as_float(p[1]);
-#endif
 }
 // reduce-scatter of 16 per-lane values over the 16 lanes of a row: lane c of the row ends with the
 // row total of v[c] (DPP row_ror:8, row_half_mirror, quad_perm xor 2, xor 1; 43 VALU)
@@ -639,7 +615,7 @@ constexpr int f1b_lds_bytes() {
 //   dW3[A-1] = -sum_{a < A-1} dW3[a]
 // which is the same loss and gradient with A - 1 head rows instead of A (at 2 actions: half of the
 // head, of dZ2's products and of the dW3 reduce-scatter, the epilogue's largest part).  AH: head rows.
-template <int A_, int NET, int KD, int W, int P, bool OPQ = false>
+template <int A_, int NET, int KD, int W, int P>
 __device__ __forceinline__ int f1a_body(const SfArgs& g, int grp) {
   constexpr int NTHR = 64 * W;
   constexpr int AH = NET == 0 ? A_ - 1 : 1;
@@ -652,9 +628,7 @@ __device__ __forceinline__ int f1a_body(const SfArgs& g, int grp) {
   float* sW3 = sB2 + HID;
 
   // w wave-uniform (readfirstlane): tile bases stay in SGPRs, stores use a 32-bit lane offset
-  int tid = threadIdx.x;
-  if constexpr (OPQ) asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(tid));
-  const int l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
+  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), c = l & 15, gq = l >> 4;
   // Prologue: every global load of the first group goes out before any result is used (the W2
   // half-chunk and W1a planes by LDS DMA, the tile's X rows, b2 and W3 into registers), so the
   // workgroup waits for one memory round trip instead of four in a row
@@ -961,10 +935,6 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g, int grp, int edz_in = 
   const int row0 = tile * 16, blk = grp;
   const int D = g.D, stride = g.x_stride;
 
-#ifdef RLKS_F1_NODMA
-  if constexpr (FUSED) hc_stage<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
-  else
-#endif
   hc_dma<W>(N.w2th, N.w2tl, 0, 0, sCh, w, l);
   if constexpr (!W1_KEPT) w1_stage<KD, NTHR>(N, sW1, tid);
   const int edz = FUSED ? edz_in : N.tile_edz[tile];
@@ -983,10 +953,6 @@ __device__ __forceinline__ void f1b_body(const SfArgs& g, int grp, int edz_in = 
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
       const int st = 2 * s + ph;
-#ifdef RLKS_F1_NODMA
-      if (FUSED && st < 15) hc_stage<W>(N.w2th, N.w2tl, 128 * (ph ^ 1), 32 * (s + ph), sCh + (ph ^ 1) * 2 * H16, w, l);
-      else
-#endif
       if (st < 15) hc_dma<W>(N.w2th, N.w2tl, 128 * (ph ^ 1), 32 * (s + ph), sCh + (ph ^ 1) * 2 * H16, w, l);
       if (ph == 0) {
         ah = dh;
@@ -1108,23 +1074,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 // Measured no faster than the two kernels (126-128 µs against 126 µs for the pair at c4).
 template <int A_, int KD, int W>
 constexpr bool f1_w1_kept() {  // F1a's epilogue slots end before the W1a planes (sW1 = 4 H16 halves in)
-#ifdef RLKS_F1_RESTAGE
-  return false;
-#endif
   return W * (A_ - 1 > 1 ? A_ - 1 : 1) * HID * 4 + W * (A_ + 4) * 4 <= 4 * H16 * 2;
 }
 template <int A_, int KD, int W>
 constexpr int f1_lds_bytes() {
-#ifdef RLKS_F1_ONEWG
-  return 96 * 1024;
-#endif
   return f1a_lds_bytes<A_, KD, W>() > f1b_lds_bytes<KD>() ? f1a_lds_bytes<A_, KD, W>() : f1b_lds_bytes<KD>();
 }
-#ifdef RLKS_F1_OPQ
-constexpr bool F1_OPQ = true;
-#else
-constexpr bool F1_OPQ = false;
-#endif
 template <int A_, int KD, int W, int P>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sf_f1(SfArgs g) {
   const int2 ng = f1_net_group<W, (A_ <= 4)>(g);
@@ -1132,19 +1087,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   // compiler from carrying F1a's values across the epilogue in registers (which spilled)
   SfArgs g2 = g;
   if (ng.x + g.net0 == 0) {
-    const int edz = f1a_body<A_, 0, KD, W, P, F1_OPQ>(g, ng.y);
+    const int edz = f1a_body<A_, 0, KD, W, P>(g, ng.y);
     __syncthreads();  // epilogue slots read; the dZ2 stores complete (the fence waits for them)
-#ifdef RLKS_F1_FENCE
-    __threadfence();
-#endif
     asm volatile("" : "+s"(g2.x));
     f1b_body<0, KD, 3 * A_ + 1, W, P, true, f1_w1_kept<A_, KD, W>()>(g2, ng.y, edz);
   } else {
-    const int edz = f1a_body<1, 1, KD, W, P, F1_OPQ>(g, ng.y);
+    const int edz = f1a_body<1, 1, KD, W, P>(g, ng.y);
     __syncthreads();
-#ifdef RLKS_F1_FENCE
-    __threadfence();
-#endif
     asm volatile("" : "+s"(g2.x));
     f1b_body<1, KD, 3 * A_ + 1, W, P, true, f1_w1_kept<1, KD, W>()>(g2, ng.y, edz);
   }

@@ -13,6 +13,8 @@ not depend on the world size.  The only exchanges are
 """
 from __future__ import annotations
 
+import os
+
 
 def group():
     """the initialised default process group's torch.distributed module, or None"""
@@ -21,6 +23,15 @@ def group():
     except Exception:  # pragma: no cover
         return None
     return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def forced():
+    """RLKS_DDP_FORCE=1 with an initialised process group: a single rank still takes the multi-rank
+    path (gradient -> all-reduce -> Adam, the overlapped two-bucket all-reduce, the per-iteration
+    sums), with every collective really issued.  On one GPU this runs RCCL's all-reduce on hardware
+    (a one-rank communicator) through the exact calls the 8-GPU run makes; the result equals the
+    ordinary one-rank path bit for bit (tests/test_gpu_multirank.py)."""
+    return os.environ.get("RLKS_DDP_FORCE") == "1" and group() is not None
 
 
 def rank_world():
@@ -41,7 +52,7 @@ def loss_scale(rows_per_rank: int, world: int) -> float:
 def allreduce_sum_(t):
     """in-place sum over ranks (no-op for a single process)"""
     d = group()
-    if d is not None and d.get_world_size() > 1:
+    if d is not None and (d.get_world_size() > 1 or forced()):
         d.all_reduce(t)
     return t
 
@@ -52,6 +63,6 @@ def allreduce_sum_async(tensors):
     (RCCL: the collective runs on its own stream, so it overlaps whatever the caller's stream does
     until then).  Single process: no-op, []."""
     d = group()
-    if d is None or d.get_world_size() == 1:
+    if d is None or (d.get_world_size() == 1 and not forced()):
         return []
     return [d.all_reduce(t, async_op=True) for t in tensors]

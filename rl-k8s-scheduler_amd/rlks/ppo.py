@@ -235,6 +235,7 @@ class PPO:
             cfg.env = env
         self.torch = torch
         self.rank, self.world = ddp.rank_world()
+        self.multi = self.world > 1 or ddp.forced()  # the multi-rank SGD step (ddp.forced: one rank, RCCL)
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -345,7 +346,7 @@ class PPO:
         off = self.params.offsets
         g = self.grad
         self._buckets = ([g[off[2]:self.params.padded]], [g[off[0]:off[2]]])
-        self._overlap = bool(cfg.overlap_allreduce) and self.world > 1 and self.precision in ("sf16", "f16")
+        self._overlap = bool(cfg.overlap_allreduce) and self.multi and self.precision in ("sf16", "f16")
         self.sample_calls = 0   # compute_actions / compute_single_action draws so far (Philox counter)
         self.iteration = 0
         self.timesteps_total = 0
@@ -411,7 +412,7 @@ class PPO:
             ne, nb = next_mb
             nxt = C.byref(_lib.GatherNext(_lib.ptr(self.packed), _lib.ptr(self.mbuf), self.perm_seed(), nb * self.mb,
                                           self.T, self.N, ne, self.groups, self.group0, self.mb))
-        if self.world == 1:  # no all-reduce between gradient and Adam: one fused launch sequence
+        if not self.multi:  # no all-reduce between gradient and Adam: one fused launch sequence
             _lib.call("rlks_ppo_sgd_step_next", desc, C.byref(self.coeffs), _lib.ptr(self.params.flat),
                       _lib.ptr(self.dyn), _lib.ptr(self.mbuf), self.mb, _lib.ptr(self.grad), _lib.ptr(stat_row),
                       _lib.ptr(self.adam_m), _lib.ptr(self.adam_v), self.params.padded, float(self.config.lr),
@@ -489,7 +490,7 @@ class PPO:
         buckets reduced, what the step's Adam waits for; with overlap_allreduce the first bucket has
         run under the dW1 kernel), its mean / max, total and share of the iteration, and the span
         from the first bucket's start; the maximum over ranks of each."""
-        if self.world == 1:
+        if not self.multi:
             return None
         torch = self.torch
         st = torch.cuda.current_stream(self.device)

@@ -20,7 +20,11 @@ def main():
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    backend = os.environ.get("RLKS_DIST_BACKEND", "gloo")  # nccl: the one-rank RCCL test (RLKS_DDP_FORCE=1)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         from rlks.ppo import PPO, PPOConfig
 
@@ -33,6 +37,7 @@ def main():
         cfg.overlap_allreduce = bool(overlap)
         algo = PPO(config=cfg, device=torch.device("cuda", 0))
         assert (algo.rank, algo.world, algo.groups, algo.group0) == (rank, world, 1, rank)
+        assert algo.multi
         results = [algo.train() for _ in range(iters)]
         assert algo._overlap == bool(overlap)
         keep = ("episode_reward_mean", "episodes_this_iter", "timesteps_total")

@@ -30,13 +30,13 @@ def _free_port():
     return p
 
 
-def _run_ranks(out, N, T, mb, epochs, iters, world, overlap=1):
+def _run_ranks(out, N, T, mb, epochs, iters, world, overlap=1, extra_env=None):
     out.mkdir(parents=True, exist_ok=True)
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0", **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, str(HERE / "multirank_worker.py"), str(out), str(N),
                                        str(T), str(mb), str(epochs), str(iters), str(overlap)], env=env))
     try:
@@ -124,3 +124,33 @@ def test_bench_launches_two_ranks(tmp_path):
     assert j["config"]["global_batch"] == 2 * 512 * 16
     assert j["value"] == pytest.approx(2 * 512 * 16 * 2 / (j["ms_per_step"] * 2e-3), rel=1e-6)
     assert j["allreduce"] is not None
+
+
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_one_rank_rccl_multirank_path_equals_one_rank(tmp_path, overlap):
+    """RCCL on hardware with one GPU: a one-rank RCCL process group with RLKS_DDP_FORCE=1 takes the
+    multi-rank SGD step (gradient -> RCCL all-reduce -> Adam; overlap=1: the two-bucket all-reduce on
+    RCCL's stream under F1b) with every collective issued, exactly the calls of the 8-GPU run.  A
+    one-rank all-reduce is the identity, so the parameters equal the ordinary one-rank run's bit for bit;
+    the worker's profile_allreduce reports RCCL's per-step time on this box."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from rlks.ppo import PPO, PPOConfig
+
+    N, T, mb, epochs, iters = 1024, 64, 8192, 2, 2
+    (z,) = _run_ranks(tmp_path, N, T, mb, epochs, iters, 1, overlap=overlap,
+                      extra_env={"RLKS_DIST_BACKEND": "nccl", "RLKS_DDP_FORCE": "1"})
+    prof = json.loads(str(z["allreduce"]))
+    assert prof is not None and prof["backend"] == "nccl" and prof["overlapped"] == bool(overlap), prof
+    print("one-rank RCCL all-reduce:", json.dumps(prof))
+    cfg = (PPOConfig().environment("K8sMultiCloudEnv").framework("torch")
+           .training(train_batch_size=N * T, sgd_minibatch_size=mb, num_sgd_iter=epochs, lr=3e-4, gamma=0.99)
+           .debugging(seed=13))
+    cfg.num_envs = N
+    cfg.rollout_fragment_length = T
+    algo = PPO(config=cfg, device=torch.device("cuda", 0))
+    assert not algo.multi
+    single = [algo.train() for _ in range(iters)]
+    assert np.array_equal(z["params"].view(np.uint32), algo.params.flat.cpu().numpy().view(np.uint32))
+    res = json.loads(str(z["results"]))
+    np.testing.assert_equal([r["episode_reward_mean"] for r in res], [r["episode_reward_mean"] for r in single])
