@@ -85,9 +85,13 @@ class PPOConfig:
         # rank.  A single-rank run with num_lane_groups = W trains exactly like W ranks (the rollout
         # picks its forward kernel from the job's lane count, rlks_rollout_bufs.global_lanes).
         self.num_lane_groups = None
-        # more than one rank, split-fp16 step: all-reduce the W2 / W3 gradient bucket while the dW1
-        # kernel runs (rlks_ppo_grad_step_part), instead of the whole gradient after it
-        self.overlap_allreduce = True
+        # more than one rank, split-fp16 step: True = all-reduce the W2 / W3 gradient bucket while the
+        # dW1 kernel runs (rlks_ppo_grad_step_part), False = the whole gradient after it in one bucket.
+        # Measured with a one-rank RCCL group at c4 (profiles/r06_rccl): one bucket costs 14 µs a step
+        # over the one-rank step, two buckets 57 µs (a second all-reduce, a second reduce launch, and
+        # RCCL's kernel on the CUs beside F1b) -- more than an 8-GPU all-reduce of 544 KB is expected
+        # to expose, so one bucket is the default
+        self.overlap_allreduce = False
         # rlks-specific knobs
         self.num_envs = None          # lanes per GPU (default: workers x envs per worker)
         self.noise = "philox"         # env utilisation noise: "philox" or "mt19937"
