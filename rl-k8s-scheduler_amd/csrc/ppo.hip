@@ -27,6 +27,8 @@ struct RedTask {
   int blk0;
   int mslot;         // fused Adam: -1, or the max |w| slot (net * 2 + 0: W2, + 1: W1a) of the output
   int mbase;         // first entry of this task's blocks in the slot
+  int kq;            // 0: output vector iv at element 4 iv; 1 (k_sf_dw2r's [k / 4][n][4] partials of a
+                     // [256][256] weight): at n * 256 + 4 (iv >> 8), n = iv & 255
 };
 constexpr int MAX_TASKS = 20;
 // torch.optim.Adam (single-tensor path) on element i: exp_avg.lerp_(g, 1-b1); exp_avg_sq =
@@ -120,7 +122,7 @@ __device__ __forceinline__ void reduce_block(const RedArgs& g, const int bx) {
   if (grp == 0) {
     double t[4] = {0.0, 0.0, 0.0, 0.0};
     for (int j = 0; j < T.V; ++j) t[j] = sh[j][o];
-    const int i0 = T.V * iv;
+    const int i0 = T.kq ? (iv & 255) * 256 + 4 * (iv >> 8) : T.V * iv;
     if (T.out64) {
       for (int j = 0; j < T.V && i0 + j < T.len; ++j) T.out64[i0 + j] = t[j];
     } else if (T.V == 4 && i0 + 3 < T.len) {
@@ -176,6 +178,7 @@ struct Reducer {
     RedTask& t = a.t[a.ntasks++];
     t.mslot = mslot;
     t.mbase = 0;
+    t.kq = 0;
     int G = 1;
     constexpr int PPT = 32;  // partials per thread (c4 reduce: 16 -> 19.0 us, 32 -> 19.0 us, 8 -> 23.9 us)
     while (G < 256 && G * PPT < P) G *= 2;
@@ -933,6 +936,7 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     }
     if (part != 2) {
       R.add(n.part_w2, grad + o[2], nullptr, SF_W2_PSTRIDE, w.splits, H * H, 2 * net);
+      R.a.t[R.a.ntasks - 1].kq = sf_f2_regs() ? 1 : 0;
       R.add(n.part_b2, grad + o[3], nullptr, H, w.splits, H);
       R.add(n.part_w3, grad + o[4], nullptr, (int64_t)An * H, f1p, An * H);
       if (net == 0) R.add(n.part_b3, grad + o[5], nullptr, An, f1p, An);

@@ -113,6 +113,9 @@ int launch_sf_prep(const SfPrepArgs& a, hipStream_t s);
 constexpr int SF_F1_FUSED = 7;
 int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int halves = 3);  // needs M % 256 == 0
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s);
+// whether F2 is k_sf_dw2r (H1 in registers; its dW2 partials in [k / 4][n][4] order, the default)
+// rather than round 3-5's k_sf_dw2 ([n][k] partials; RLKS_F2_IMAGE=1, kept for same-box A/B runs)
+bool sf_f2_regs();
 // F1's partials per net (one per F1 workgroup): dW1 / db1, and dW3 / db3 / stats; the workspace holds
 // the split kernels' count (the larger), the fused kernel writes half as many
 int sf_f1_parts(int M, bool fused);

@@ -1459,6 +1459,248 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
 #endif
 }
 
+// F2 with H1 in registers (round 6): dW2^T = H1^T dZ2 over the workgroup's rows, eight waves of 32
+// hidden units k x 256 outputs n (8 v_mfma_f32_32x32x16_f16 tiles, 128 accumulator registers, two
+// waves per SIMD).  Wave w's A operand is H1 of its own hidden units k = 32 w + (l & 31), taken from
+// its Z1 = Xa W1a^T accumulator as it stands: the accumulator's rows acc_row(8 s + j) are the K order
+// perm(s, h, j) in which k_sf_dw2's transposed reads deliver the dZ2 chunk, so that image is this
+// kernel's B operand unchanged.  No H1 image and no ping-pong between wave halves (k_sf_dw2's phases,
+// bound by their pairing): every wave issues its MFMAs of chunk c beside its own
+// production of chunk c + 1 (its share of the dZ2 image, its H1), one barrier per chunk.  Each wave
+// holds 4 consecutive k of one n per accumulator quad, so the partials are written in [k / 4][n][4]
+// order (16-byte stores, 512 contiguous bytes per half-wave); the reduce maps them back
+// (RedTask::kq).
+constexpr int F2R_ABUF = 2 * F2_APLANE;
+#ifndef F2R_SCHED
+#define F2R_SCHED 0  // (A/B builds: the loop's MFMA / VALU / LDS-read interleave pattern)
+#endif
+#ifndef F2R_DIAG
+#define F2R_DIAG 0  // (timing-only diagnostic builds, wrong gradients: 1 no partial stores, 2 no MFMAs, 3 no production)
+#endif  // halves per buffer: the dZ2 image's hi and lo planes
+template <int KD, int P>
+__global__ __launch_bounds__(F2_THREADS) void k_sf_dw2r(SfArgs g) {
+  const SfNet& N = g.n[blockIdx.y];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  _Float16* sm = reinterpret_cast<_Float16*>(lds);  // [2 buf][F2R_ABUF]
+  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = l & 15, gq = l >> 4, r = l & 31, h = l >> 5;
+  const int D = g.D, stride = g.x_stride;
+  int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
+  if (!dcheck(t1 <= g.M / 32, DC_SGD_TILE, t1)) t0 = t1 = 0;
+  const int nk = t1 - t0;
+
+  // F1a's X and dZ2 exponents of the workgroup's 16-row tiles -> LDS; E = min e_T (as k_sf_dw2)
+  int* sEx = reinterpret_cast<int*>(sm + 2 * F2R_ABUF);
+  int* sEd = sEx + F2_MAX_TILES;
+  int emin = 120;
+  for (int i = tid; i < 2 * nk; i += F2_THREADS) {
+    sEx[i] = N.tile_ex[2 * t0 + i];
+    const int e = N.tile_edz[2 * t0 + i];
+    sEd[i] = e;
+    emin = min(emin, e);
+  }
+  __shared__ float s_emin[F2_THREADS / 64];
+  emin = (int)-wave_max((float)-emin);
+  if (l == 0) s_emin[w] = (float)emin;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < F2_THREADS / 64; ++i) emin = min(emin, (int)s_emin[i]);
+  const int E = __builtin_amdgcn_readfirstlane(emin);
+  const float ssgn = tile_sign(blockIdx.x);  // odd splits: products on -H1, partial negated back
+  const float unscale = ssgn * pow2(-14 - E);
+
+  // B fragments (k_sf_dw2's A reads): output block n = 32 ob + r, K order of k-step s as above
+  const int aq = (4 * ((l >> 4) & 1) + (l & 3)) ^ (2 * h);
+  const int bbase = (4 * h + ((l & 15) >> 2)) * F2_AROW + 4 * aq;
+  const int bbase8 = (4 * h + ((l & 15) >> 2) + 8) * F2_AROW + 4 * (aq ^ 4);
+  f32x16 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+  auto mfma_chunk = [&](const _Float16* b, const h8 (&hh)[2], const h8 (&hl)[2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob) {
+        const _Float16* pb = b + bbase + s * 16 * F2_AROW + 32 * ob;
+        const _Float16* pb8 = b + bbase8 + s * 16 * F2_AROW + 32 * ob;
+        const h4 a0 = tr_read(pb), a1 = tr_read(pb8);
+        const h4 c0 = tr_read(pb + F2_APLANE), c1 = tr_read(pb8 + F2_APLANE);
+        const h8 bh = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+        const h8 bl = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
+        acc[ob] = mmaP<P>(hh[s], hl[s], bh, bl, acc[ob]);
+      }
+  };
+
+  // dZ2 pieces (k_sf_dw2's load_dz / store_dz: wave w moves n-step w of the chunk's two tiles)
+  const __amdgpu_buffer_rsrc_t dz_rsrc = __builtin_amdgcn_make_buffer_rsrc(N.dz2s, (short)0, 0x7fffffff, 0x00020000);
+  const int dz_lane = 2 * (w * 1024 + l * 8);
+  h8 dp[4];
+  auto load_dz = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dp[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(
+                                         dz_rsrc, dz_lane, t * (32 * HID * 4) + (i >> 1) * (16 * HID * 4) + (i & 1) * 1024, 0));
+  };
+  float db2[8] = {};
+  auto store_dz = [&](_Float16* img, float s0, float s1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float sc = (i >> 1) ? s1 : s0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) db2[j] = fmaf((float)dp[i][j], sc, db2[j]);
+      const int off = (i & 1) * F2_APLANE + (16 * (i >> 1) + c) * F2_AROW + 32 * w;
+      const int sw = 2 * ((c >> 2) & 3);
+      *reinterpret_cast<h4*>(img + off + 4 * (gq ^ sw)) = __builtin_shufflevector(dp[i], dp[i], 0, 1, 2, 3);
+      *reinterpret_cast<h4*>(img + off + 4 * ((gq + 4) ^ sw)) = __builtin_shufflevector(dp[i], dp[i], 4, 5, 6, 7);
+    }
+  };
+
+  // H1 of the chunk for this wave's hidden units kh = 32 w + r: Z1 = Xa W1a^T on
+  // v_mfma_f32_32x32x8_f16 (as k_sf_dw2), tanh, split into the two k-steps' A fragments
+  constexpr int KB = KD / 8;
+  const int kh = 32 * w + r;
+  h4 wh[KB], wl[KB];
+  auto load_w1 = [&]() {
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      wh[kb] = *reinterpret_cast<const h4*>(N.w1h + kh * KD + 8 * kb + 4 * h);
+      wl[kb] = *reinterpret_cast<const h4*>(N.w1l + kh * KD + 8 * kb + 4 * h);
+    }
+  };
+  if constexpr (KB <= 2) load_w1();
+  const float inv_w1 = N.sc[1];
+  v4f xr[KB];
+  int2 xe, de;
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.x), (short)0, 0x7fffffff, 0x00020000);
+  auto load_x = [&](int t) {
+    xe = *reinterpret_cast<const int2*>(sEx + 2 * (t - t0));
+    de = *reinterpret_cast<const int2*>(sEd + 2 * (t - t0));
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const int base = 8 * kb + 4 * h, pb = base < stride - 4 ? base : stride - 4;
+      xr[kb] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(x_rsrc, 4 * (r * stride + pb), 4 * t * 32 * stride, 0));
+    }
+  };
+  auto make_h1 = [&](h8 (&hh)[2], h8 (&hl)[2]) {
+    if constexpr (KB > 2) load_w1();
+    const int ex = min(xe.x, xe.y);
+    const float sx = ssgn * pow2(ex), k_z1 = ssgn * inv_w1 * pow2(-ex) * SF_2LOG2E;
+    f32x16 z;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const int base = 8 * kb + 4 * h;
+      const bool inrow = base < stride - 4;
+      h4 xh, xl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = base + j;
+        _Float16 a, b;
+        split1(fmaf(xr[kb][j], (d < D && inrow) ? sx : 0.f, d == D ? sx : 0.f), a, b);
+        xh[j] = a;
+        xl[j] = b;
+      }
+      if constexpr (P != 1) {
+        z = __builtin_amdgcn_mfma_f32_32x32x8f16(xl, wh[kb], z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wl[kb], z, 0, 0, 0);
+      }
+      z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wh[kb], z, 0, 0, 0);
+    }
+    // k-step s = rows of tile 2t + s: H1 at 2^(14 + E - e_T) (the odd tile arrives negated: -hs1)
+    const float hs0 = ssgn * pow2(14 + E - de.x), hs1 = -ssgn * pow2(14 + E - de.y);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const float hs = s ? hs1 : hs0;
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = fmaf(-2.f * hs, tanh_r(z[8 * s + j] * k_z1), hs);
+      split8v(x, hh[s], hl[s]);
+    }
+  };
+  auto barrier = [&]() {  // (k_sf_dw2's phase barrier: LDS stores drained, prefetches left in flight)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  h8 hh[2], hl[2];
+  if (nk > 0) {
+    load_dz(t0);
+    load_x(t0);
+    store_dz(sm, pow2(-de.x), -pow2(-de.y));
+    make_h1(hh, hl);
+    load_x(min(t0 + 1, t1 - 1));
+    load_dz(min(t0 + 1, t1 - 1));
+  }
+  __syncthreads();
+  for (int ci = 0; ci < nk; ++ci) {
+#if F2R_DIAG != 2
+    mfma_chunk(sm + (ci & 1) * F2R_ABUF, hh, hl);
+#endif
+    // chunk ci + 1 (past the end: the last chunk again, into the idle buffer, uncounted -- unconditional,
+    // so that this production shares the MFMAs' basic block)
+    const bool counted = ci + 1 < nk;
+    const float s0 = counted ? pow2(-de.x) : 0.f, s1 = counted ? -pow2(-de.y) : 0.f;
+    h8 nh[2], nl[2];
+#if F2R_DIAG != 3
+    store_dz(sm + ((ci + 1) & 1) * F2R_ABUF, s0, s1);
+    make_h1(nh, nl);
+#else
+    nh[0] = hh[1]; nh[1] = hh[0]; nl[0] = hl[1]; nl[1] = hl[0];
+#endif
+    load_x(min(t0 + ci + 2, t1 - 1));
+#if F2R_SCHED == 1
+    sched_interleave<6 * KB / 2 + 48, 4>();
+#elif F2R_SCHED == 2
+#pragma unroll
+    for (int i = 0; i < 6 * KB / 2 + 48; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+#elif F2R_SCHED == 3
+#pragma unroll
+    for (int i = 0; i < 6 * KB / 2 + 48; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+    }
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+    load_dz(min(t0 + ci + 2, t1 - 1));
+    barrier();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      hh[s] = nh[s];
+      hl[s] = nl[s];
+    }
+  }
+
+  // partials [k / 4][n][4]: accumulator quad t of tile ob = k 32 w + 8 t + 4 h + 0..3, n = 32 ob + r
+  float* out = N.part_w2 + (size_t)blockIdx.x * SF_W2_PSTRIDE;
+#pragma unroll
+  for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const v4f v = {acc[ob][4 * t] * unscale, acc[ob][4 * t + 1] * unscale, acc[ob][4 * t + 2] * unscale,
+                     acc[ob][4 * t + 3] * unscale};
+#if F2R_DIAG != 1
+      *reinterpret_cast<v4f*>(out + ((size_t)(8 * w + 2 * t + h) * HID + 32 * ob + r) * 4) = v;
+#else
+      if (v[0] == 1.2345f) out[0] = v[1];  // (keeps the accumulators live)
+#endif
+    }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) db2[j] = row_sum16(db2[j]);
+  if (c == 0)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) N.part_b2[(size_t)blockIdx.x * HID + 32 * w + 16 * (j >> 2) + 4 * gq + (j & 3)] = db2[j];
+}
+
 
 // ----------------------------------------------------------------------------- forward only
 // Rollout forward of both nets on 16-row tiles (the F1a schedule above without the loss and the
@@ -1650,8 +1892,29 @@ int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int 
   }
 }
 
+bool sf_f2_regs() {
+  static const bool on = [] {
+    const char* e = getenv("RLKS_F2_IMAGE");
+    return !(e && e[0] == '1');
+  }();
+  return on;
+}
+
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {
   RLKS_REQUIRE(a.tiles_per_split <= F2_MAX_TILES / 2, RLKS_ERR_ARG, "split-fp16 F2: too many row chunks per split");
+  if (sf_f2_regs()) {
+    const size_t lds = (size_t)2 * F2R_ABUF * sizeof(_Float16) + 2 * F2_MAX_TILES * sizeof(int);  // 76 KB
+    const bool p1 = a.products == 1;
+    if (sf_kd(a.D) == 16) {
+      if (p1) launch_timed(KEV_F2, k_sf_dw2r<16, 1>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+      else launch_timed(KEV_F2, k_sf_dw2r<16, 3>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+    } else {
+      if (p1) launch_timed(KEV_F2, k_sf_dw2r<32, 1>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+      else launch_timed(KEV_F2, k_sf_dw2r<32, 3>, dim3(splits, 2), dim3(F2_THREADS), lds, s, a);
+    }
+    RLKS_LAUNCHED();
+    return RLKS_OK;
+  }
   const size_t lds = (size_t)2 * F2_BUF * sizeof(_Float16) + 2 * F2_MAX_TILES * sizeof(int);  // 140 KB
   const bool p1 = a.products == 1;
   if (sf_kd(a.D) == 16) {
