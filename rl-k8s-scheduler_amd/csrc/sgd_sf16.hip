@@ -1471,9 +1471,6 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2(SfArgs g) {
 // order (16-byte stores, 512 contiguous bytes per half-wave); the reduce maps them back
 // (RedTask::kq).
 constexpr int F2R_ABUF = 2 * F2_APLANE;
-#ifndef F2R_SCHED
-#define F2R_SCHED 0  // (A/B builds: the loop's MFMA / VALU / LDS-read interleave pattern)
-#endif
 #ifndef F2R_DIAG
 #define F2R_DIAG 0  // (timing-only diagnostic builds, wrong gradients: 1 no partial stores, 2 no MFMAs, 3 no production)
 #endif  // halves per buffer: the dZ2 image's hi and lo planes
@@ -1638,6 +1635,10 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2r(SfArgs g) {
     load_dz(min(t0 + 1, t1 - 1));
   }
   __syncthreads();
+  // (An interleave of 1 MFMA with 4-6 VALU and LDS reads by sched_group_barrier: 50 -> 51 us at c4;
+  // waves 0-3 MFMAs then production and 4-7 production then MFMAs, so that a SIMD's two waves overlap
+  // one's VALU with the other's MFMAs: 50 -> 60 us, 13 registers spilled from the second order's
+  // longer-lived operands; profiles/r06_f2regs/sched, order.)
   for (int ci = 0; ci < nk; ++ci) {
 #if F2R_DIAG != 2
     mfma_chunk(sm + (ci & 1) * F2R_ABUF, hh, hl);
@@ -1654,22 +1655,6 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2r(SfArgs g) {
     nh[0] = hh[1]; nh[1] = hh[0]; nl[0] = hl[1]; nl[1] = hl[0];
 #endif
     load_x(min(t0 + ci + 2, t1 - 1));
-#if F2R_SCHED == 1
-    sched_interleave<6 * KB / 2 + 48, 4>();
-#elif F2R_SCHED == 2
-#pragma unroll
-    for (int i = 0; i < 6 * KB / 2 + 48; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-#elif F2R_SCHED == 3
-#pragma unroll
-    for (int i = 0; i < 6 * KB / 2 + 48; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-    }
-#endif
     __builtin_amdgcn_sched_barrier(0);
     load_dz(min(t0 + ci + 2, t1 - 1));
     barrier();
