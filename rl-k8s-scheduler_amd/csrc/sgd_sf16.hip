@@ -1638,7 +1638,9 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2r(SfArgs g) {
   // (An interleave of 1 MFMA with 4-6 VALU and LDS reads by sched_group_barrier: 50 -> 51 us at c4;
   // waves 0-3 MFMAs then production and 4-7 production then MFMAs, so that a SIMD's two waves overlap
   // one's VALU with the other's MFMAs: 50 -> 60 us, 13 registers spilled from the second order's
-  // longer-lived operands; profiles/r06_f2regs/sched, order.)
+  // longer-lived operands; the next chunk's Z1 MFMAs issued ahead of the chunk's 48 (and interleaved
+  // 1 : 5 with the VALU): within noise; nontemporal partial stores: the reduce 9.4 -> 12.5 us;
+  // profiles/r06_f2regs/sched, order, zfirst, nt.)
   for (int ci = 0; ci < nk; ++ci) {
 #if F2R_DIAG != 2
     mfma_chunk(sm + (ci & 1) * F2R_ABUF, hh, hl);
