@@ -33,18 +33,20 @@ struct RedTask {
 constexpr int MAX_TASKS = 20;
 // torch.optim.Adam (single-tensor path) on element i: exp_avg.lerp_(g, 1-b1); exp_avg_sq =
 // b2*v + (1-b2)*g*g; p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps).  Shared by
-// k_adam and the fused reduce so that both paths compute the same bits.
+// k_adam and the fused reduce so that both paths compute the same bits; every rounding is spelled out
+// (__fmul_rn / __fadd_rn / fmaf) so that no inlining context contracts them differently (an -fno-slp-vectorize
+// build fused m + w1 (g - m) into an fma in one kernel and not in the other, profiles/r06_noslp).
 struct AdamCo {
   float w1, b2, omb2, step_size, bc2_sqrt, eps;
 };
 __device__ __forceinline__ float adam_elem(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                            int64_t i, float gi, const AdamCo& c) {
-  const float mi = m[i] + c.w1 * (gi - m[i]);
-  const float vi = c.b2 * v[i] + c.omb2 * gi * gi;
+  const float mi = __fadd_rn(m[i], __fmul_rn(c.w1, __fsub_rn(gi, m[i])));
+  const float vi = fmaf(gi, __fmul_rn(c.omb2, gi), __fmul_rn(c.b2, v[i]));
   m[i] = mi;
   v[i] = vi;
-  const float denom = sqrtf(vi) / c.bc2_sqrt + c.eps;
-  const float pn = p[i] - c.step_size * (mi / denom);
+  const float denom = __fadd_rn(__fdiv_rn(sqrtf(vi), c.bc2_sqrt), c.eps);
+  const float pn = fmaf(-c.step_size, __fdiv_rn(mi, denom), p[i]);
   p[i] = pn;
   return pn;
 }
