@@ -1636,11 +1636,35 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2r(SfArgs g) {
   }
   __syncthreads();
   // (An interleave of 1 MFMA with 4-6 VALU and LDS reads by sched_group_barrier: 50 -> 51 us at c4;
-  // waves 0-3 MFMAs then production and 4-7 production then MFMAs, so that a SIMD's two waves overlap
-  // one's VALU with the other's MFMAs: 50 -> 60 us, 13 registers spilled from the second order's
-  // longer-lived operands; the next chunk's Z1 MFMAs issued ahead of the chunk's 48 (and interleaved
-  // 1 : 5 with the VALU): within noise; nontemporal partial stores: the reduce 9.4 -> 12.5 us;
-  // profiles/r06_f2regs/sched, order, zfirst, nt.)
+  // the opposite orders below before the -fno-slp-vectorize build: 50 -> 60 us, 13 registers spilled;
+  // the next chunk's Z1 MFMAs issued ahead of the chunk's 48 (and interleaved 1 : 5 with the VALU):
+  // within noise; nontemporal partial stores: the reduce 9.4 -> 12.5 us; profiles/r06_f2regs/sched,
+  // order, zfirst, nt.)
+  // At 16 columns of Xa (2 and 4 actions) waves 4-7 produce before their MFMAs and waves 0-3 after, so
+  // that each SIMD pairs one wave's production with the other's MFMAs (c4 F2 50.0 -> 47.6 µs, same box,
+  // profiles/r06_order); at KD = 32 that form spills 23 registers and is slower (c3 F2 60 -> 63 µs), so
+  // both halves keep the one order there.
+  if (KD == 16 && w >= 4) {
+    for (int ci = 0; ci < nk; ++ci) {
+      const bool counted = ci + 1 < nk;
+      const float s0 = counted ? pow2(-de.x) : 0.f, s1 = counted ? -pow2(-de.y) : 0.f;
+      h8 nh[2], nl[2];
+      store_dz(sm + ((ci + 1) & 1) * F2R_ABUF, s0, s1);
+      make_h1(nh, nl);
+      load_x(min(t0 + ci + 2, t1 - 1));
+      __builtin_amdgcn_sched_barrier(0);
+      load_dz(min(t0 + ci + 2, t1 - 1));
+#if F2R_DIAG != 2
+      mfma_chunk(sm + (ci & 1) * F2R_ABUF, hh, hl);
+#endif
+      barrier();
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        hh[s] = nh[s];
+        hl[s] = nl[s];
+      }
+    }
+  } else
   for (int ci = 0; ci < nk; ++ci) {
 #if F2R_DIAG != 2
     mfma_chunk(sm + (ci & 1) * F2R_ABUF, hh, hl);
