@@ -302,6 +302,10 @@ def kernel_timing(algo, torch, config="c2", reps=20):
     if "f1_total" in out:
         tf = flops_per_row("f1_total", D, H, A) * algo.mb / (out["f1_total"]["ms"] * 1e-3) / 1e12
         out["f1_total"].update({"tflops": tf, peak_name: tf / peak})
+        if f1_fused(desc):  # both nets' F1 phases = the fused kernel's launches
+            tf = flops_per_row("k_sf_f1", D, H, A) * algo.mb / (out["f1_total"]["ms"] * 1e-3) / 1e12
+            out["k_sf_f1"] = {"ms": out["f1_total"]["ms"], "tflops": tf, peak_name: tf / peak,
+                              "frac_fp32_mfma_peak": tf / FP32_MFMA_PEAK_TFLOPS}
     if algo.precision in ("sf16", "f16"):
         # in-pipeline: every kernel of full gradients launched back to back as the SGD step runs them,
         # HIP events between the launches (rlks_ppo_grad_profile): the durations rocprofv3 sees, which
@@ -310,7 +314,7 @@ def kernel_timing(algo, torch, config="c2", reps=20):
         _lib.call("rlks_ppo_grad_profile", desc, C.byref(algo.coeffs), algo.params.flat.data_ptr(), algo.dyn.data_ptr(),
                   algo.mbuf.data_ptr(), algo.mb, algo.grad.data_ptr(), None, algo.ws.data_ptr(), algo.ws.numel(), reps,
                   ms5, s.cuda_stream)
-        fused = bool(os.environ.get("RLKS_F1_FUSED"))
+        fused = f1_fused(desc)  # F1 as one kernel (the library's default up to 4 actions)
         f1 = ("k_sf_f1",) if fused else ("k_sf_fwd", "k_sf_bwd")
         pipe = {"k_sf_prep": ms5[0], f1[0]: ms5[1], **({} if fused else {"k_sf_bwd": ms5[2]}),
                 "k_sf_dw2": ms5[3], "k_reduce": ms5[4]}
@@ -517,6 +521,17 @@ def mfma_calibration(torch, sf16_tflops, products=3):
     return res
 
 
+def f1_fused(desc):
+    """Whether the library runs a whole split-fp16 gradient's F1 as one kernel (k_sf_f1).  An older
+    variant library (RLKS_LIB, A/B runs) without the query fused it only under RLKS_F1_FUSED."""
+    from rlks import _lib
+
+    lib = _lib.lib()
+    if hasattr(lib, "rlks_sf_f1_fused"):
+        return bool(lib.rlks_sf_f1_fused(desc))
+    return bool(os.environ.get("RLKS_F1_FUSED"))
+
+
 def pmc_traffic():
     """per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC summary, if any"""
     p = ROOT / "profiles" / "pmc_traffic.json"
@@ -721,7 +736,7 @@ def main():
                 # parameters read by the weight split, and Adam (p, m, v read + written, the gradient
                 # written and read): everything else is a hand-off between the step's own kernels
                 step = [k for k in ("k_sf_split", "k_sf_fwd", "k_sf_bwd", "k_sf_dw2", "k_reduce") if k in pmc]
-                if os.environ.get("RLKS_F1_FUSED") and "k_sf_f1" in pmc:
+                if "k_sf_f1" in kernels.get("pipeline", {}).get("ms", {}) and "k_sf_f1" in pmc:
                     step = [k for k in ("k_sf_split", "k_sf_f1", "k_sf_dw2", "k_reduce") if k in pmc]
                 moved = sum(pmc[k]["hbm_bytes_per_launch"] for k in step)
                 P = algo.params.padded

@@ -282,12 +282,17 @@ int rlks_ppo_grad_phases(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeff
 /* In-pipeline kernel timing of the split-fp16 gradient (bench.py roofline): `reps` full rlks_ppo_grad
  * passes on `stream` (after one untimed pass), each kernel launched with a start / stop event pair
  * (hipExtLaunchKernelGGL: the kernel's own duration, as rocprofv3 measures it); ms_out[6] = average ms
- * of the weight split (k_sf_split), F1a (k_sf_fwd; or the fused k_sf_f1 under RLKS_F1_FUSED), F1b
- * (k_sf_bwd; 0 when fused), F2 (k_sf_dw2) and the reduce (k_reduce), each less the event bracket's own
+ * of the weight split (k_sf_split), F1a (k_sf_fwd; or the fused k_sf_f1, see rlks_sf_f1_fused), F1b
+ * (k_sf_bwd; 0 when fused), F2 (k_sf_dw2r) and the reduce (k_reduce), each less the event bracket's own
  * cost, which ms_out[5] reports (the same bracket around an empty kernel).  Synchronises the stream. */
 int rlks_ppo_grad_profile(const rlks_mlp_desc* desc, const rlks_ppo_coeffs* coeffs, const float* params_dev,
                           const float* dyn_dev, const float* mb_dev, int rows, float* grad_dev, double* stats_dev,
                           void* workspace_dev, int64_t workspace_bytes, int reps, double* ms_out, void* stream);
+
+/* 1 if a whole split-fp16 gradient of this descriptor runs F1 as one kernel (k_sf_f1: the default up to
+ * 4 actions; RLKS_F1_FUSED=1 / RLKS_F1_SPLIT=1 in the environment force either form), else 0 (bench.py
+ * names the kernels it times and profiles by it).  Not a reference interface: build introspection. */
+int rlks_sf_f1_fused(const rlks_mlp_desc* desc);
 
 /* torch.optim.Adam step (lerp form of exp_avg, bias-corrected), in place on n floats */
 int rlks_adam_step(float* params_dev, const float* grad_dev, float* m_dev, float* v_dev, int64_t n,

@@ -906,10 +906,10 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
     a.n[net].b2 = P.b2; a.n[net].w3 = P.w3; a.n[net].b3 = P.b3;
   }
   // F1 (forward, loss, dZ2, dH1 -> dW1 / db1, dW3 / db3) per net; F2 (dW2, db2) for both.  F1 is the
-  // two kernels F1a, F1b; RLKS_F1_FUSED=1 runs the fused kernel for a whole one-rank gradient
-  // (rlks_ppo_grad, the fused-Adam SGD step) -- the multi-rank step keeps the two kernels in both its
-  // forms (one bucket, or F1b overlapping the all-reduce: part 1 / 2), so that those stay bit-identical
-  const bool fused_f1 = part == 0 && !(fa && !fa->apply) && sf_f1_fused();
+  // fused kernel for a whole gradient (part 0: rlks_ppo_grad, the fused-Adam SGD step, the multi-rank
+  // step's one-bucket form) where sf_f1_fused says so, else the two kernels F1a, F1b; the overlapped
+  // multi-rank form (part 1 / 2: F1b under the all-reduce) always runs the two
+  const bool fused_f1 = part == 0 && sf_f1_fused(A);
   if (f_pi || f_vf) {
     const int net0 = f_pi ? 0 : 1, nets = (f_pi && f_vf) ? 2 : 1;
     if (fused_f1 || part != 0) {
@@ -1064,6 +1064,11 @@ int rlks_ppo_grad_phases(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, cons
   return RLKS_OK;
 }
 
+int rlks_sf_f1_fused(const rlks_mlp_desc* d) {
+  if (!d || !is_sf(d) || is_wide(d)) return 0;
+  return sf_f1_fused(d->n_actions) ? 1 : 0;
+}
+
 int rlks_ppo_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const float* params, const float* dyn,
                   const float* mb, int M, float* grad, double* stats, void* workspace, int64_t ws_bytes,
                   void* stream) {
@@ -1093,6 +1098,7 @@ int rlks_ppo_grad_profile(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, con
     for (int k = 0; k < KEV_N; ++k) {
       float ms = 0.f;
       if (hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]) == hipSuccess) ms_out[k] += ms / reps;
+      else (void)hipGetLastError();  // (an unrecorded pair: clear the error before the next pass's launch checks)
     }
   }
   g_kernel_events = nullptr;

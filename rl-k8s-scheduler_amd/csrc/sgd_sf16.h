@@ -119,8 +119,9 @@ bool sf_f2_regs();
 // F1's partials per net (one per F1 workgroup): dW1 / db1, and dW3 / db3 / stats; the workspace holds
 // the split kernels' count (the larger), the fused kernel writes half as many
 int sf_f1_parts(int M, bool fused);
-// whether a one-rank gradient runs the fused kernel (opt-in: RLKS_F1_FUSED set; measured no faster
-// than the two kernels)
-bool sf_f1_fused();
+// whether a whole gradient (part 0: one rank, or the multi-rank step's one-bucket form) runs the fused
+// F1 kernel at A actions: by default up to 4 actions; RLKS_F1_FUSED=1 / RLKS_F1_SPLIT=1 force it
+// 
+bool sf_f1_fused(int A);
 
 }  // namespace rlks

@@ -906,7 +906,15 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 }
 
 int sf_f1_parts(int M, bool fused) { return M / (16 * (fused ? SF_F1F_W : SF_F1_W)); }
-bool sf_f1_fused() { return getenv("RLKS_F1_FUSED") != nullptr; }
+// F1a + F1b as one kernel (k_sf_f1) for a whole gradient by default at up to 4 actions (16 columns of
+// Xa): with F2 = k_sf_dw2r and the no-SLP build it is the faster form there (c4 +1.3-2.1%, three same-box
+// alternations, profiles/r06_fusedab); at 8 actions the two kernels stay (c3 -0.2 to -3.9% fused).
+// RLKS_F1_FUSED=1 / RLKS_F1_SPLIT=1 force either form (A/B runs, the tests' references).
+bool sf_f1_fused(int A) {
+  if (getenv("RLKS_F1_FUSED")) return true;
+  if (getenv("RLKS_F1_SPLIT")) return false;
+  return A <= 4;
+}
 
 // FUSED (k_sf_f1: right after f1a_body in the same workgroup): the tile's dZ2 exponent arrives in a
 // register (edz_in), and the W1a planes F1a staged are still in LDS when its epilogue slots stopped
@@ -1065,13 +1073,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   else f1b_body<1, KD, ND, W, P>(g, ng.y);
 }
 
-// F1 fused (opt-in, RLKS_F1_FUSED=1): F1a then F1b on the same 16-row tiles in one
+// F1 fused (the default up to 4 actions, sf_f1_fused): F1a then F1b on the same 16-row tiles in one
 // workgroup.  The dZ2 hand-off is still written for F2, but F1b reads each lane's own fragments back
 // right after they were written (from the XCD's L2, not HBM), the tile exponent stays in a register,
 // the W1a planes stay in LDS (up to 4 actions), and there is one launch boundary less per SGD step.
 // Launched with 16-wave workgroups, one per CU (SF_F1F_W): with two 8-wave workgroups per CU in
 // different phases a few policy tiles a step came out different from run to run (cause not isolated).
-// Measured no faster than the two kernels (126-128 µs against 126 µs for the pair at c4).
+// Measured no faster than the two kernels on round 6's first trees (126-128 µs against 126 µs for the
+// pair at c4); faster end to end with k_sf_dw2r and the no-SLP build (profiles/r06_fusedab).
 template <int A_, int KD, int W>
 constexpr bool f1_w1_kept() {  // F1a's epilogue slots end before the W1a planes (sW1 = 4 H16 halves in)
   return W * (A_ - 1 > 1 ? A_ - 1 : 1) * HID * 4 + W * (A_ + 4) * 4 <= 4 * H16 * 2;

@@ -129,6 +129,7 @@ SIGNATURES = {
     "rlks_ppo_grad": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _P],
     "rlks_ppo_grad_phases": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _I, _P],
     "rlks_ppo_grad_profile": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _I64, _I, _P, _P],
+    "rlks_sf_f1_fused": [C.POINTER(MlpDesc)],
     "rlks_adam_step": [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _I, _P],
     "rlks_ppo_sgd_step": [C.POINTER(MlpDesc), C.POINTER(PpoCoeffs), _P, _P, _P, _I, _P, _P, _P, _P, _I64, _F, _F, _F,
                           _F, _I, _I, _P, _I64, _P],
@@ -150,6 +151,9 @@ class RlksError(RuntimeError):
 
 
 _lib = None
+# entry points an older variant library (RLKS_LIB, same-box A/B runs) may lack: diagnostics and build
+# introspection, never compute.  The product library must export all of them (tests/test_abi_host.py)
+_OPTIONAL = {n for n in SIGNATURES if n.startswith("rlks_debug_")} | {"rlks_sf_f1_fused"}
 
 
 def _warn_if_stale() -> None:
@@ -178,8 +182,8 @@ def lib() -> C.CDLL:
         _warn_if_stale()
         handle = C.CDLL(str(LIB_PATH))
         for name, argtypes in SIGNATURES.items():
-            if name.startswith("rlks_debug_") and not hasattr(handle, name):
-                continue  # diagnostics entry points of later builds (an older variant library for A/B runs)
+            if name in _OPTIONAL and "RLKS_LIB" in os.environ and not hasattr(handle, name):
+                continue  # entry points of later builds, absent from an older variant library (A/B runs)
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = _RESTYPES.get(name, C.c_int)

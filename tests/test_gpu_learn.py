@@ -444,9 +444,9 @@ def test_fused_sgd_step_equals_grad_then_adam(A, f1, monkeypatch):
     its slots) and the multi-rank pair rlks_ppo_grad_step + rlks_ppo_adam_apply (an all-reduce goes
     between them) give the parameters, Adam moments and gradients of rlks_ppo_grad + rlks_adam_step,
     bit for bit, over consecutive steps -- including a first step that claims prev_fused with no
-    fused predecessor (the device-side tag check falls back to scanning the weights).  f1 = "fused":
-    the one-rank step and rlks_ppo_grad run the fused F1 kernel (RLKS_F1_FUSED=1) while the
-    multi-rank pair always runs the two F1 kernels, so its reference is then rlks_ppo_grad without it"""
+    fused predecessor (the device-side tag check falls back to scanning the weights).  f1 = "fused" /
+    "split": every call runs the fused F1 kernel (RLKS_F1_FUSED=1) / the two F1 kernels
+    (RLKS_F1_SPLIT=1; by default the library fuses them up to 4 actions)"""
     from rlks import _lib
     from rlks.policy import PolicyParams
 
@@ -476,8 +476,7 @@ def test_fused_sgd_step_equals_grad_then_adam(A, f1, monkeypatch):
     stats_ref = torch.zeros(8, dtype=torch.float64, device=d)
     stats_fus = torch.zeros(8, dtype=torch.float64, device=d)
     stats_spl = torch.zeros(8, dtype=torch.float64, device=d)
-    if f1 == "fused":
-        monkeypatch.setenv("RLKS_F1_FUSED", "1")
+    monkeypatch.setenv("RLKS_F1_FUSED" if f1 == "fused" else "RLKS_F1_SPLIT", "1")
     for step in range(1, 6):
         mb = torch.zeros(M, stride, device=d)
         mb[:, :D] = torch.rand(M, D, generator=g, device=d)
@@ -490,12 +489,8 @@ def test_fused_sgd_step_equals_grad_then_adam(A, f1, monkeypatch):
                   st["g_ref"].data_ptr(), stats_ref.data_ptr(), ws_ref.data_ptr(), ws_ref.numel(), None)
         _lib.call("rlks_adam_step", p_ref.flat.data_ptr(), st["g_ref"].data_ptr(), st["m_ref"].data_ptr(),
                   st["v_ref"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, None)
-        monkeypatch.delenv("RLKS_F1_FUSED", raising=False)
         _lib.call("rlks_ppo_grad", C.byref(desc), C.byref(co), p_rs.flat.data_ptr(), dyn.data_ptr(), mb.data_ptr(), M,
                   st["g_rs"].data_ptr(), stats_rs.data_ptr(), ws_rs.data_ptr(), ws_rs.numel(), None)
-        torch.cuda.synchronize()
-        if f1 == "fused":
-            monkeypatch.setenv("RLKS_F1_FUSED", "1")
         _lib.call("rlks_adam_step", p_rs.flat.data_ptr(), st["g_rs"].data_ptr(), st["m_rs"].data_ptr(),
                   st["v_rs"].data_ptr(), P, 3e-3, 0.9, 0.999, 1e-8, step, None)
         _lib.call("rlks_ppo_sgd_step", C.byref(desc), C.byref(co), p_fus.flat.data_ptr(), dyn.data_ptr(),
@@ -677,10 +672,10 @@ def test_ppo_iteration_parity_and_surface(tmp_path):
 
 @pytest.mark.parametrize("A", [2, 4, 8])
 def test_fused_f1_is_deterministic_and_matches_split_kernels(A, monkeypatch):
-    """F1a + F1b as one kernel (k_sf_f1, 16-wave workgroups, one per CU; opt-in,
-    RLKS_F1_FUSED=1: measured no faster than the two kernels).  At the c4 minibatch (65,536 rows: two
+    """F1a + F1b as one kernel (k_sf_f1, 16-wave workgroups, one per CU; the
+    default up to 4 actions, RLKS_F1_FUSED=1 forces it).  At the c4 minibatch (65,536 rows: two
     rounds of workgroups) three runs are bit for bit the same, and the gradient equals the two split
-    kernels' (8-wave workgroups, the default) up to the order of the workgroup sums (16 waves' slots
+    kernels' (8-wave workgroups, RLKS_F1_SPLIT=1) up to the order of the workgroup sums (16 waves' slots
     added in LDS instead of 8, and half as many partials).  (The fused kernel on 8-wave workgroups, two per CU, was measured
     non-deterministic in a few tiles a step: DESIGN.md §15.)"""
     from rlks import _lib
@@ -706,7 +701,9 @@ def test_fused_f1_is_deterministic_and_matches_split_kernels(A, monkeypatch):
         torch.cuda.synchronize()
         return g.cpu().numpy(), st.cpu().numpy()
 
+    monkeypatch.setenv("RLKS_F1_SPLIT", "1")
     gs, ss = grad()
+    monkeypatch.delenv("RLKS_F1_SPLIT")
     monkeypatch.setenv("RLKS_F1_FUSED", "1")
     runs = [grad() for _ in range(3)]
     for gf, sf in runs[1:]:

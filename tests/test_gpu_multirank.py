@@ -91,8 +91,11 @@ def test_overlapped_allreduce_is_bit_identical(tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     N, T, mb, epochs, iters, world = 512, 64, 4096, 2, 2, 2
-    on = _run_ranks(tmp_path / "on", N, T, mb, epochs, iters, world, overlap=1)
-    off = _run_ranks(tmp_path / "off", N, T, mb, epochs, iters, world, overlap=0)
+    # (both forms on the two F1 kernels: the overlapped form always runs them, the one-bucket form by
+    # default runs the fused F1 at 2 actions, whose workgroup sums add in another order)
+    split = {"RLKS_F1_SPLIT": "1"}
+    on = _run_ranks(tmp_path / "on", N, T, mb, epochs, iters, world, overlap=1, extra_env=split)
+    off = _run_ranks(tmp_path / "off", N, T, mb, epochs, iters, world, overlap=0, extra_env=split)
     for r in range(world):
         assert np.array_equal(on[r]["params"].view(np.int32), off[r]["params"].view(np.int32)), r
         assert float(on[r]["kl_coeff"]) == float(off[r]["kl_coeff"])
@@ -127,7 +130,7 @@ def test_bench_launches_two_ranks(tmp_path):
 
 
 @pytest.mark.parametrize("overlap", [1, 0])
-def test_one_rank_rccl_multirank_path_equals_one_rank(tmp_path, overlap):
+def test_one_rank_rccl_multirank_path_equals_one_rank(tmp_path, overlap, monkeypatch):
     """RCCL on hardware with one GPU: a one-rank RCCL process group with RLKS_DDP_FORCE=1 takes the
     multi-rank SGD step (gradient -> RCCL all-reduce -> Adam; overlap=1: the two-bucket all-reduce on
     RCCL's stream under F1b) with every collective issued, exactly the calls of the 8-GPU run.  A
@@ -138,8 +141,11 @@ def test_one_rank_rccl_multirank_path_equals_one_rank(tmp_path, overlap):
     from rlks.ppo import PPO, PPOConfig
 
     N, T, mb, epochs, iters = 1024, 64, 8192, 2, 2
-    (z,) = _run_ranks(tmp_path, N, T, mb, epochs, iters, 1, overlap=overlap,
-                      extra_env={"RLKS_DIST_BACKEND": "nccl", "RLKS_DDP_FORCE": "1"})
+    env = {"RLKS_DIST_BACKEND": "nccl", "RLKS_DDP_FORCE": "1"}
+    if overlap:  # the overlapped form runs the two F1 kernels: so does the one-rank reference here
+        env["RLKS_F1_SPLIT"] = "1"
+        monkeypatch.setenv("RLKS_F1_SPLIT", "1")
+    (z,) = _run_ranks(tmp_path, N, T, mb, epochs, iters, 1, overlap=overlap, extra_env=env)
     prof = json.loads(str(z["allreduce"]))
     assert prof is not None and prof["backend"] == "nccl" and prof["overlapped"] == bool(overlap), prof
     print("one-rank RCCL all-reduce:", json.dumps(prof))
