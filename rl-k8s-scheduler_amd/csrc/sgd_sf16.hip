@@ -1913,11 +1913,8 @@ int launch_sf_f1(const SfArgs& a, int net0, int nets, int A, hipStream_t s, int 
 }
 
 bool sf_f2_regs() {
-  static const bool on = [] {
-    const char* e = getenv("RLKS_F2_IMAGE");
-    return !(e && e[0] == '1');
-  }();
-  return on;
+  const char* e = getenv("RLKS_F2_IMAGE");  // (read per call: tests switch it within a process)
+  return !(e && e[0] == '1');
 }
 
 int launch_sf_dw2(const SfArgs& a, int splits, hipStream_t s) {

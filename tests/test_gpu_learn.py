@@ -670,6 +670,45 @@ def test_ppo_iteration_parity_and_surface(tmp_path):
     assert algo2.compute_single_action(np.full(6, 0.5, np.float32), explore=False) == a0
 
 
+@pytest.mark.parametrize("A", [2, 8])
+def test_f2_image_kernel_matches_register_kernel(A, monkeypatch):
+    """Round 6's F2 (k_sf_dw2r: H1 in registers, [k / 4][n][4] partials, the default) and rounds 3-5's
+    (k_sf_dw2: H1 through an LDS image, [n][k] partials; RLKS_F2_IMAGE=1, kept for same-box A/B runs)
+    give the same gradient up to the MFMAs' operand roles (the same products, accumulated in another
+    order): every tensor within 1e-6 of its norm, dW2 / db2 included, and both are deterministic"""
+    from rlks import _lib
+    from rlks.policy import TENSOR_NAMES
+
+    d = _dev()
+    rows, D = 16384, 3 * A
+    p = _params(d, seed=rows + 7 * A, D=D, A=A)
+    p.desc.precision = _lib.RLKS_PRECISION_SF16
+    mb = _minibatch(rows, np.random.default_rng(rows + 3), D=D, A=A, p=p, d=d)
+    mbt = torch.from_numpy(mb).to(d)
+    dyn = torch.tensor([0.3, 0.7, 0.2, 1.0 / rows, 0, 0, 0, 0], dtype=torch.float32, device=d)
+    co = _lib.PpoCoeffs(0.3, 10.0, 1.0, 0.01)
+    wsb = C.c_int64()
+    _lib.call("rlks_ppo_workspace_bytes", C.byref(p.desc), rows, C.byref(wsb))
+    ws = torch.zeros(wsb.value, dtype=torch.uint8, device=d)
+
+    def grad():
+        g = torch.zeros(p.padded, device=d)
+        _lib.call("rlks_ppo_grad", C.byref(p.desc), C.byref(co), p.flat.data_ptr(), dyn.data_ptr(), mbt.data_ptr(),
+                  rows, g.data_ptr(), None, ws.data_ptr(), ws.numel(), None)
+        torch.cuda.synchronize()
+        return g.cpu().numpy()
+
+    gr = [grad(), grad()]
+    monkeypatch.setenv("RLKS_F2_IMAGE", "1")
+    gi = [grad(), grad()]
+    for a, b in (gr, gi):
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    for i, (name, _, _) in enumerate(TENSOR_NAMES):
+        o, n = p.offsets[i], int(np.prod(p.shapes[i]))
+        a, b = gi[0][o:o + n].astype(np.float64), gr[0][o:o + n].astype(np.float64)
+        assert np.linalg.norm(a - b) <= 1e-6 * np.linalg.norm(b) + 1e-12, name
+
+
 @pytest.mark.parametrize("A", [2, 4, 8])
 def test_fused_f1_is_deterministic_and_matches_split_kernels(A, monkeypatch):
     """F1a + F1b as one kernel (k_sf_f1, 16-wave workgroups, one per CU; the
