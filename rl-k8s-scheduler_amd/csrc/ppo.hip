@@ -483,6 +483,7 @@ struct SfWs {
   SfNet n[2];
   double* stat64;
   float* pmax_roll[2];  // the rollout's weight-max slots (the SGD steps' pmax keeps its parity state)
+  _Float16* xsp;        // F1a's Xa split for F2 (SfArgs::xsp)
   int64_t bytes, weight_bytes;
   int blocks, splits, tiles_per_split;
   int fa_parts;  // F1's dW3 / db3 / stats partials per net (the split kernels' count: the allocation)
@@ -538,6 +539,7 @@ static SfWs sf_ws_layout(int D, int A, int M, char* base) {
     n.part_b2 = (float*)take(4LL * w.splits * HID);
   }
   w.stat64 = (double*)take(8 * 8);
+  w.xsp = (_Float16*)take(2LL * 2 * M * KD);
   w.bytes = o;
   return w;
 }
@@ -898,7 +900,7 @@ static int sf_grad(const rlks_mlp_desc* d, const rlks_ppo_coeffs* co, const floa
   }
   SfArgs a{};
   a.x = mb; a.x_stride = mb_stride(D, A); a.M = M; a.D = D; a.A_pi = A;
-  a.tiles_per_split = w.tiles_per_split; a.co = *co; a.dyn = dyn;
+  a.tiles_per_split = w.tiles_per_split; a.co = *co; a.dyn = dyn; a.xsp = w.xsp;
   a.products = d->precision == RLKS_PRECISION_F16 ? 1 : 3;
   for (int net = 0; net < 2; ++net) {
     a.n[net] = w.n[net];

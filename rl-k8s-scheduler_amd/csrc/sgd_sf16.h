@@ -68,6 +68,8 @@ struct SfArgs {
   int tiles_per_split;
   int net0;  // F1: first net of the grid (blockIdx.y + net0)
   int products;  // MFMA products per split product: 1 = RLKS_PRECISION_F16 (hi hi), else 3 (fp32-accurate)
+  _Float16* xsp;  // [2 hi, lo][M][KD]: Xa = [X | 1 | 0] of every row split by F1a at its 16-row tile's
+                  // exponent and sign (tile_ex, tile_sign), written by the policy net's F1a, read by F2
   rlks_ppo_coeffs co;
   const float* dyn;
 };

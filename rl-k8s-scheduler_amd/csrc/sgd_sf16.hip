@@ -670,6 +670,12 @@ __device__ __forceinline__ int f1a_body(const SfArgs& g, int grp) {
   h8 xh, xl;
   const float sgn = tile_sign(tile);
   const int ex = x_split(xv, xh, xl, sgn);
+  if ((NET == 0 || g.net0 == 1) && 8 * gq < KD) {  // the rows' Xa split for F2: by the policy net (both
+                                                    // nets split the same rows alike), or the value net alone
+    _Float16* xo = g.xsp + (size_t)(row0 + c) * KD + 8 * gq;
+    *reinterpret_cast<h8*>(xo) = xh;
+    *reinterpret_cast<h8*>(xo + (size_t)g.M * KD) = xl;
+  }
   const float k_z1 = sgn * N.sc[1] * pow2(-ex) * SF_2LOG2E;  // Z1 accumulator -> 2 log2(e) Z1
   const float h1s = sgn * SF_H1_SCALE;                        // H1 enters Z2's products as sgn 2^14 H1
   vm_drain();
@@ -1490,7 +1496,6 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2r(SfArgs g) {
   _Float16* sm = reinterpret_cast<_Float16*>(lds);  // [2 buf][F2R_ABUF]
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = l & 15, gq = l >> 4, r = l & 31, h = l >> 5;
-  const int D = g.D, stride = g.x_stride;
   int t0 = blockIdx.x * g.tiles_per_split, t1 = t0 + g.tiles_per_split;
   if (!dcheck(t1 <= g.M / 32, DC_SGD_TILE, t1)) t0 = t1 = 0;
   const int nk = t1 - t0;
@@ -1577,52 +1582,45 @@ __global__ __launch_bounds__(F2_THREADS) void k_sf_dw2r(SfArgs g) {
   };
   if constexpr (KB <= 2) load_w1();
   const float inv_w1 = N.sc[1];
-  v4f xr[KB];
+  // the chunk's Xa rows as F1a split them (SfArgs::xsp: tile 2t + s at 2^e_T and sign (-1)^s): lane row
+  // r, columns 8 kb + 4 h + 0..3, the Z1 MFMA's A fragment as loaded (no split here)
+  h4 xrh[KB], xrl[KB];
   int2 xe, de;
-  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.x), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(g.xsp, (short)0, 0x7fffffff, 0x00020000);
+  const int xlo = 2 * g.M * KD;  // bytes from the hi plane to the lo plane
   auto load_x = [&](int t) {
     xe = *reinterpret_cast<const int2*>(sEx + 2 * (t - t0));
     de = *reinterpret_cast<const int2*>(sEd + 2 * (t - t0));
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-      const int base = 8 * kb + 4 * h, pb = base < stride - 4 ? base : stride - 4;
-      xr[kb] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(x_rsrc, 4 * (r * stride + pb), 4 * t * 32 * stride, 0));
+      const int off = 2 * (r * KD + 8 * kb + 4 * h);
+      xrh[kb] = __builtin_bit_cast(h4, __builtin_amdgcn_raw_buffer_load_b64(x_rsrc, off, 2 * t * 32 * KD, 0));
+      xrl[kb] = __builtin_bit_cast(h4, __builtin_amdgcn_raw_buffer_load_b64(x_rsrc, off + xlo, 2 * t * 32 * KD, 0));
     }
   };
   auto make_h1 = [&](h8 (&hh)[2], h8 (&hl)[2]) {
     if constexpr (KB > 2) load_w1();
-    const int ex = min(xe.x, xe.y);
-    const float sx = ssgn * pow2(ex), k_z1 = ssgn * inv_w1 * pow2(-ex) * SF_2LOG2E;
     f32x16 z;
 #pragma unroll
     for (int q = 0; q < 16; ++q) z[q] = 0.f;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-      const int base = 8 * kb + 4 * h;
-      const bool inrow = base < stride - 4;
-      h4 xh, xl;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int d = base + j;
-        _Float16 a, b;
-        split1(fmaf(xr[kb][j], (d < D && inrow) ? sx : 0.f, d == D ? sx : 0.f), a, b);
-        xh[j] = a;
-        xl[j] = b;
-      }
       if constexpr (P != 1) {
-        z = __builtin_amdgcn_mfma_f32_32x32x8f16(xl, wh[kb], z, 0, 0, 0);
-        z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wl[kb], z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_32x32x8f16(xrl[kb], wh[kb], z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_32x32x8f16(xrh[kb], wl[kb], z, 0, 0, 0);
       }
-      z = __builtin_amdgcn_mfma_f32_32x32x8f16(xh, wh[kb], z, 0, 0, 0);
+      z = __builtin_amdgcn_mfma_f32_32x32x8f16(xrh[kb], wh[kb], z, 0, 0, 0);
     }
-    // k-step s = rows of tile 2t + s: H1 at 2^(14 + E - e_T) (the odd tile arrives negated: -hs1)
+    // k-step s = rows of tile 2t + s: Z1 unscaled by that tile's X exponent and sign; H1 at
+    // 2^(14 + E - e_T) (the odd tile's dZ2 arrives negated: -hs1), times this split's sign
+    const float kz0 = inv_w1 * pow2(-xe.x) * SF_2LOG2E, kz1 = -inv_w1 * pow2(-xe.y) * SF_2LOG2E;
     const float hs0 = ssgn * pow2(14 + E - de.x), hs1 = -ssgn * pow2(14 + E - de.y);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const float hs = s ? hs1 : hs0;
+      const float hs = s ? hs1 : hs0, kz = s ? kz1 : kz0;
       float x[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = fmaf(-2.f * hs, tanh_r(z[8 * s + j] * k_z1), hs);
+      for (int j = 0; j < 8; ++j) x[j] = fmaf(-2.f * hs, tanh_r(z[8 * s + j] * kz), hs);
       split8v(x, hh[s], hl[s]);
     }
   };
